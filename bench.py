@@ -1,0 +1,204 @@
+#!/usr/bin/env python3
+"""bench.py -- assembled DoFs/s of the SWIPDG global stiffness (BASELINE.json metric) on MI355X.
+
+Workload (BASELINE.json configs[1]): SPE10 model1, SWIPDG p=1 on a Kuhn-triangulated
+3200 x 640 grid over [0,5]x[0,1] (ALUConform-like simplices): 4,096,000 triangles, 12,288,000 DoFs,
+147,386,880 nnz; A = k_cell I on the 100x20 Model1 checkerboard with a SYNTHETIC permeability
+(perm_case1.dat is absent: log10 k ~ U(-3,3), seed 10), diffusion factor 1, AllDirichlet.
+
+A "step" = one assembly of the global stiffness values (Q+1 = 1 value array) on the pre-built pattern, from
+mesh + coefficient arrays resident in HBM (the reference times the same region: SWIPDG::init()'s walk, the
+pattern being built in the constructor, swipdg.hh:169, 216-217, 485-486).
+
+Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): weak scaling, block-SWIPDG strip
+partition -- rank r owns the r-th 3200 x 640 strip of a (3200 N) x 640 grid over [0,5N]x[0,1] (the
+checkerboard widened to 100N x 20 cells) and assembles its own rows (owner-computes, no reduction); the
+face-halo records (vertex coordinates + tensor of the ghost elements) are exchanged with RCCL send/recv
+inside every step.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "dune-hdd_amd", "python"))
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--nx", type=int, default=3200, help="squares per strip in x (per rank)")
+    ap.add_argument("--ny", type=int, default=640)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU work of the baseline sample")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    return ap.parse_args()
+
+
+def cpu_baseline(nx_full, ny, target_s):
+    """The CPU oracle (single thread: the reference's walk() runs without TBB, swipdg.hh:485) timed on a
+    bounded strip of the same workload: nxs x ny Kuhn squares over [0, 5 nxs/nx_full] x [0,1]."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    perm = O.spe10_synthetic_permeability()
+    lower = (0.0, 0.0)
+
+    def run(nxs):
+        upper = (5.0 * nxs / nx_full, 1.0)
+        et, c, ev = O.kuhn_grid(nxs, ny, lower, upper)
+        # checkerboard of the FULL domain, evaluated at the strip's element centres
+        k = O.checkerboard(O.element_centers(c, ev), (0.0, 0.0), (5.0, 1.0), 100, 20, perm)
+        g = O.Grid(et, c, ev)
+        rp, col = g.pattern()
+        kap, ten, prm = O.scalar(O.FN_CONST, 1.0), O.tensor(O.TENSOR_ISO_PER_ELEM, per_elem=k), O.params()
+        O.assemble(g, kap, ten, prm, pattern=(rp, col))          # warm-up
+        ts = []
+        for _ in range(3):
+            t = time.perf_counter()
+            O.assemble(g, kap, ten, prm, pattern=(rp, col))
+            ts.append(time.perf_counter() - t)
+        return float(np.median(ts)), g.ne * 3
+
+    t_cal, _ = run(25)
+    nxs = int(min(nx_full, max(25, 25 * (target_s / 3.0) / max(t_cal, 1e-6))))
+    t, dofs = run(nxs)
+    return dict(value=dofs / t, unit="DoFs/s", cores=1, kind="port",
+                sample="CPU oracle (oracle/swipdg_oracle.c, sequential element walk + per-entry CSR binary "
+                       "search, 1 thread, median of 3 after 1 warm-up) on a %d x %d Kuhn strip = %d DoFs "
+                       "(%.2f s per assembly)" % (nxs, ny, dofs, t))
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    import hdd_amd as H
+    from hdd_amd.halo import HaloExchange, strip_owner
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit("--gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    nx, ny = args.nx * world, args.ny
+    lower, upper = (0.0, 0.0), (5.0 * world, 1.0)
+    grid = H.Grid.structured(H.SIMPLEX, nx, ny, lower, upper, px=world, py=1)
+    local = grid.local(rank, rank + 1)
+    rng = np.random.default_rng(10)
+    perm = 10.0 ** rng.uniform(-3.0, 3.0, size=100 * world * 20)     # == oracle synthetic field at world=1
+    kcell = local.checkerboard(lower, upper, 100 * world, 20, perm)
+    ctx = H.Context(local_rank)
+    dmesh = H.DeviceMesh(local, local_rank, zero_ghosts=world > 1)
+    tens = torch.from_numpy(kcell).cuda()
+    if world > 1:
+        tens[:local.own_begin] = 0
+        tens[local.own_end:] = 0
+    dpat = H.DevicePattern(local, local_rank)
+    kappa = [H.scalar_fn(H.FN_CONST, 1.0)]
+    tensor = H.tensor_fn(H.TENSOR_ISO_PER_ELEM, per_elem=tens)
+    vals = [torch.empty(dpat.nnz, dtype=torch.float64, device="cuda")]
+    halo = None
+    if world > 1:
+        halo = HaloExchange(ctx, local, [(dmesh.coords, dmesh.coords.shape[0]), (tens.view(1, -1), 1)],
+                            strip_owner(grid.n_sub, world), rank)
+
+    n_own = local.n_own
+    dofs_rank = 3 * n_own
+    nbr = local.neighbors[:, local.own_begin:local.own_end]
+    interior = nbr >= 0
+    owned_pair = interior & (nbr >= local.own_begin) & (nbr < local.own_end)
+    nif = int(owned_pair.sum()) // 2 + int((interior & ~owned_pair).sum())
+    qp1 = 1
+    alg_bytes = 8 * dpat.nnz * qp1 + n_own * (84 + 8 * qp1) + 12 * nif     # SURVEY.md 8(d) formula
+
+    stream = torch.cuda.current_stream()
+
+    def step(ev=None):
+        if halo is not None:
+            halo.exchange()
+        if ev is not None:
+            ev[0].record(stream)
+        H.assemble(ctx, dmesh, dpat, kappa, tensor, vals=vals)
+        if ev is not None:
+            ev[1].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(events[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
+    t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, kernel_ms_max = float(t[0]), float(t[1])
+    total_dofs = dofs_rank * world
+    value = total_dofs * args.steps / elapsed
+
+    if rank == 0:
+        achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
+        traffic = None
+        if os.path.exists(args.traffic_json):
+            try:
+                tj = json.load(open(args.traffic_json))
+                if tj.get("workload") == "spe10_swipdg_p1_kuhn_%dx%d" % (args.nx, args.ny):
+                    traffic = tj.get("hbm_bytes_per_launch")
+            except (OSError, ValueError):
+                traffic = None
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(args.nx, args.ny, args.cpu_seconds)
+        out = {
+            "metric": "assembled DoFs/sec (global stiffness), SPE10 SWIPDG p=1",
+            "value": value,
+            "unit": "DoFs/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": 1e3 * elapsed / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (SPE10 Model1 stand-in permeability: perm_case1.dat absent)",
+            "config": {"workload": "spe10_swipdg_p1_kuhn_%dx%d_per_gpu" % (args.nx, args.ny),
+                       "elements_per_gpu": n_own, "dofs_per_gpu": dofs_rank, "nnz_per_gpu": dpat.nnz,
+                       "total_dofs": total_dofs, "components": qp1,
+                       "parallelism": "block-swipdg strips x%d, owner-computes, RCCL face halo" % world
+                       if world > 1 else "single GPU"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "swipdg_assemble_kernel<Simplex,1,2,pwc>",
+                         "kernel_ms_avg": kernel_ms, "kernel_ms_avg_max_rank": kernel_ms_max,
+                         "algorithmic_bytes_per_launch": alg_bytes},
+            "cpu_baseline": cpu,
+        }
+        if halo is not None:
+            out["config"]["halo_bytes_per_step_rank0"] = halo.halo_bytes
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,638 @@
+// dune-hdd_amd/csrc/host/grid.cpp
+//
+// Host-side grids, rank-local views, halo plans and the sparsity pattern of the SWIPDG operator.
+//
+// Replaces, for the assembly hot path, the grid providers and patterns the reference builds on:
+//   - Stuff::Grid::Providers::Cube + globalRefine            (testcases/ESV2007.hh:123-129, spe10.hh:301-307)
+//   - grid::Multiscale::Providers::Cube with num_partitions   (testcases/base.hh:150-191)
+//   - EllipticSWIPDG::pattern(test, ansatz)                    (discretizations/swipdg.hh:169)
+//   - BlockSWIPDG add_local_to_global_pattern / compute_face_pattern (block-swipdg.hh:304-325, 1036-1049)
+//
+// Element numbering is subdomain-major (Spaces::Block::mapToGlobal(ss, ii) = offset(ss) + ii), subdomain
+// id = sx*py + sy so that vertical strips of subdomains are contiguous element ranges (one per rank).
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "hdd.h"
+#include "hdd_internal.hh"
+
+namespace hdd {
+
+// Dune reference elements: simplex faces 0:(0,1) 1:(0,2) 2:(1,2); cube faces 0:(0,2) 1:(1,3) 2:(0,1) 3:(2,3)
+static const int kSimplexFV[3][2] = {{0, 1}, {0, 2}, {1, 2}};
+static const int kCubeFV[4][2] = {{0, 2}, {1, 3}, {0, 1}, {2, 3}};
+
+static inline const int (*face_table(int et))[2] { return et == HDD_SIMPLEX ? kSimplexFV : kCubeFV; }
+static inline int nvpe_of(int et) { return et == HDD_SIMPLEX ? 3 : 4; }
+
+// numpy.linspace-compatible node coordinate (i*step + start, last node = stop)
+static inline double linspace_node(double a, double b, int64_t n, int64_t i)
+{
+  if (i == n) return b;
+  const double step = (b - a) / double(n);
+  return double(i) * step + a;
+}
+
+struct Grid {
+  virtual ~Grid() = default;
+  int elem_type = HDD_SIMPLEX, nvpe = 3, nf = 3, nb = 3;
+  int64_t ne = 0, nv = 0;
+  int32_t n_sub = 1;
+  std::vector<int64_t> sub_first;   // [n_sub+1] element ranges of the subdomains
+  virtual void vertices(int64_t g, int64_t* v) const = 0;
+  virtual void vertex_coord(int64_t v, double* xy) const = 0;
+  virtual int64_t neighbor(int64_t g, int f) const = 0;      // >= 0 element, else HDD_NBR_*
+  virtual uint32_t face_info(int64_t g) const = 0;
+  int32_t subdomain(int64_t g) const
+  {
+    return int32_t(std::upper_bound(sub_first.begin(), sub_first.end(), g) - sub_first.begin()) - 1;
+  }
+};
+
+// ------------------------------------------------------------------------------------------------
+// structured nx x ny squares (Kuhn split for simplices), px x py subdomains, implicit formulas
+// ------------------------------------------------------------------------------------------------
+struct StructuredGrid final : Grid {
+  hdd_structured_desc d{};
+  int ec = 1;                          // elements per square
+  std::vector<int64_t> cs, rs;         // first column / row of each subdomain column / row  [p+1]
+  std::vector<int64_t> sq_first;       // first square of each subdomain [n_sub+1]
+  int32_t bcode = HDD_NBR_DIRICHLET;
+
+  explicit StructuredGrid(const hdd_structured_desc& desc) : d(desc)
+  {
+    elem_type = d.elem_type;
+    nvpe = nvpe_of(elem_type);
+    nf = nvpe;
+    nb = nvpe;
+    ec = elem_type == HDD_SIMPLEX ? 2 : 1;
+    nv = int64_t(d.nx + 1) * (d.ny + 1);
+    ne = int64_t(d.nx) * d.ny * ec;
+    bcode = d.boundary == HDD_BOUNDARY_ALL_NEUMANN ? HDD_NBR_NEUMANN : HDD_NBR_DIRICHLET;
+    // square column i belongs to subdomain column floor(i*px/nx): first column of sx = ceil(sx*nx/px)
+    cs.resize(d.px + 1);
+    rs.resize(d.py + 1);
+    for (int s = 0; s <= d.px; ++s) cs[s] = (int64_t(s) * d.nx + d.px - 1) / d.px;
+    for (int s = 0; s <= d.py; ++s) rs[s] = (int64_t(s) * d.ny + d.py - 1) / d.py;
+    n_sub = d.px * d.py;
+    sq_first.assign(n_sub + 1, 0);
+    for (int sx = 0; sx < d.px; ++sx)
+      for (int sy = 0; sy < d.py; ++sy) {
+        const int s = sx * d.py + sy;
+        sq_first[s + 1] = (cs[sx + 1] - cs[sx]) * (rs[sy + 1] - rs[sy]);
+      }
+    for (int s = 0; s < n_sub; ++s) sq_first[s + 1] += sq_first[s];
+    sub_first.resize(n_sub + 1);
+    for (int s = 0; s <= n_sub; ++s) sub_first[s] = sq_first[s] * ec;
+  }
+
+  int64_t square_id(int64_t i, int64_t j) const
+  {
+    const int64_t sx = (i * d.px) / d.nx, sy = (j * d.py) / d.ny;
+    const int64_t s = sx * d.py + sy;
+    const int64_t w = cs[sx + 1] - cs[sx];
+    return sq_first[s] + (j - rs[sy]) * w + (i - cs[sx]);
+  }
+
+  void square_of(int64_t sq, int64_t* i, int64_t* j) const
+  {
+    const int64_t s = int64_t(std::upper_bound(sq_first.begin(), sq_first.end(), sq) - sq_first.begin()) - 1;
+    const int64_t sx = s / d.py, sy = s % d.py;
+    const int64_t w = cs[sx + 1] - cs[sx];
+    const int64_t loc = sq - sq_first[s];
+    *i = cs[sx] + loc % w;
+    *j = rs[sy] + loc / w;
+  }
+
+  void vertices(int64_t g, int64_t* v) const override
+  {
+    int64_t i, j;
+    square_of(g / ec, &i, &j);
+    const int64_t v00 = j * (d.nx + 1) + i, v10 = v00 + 1, v01 = v00 + d.nx + 1, v11 = v01 + 1;
+    if (elem_type == HDD_CUBE) {
+      v[0] = v00; v[1] = v10; v[2] = v01; v[3] = v11;
+    } else if (g % 2 == 0) {   // createSimplexGrid permutation (x, y): v00, v10, v11
+      v[0] = v00; v[1] = v10; v[2] = v11;
+    } else {                   // permutation (y, x): v00, v01, v11
+      v[0] = v00; v[1] = v01; v[2] = v11;
+    }
+  }
+
+  void vertex_coord(int64_t v, double* xy) const override
+  {
+    const int64_t i = v % (d.nx + 1), j = v / (d.nx + 1);
+    xy[0] = linspace_node(d.lower[0], d.upper[0], d.nx, i);
+    xy[1] = linspace_node(d.lower[1], d.upper[1], d.ny, j);
+  }
+
+  int64_t elem_at(int64_t i, int64_t j, int t) const
+  {
+    if (i < 0 || j < 0 || i >= d.nx || j >= d.ny) return bcode;
+    return square_id(i, j) * ec + t;
+  }
+
+  int64_t neighbor(int64_t g, int f) const override
+  {
+    int64_t i, j;
+    square_of(g / ec, &i, &j);
+    if (elem_type == HDD_CUBE) {
+      switch (f) {
+        case 0: return elem_at(i - 1, j, 0);
+        case 1: return elem_at(i + 1, j, 0);
+        case 2: return elem_at(i, j - 1, 0);
+        default: return elem_at(i, j + 1, 0);
+      }
+    }
+    if (g % 2 == 0) {          // (v00, v10, v11): bottom, diagonal, right
+      switch (f) {
+        case 0: return elem_at(i, j - 1, 1);
+        case 1: return elem_at(i, j, 1);
+        default: return elem_at(i + 1, j, 1);
+      }
+    }
+    switch (f) {               // (v00, v01, v11): left, diagonal, top
+      case 0: return elem_at(i - 1, j, 0);
+      case 1: return elem_at(i, j, 0);
+      default: return elem_at(i, j + 1, 0);
+    }
+  }
+
+  uint32_t face_info(int64_t g) const override
+  {
+    // twin faces (no reversed orientation on structured grids)
+    if (elem_type == HDD_CUBE) return (1u << 0) | (0u << 4) | (3u << 8) | (2u << 12);
+    if (g % 2 == 0) return (2u << 0) | (1u << 4) | (0u << 8);
+    return (2u << 0) | (1u << 4) | (0u << 8);
+  }
+};
+
+// ------------------------------------------------------------------------------------------------
+// general conforming mesh from connectivity
+// ------------------------------------------------------------------------------------------------
+struct ExplicitGrid final : Grid {
+  std::vector<double> vc;       // [nv][2]
+  std::vector<int64_t> ev;      // [ne][nvpe] (renumbered elements)
+  std::vector<int64_t> nbr;     // [ne][nf]
+  std::vector<uint32_t> finfo;  // [ne]
+
+  void vertices(int64_t g, int64_t* v) const override
+  {
+    for (int k = 0; k < nvpe; ++k) v[k] = ev[g * nvpe + k];
+  }
+  void vertex_coord(int64_t v, double* xy) const override { xy[0] = vc[2 * v]; xy[1] = vc[2 * v + 1]; }
+  int64_t neighbor(int64_t g, int f) const override { return nbr[g * nf + f]; }
+  uint32_t face_info(int64_t g) const override { return finfo[g]; }
+};
+
+// ------------------------------------------------------------------------------------------------
+// rank-local view
+// ------------------------------------------------------------------------------------------------
+struct Local {
+  const Grid* g = nullptr;
+  int32_t s_begin = 0, s_end = 0;
+  int64_t g0 = 0, g1 = 0;               // owned global range
+  std::vector<int64_t> ghost_lo, ghost_hi;  // sorted global ids of ghosts below g0 / above g1
+  int64_t n_local() const { return int64_t(ghost_lo.size()) + (g1 - g0) + int64_t(ghost_hi.size()); }
+  int64_t own_begin() const { return int64_t(ghost_lo.size()); }
+  int64_t own_end() const { return own_begin() + (g1 - g0); }
+  int64_t global_of(int64_t l) const
+  {
+    const int64_t nlo = int64_t(ghost_lo.size());
+    if (l < nlo) return ghost_lo[l];
+    if (l < nlo + (g1 - g0)) return g0 + (l - nlo);
+    return ghost_hi[l - nlo - (g1 - g0)];
+  }
+  int64_t local_of(int64_t gid) const
+  {
+    if (gid >= g0 && gid < g1) return own_begin() + (gid - g0);
+    if (gid < g0) {
+      auto it = std::lower_bound(ghost_lo.begin(), ghost_lo.end(), gid);
+      return (it != ghost_lo.end() && *it == gid) ? int64_t(it - ghost_lo.begin()) : -1;
+    }
+    auto it = std::lower_bound(ghost_hi.begin(), ghost_hi.end(), gid);
+    return (it != ghost_hi.end() && *it == gid) ? own_end() + int64_t(it - ghost_hi.begin()) : -1;
+  }
+};
+
+}  // namespace hdd
+
+struct hdd_grid {
+  std::unique_ptr<hdd::Grid> impl;
+};
+struct hdd_local {
+  hdd::Local impl;
+};
+
+using namespace hdd;
+
+// ------------------------------------------------------------------------------------------------
+// C ABI
+// ------------------------------------------------------------------------------------------------
+extern "C" int hdd_grid_create_structured(const hdd_structured_desc* desc, hdd_grid** out)
+{
+  if (!desc || !out) return set_error(HDD_ERR_INVALID, "hdd_grid_create_structured: null argument");
+  if (desc->elem_type != HDD_SIMPLEX && desc->elem_type != HDD_CUBE)
+    return set_error(HDD_ERR_UNSUPPORTED, "hdd_grid_create_structured: unknown element type");
+  if (desc->nx < 1 || desc->ny < 1 || desc->px < 1 || desc->py < 1 || desc->px > desc->nx || desc->py > desc->ny)
+    return set_error(HDD_ERR_INVALID, "hdd_grid_create_structured: need 1 <= px <= nx and 1 <= py <= ny");
+  if (!(desc->upper[0] > desc->lower[0]) || !(desc->upper[1] > desc->lower[1]))
+    return set_error(HDD_ERR_INVALID, "hdd_grid_create_structured: empty domain");
+  const int64_t ne = int64_t(desc->nx) * desc->ny * (desc->elem_type == HDD_SIMPLEX ? 2 : 1);
+  if (ne > int64_t(INT32_MAX) / 4)
+    return set_error(HDD_ERR_RANGE, "hdd_grid_create_structured: too many elements for int32 DoF columns");
+  auto* g = new hdd_grid;
+  g->impl.reset(new StructuredGrid(*desc));
+  *out = g;
+  return HDD_OK;
+}
+
+extern "C" int hdd_grid_create_from_connectivity(int32_t elem_type, int64_t n_vertices, const double* vertex_coords,
+                                                 int64_t n_elements, const int32_t* elem_vert,
+                                                 const int32_t* subdomain, int32_t n_subdomains, int32_t boundary,
+                                                 hdd_grid** out)
+{
+  if (!vertex_coords || !elem_vert || !out || n_vertices <= 0 || n_elements <= 0)
+    return set_error(HDD_ERR_INVALID, "hdd_grid_create_from_connectivity: invalid argument");
+  if (elem_type != HDD_SIMPLEX && elem_type != HDD_CUBE)
+    return set_error(HDD_ERR_UNSUPPORTED, "hdd_grid_create_from_connectivity: unknown element type");
+  auto G = std::make_unique<ExplicitGrid>();
+  G->elem_type = elem_type;
+  G->nvpe = nvpe_of(elem_type);
+  G->nf = G->nvpe;
+  G->nb = G->nvpe;
+  G->nv = n_vertices;
+  G->ne = n_elements;
+  G->n_sub = subdomain ? n_subdomains : 1;
+  if (G->n_sub < 1) return set_error(HDD_ERR_INVALID, "hdd_grid_create_from_connectivity: n_subdomains < 1");
+  const int nvpe = G->nvpe, nf = G->nf;
+  // subdomain-major renumbering (stable)
+  std::vector<int64_t> order(n_elements);
+  G->sub_first.assign(G->n_sub + 1, 0);
+  for (int64_t e = 0; e < n_elements; ++e) {
+    const int32_t s = subdomain ? subdomain[e] : 0;
+    if (s < 0 || s >= G->n_sub) return set_error(HDD_ERR_RANGE, "hdd_grid_create_from_connectivity: bad subdomain");
+    G->sub_first[s + 1]++;
+  }
+  for (int s = 0; s < G->n_sub; ++s) G->sub_first[s + 1] += G->sub_first[s];
+  {
+    std::vector<int64_t> pos(G->sub_first.begin(), G->sub_first.end() - 1);
+    for (int64_t e = 0; e < n_elements; ++e) order[pos[subdomain ? subdomain[e] : 0]++] = e;  // new -> old
+  }
+  G->vc.assign(vertex_coords, vertex_coords + 2 * n_vertices);
+  G->ev.resize(n_elements * nvpe);
+  for (int64_t n = 0; n < n_elements; ++n)
+    for (int k = 0; k < nvpe; ++k) {
+      const int32_t v = elem_vert[order[n] * nvpe + k];
+      if (v < 0 || v >= n_vertices) return set_error(HDD_ERR_RANGE, "hdd_grid_create_from_connectivity: bad vertex");
+      G->ev[n * nvpe + k] = v;
+    }
+  // face matching by sorted (min vertex, max vertex) keys
+  struct Rec { int64_t a, b, ef; };
+  std::vector<Rec> rec(n_elements * nf);
+  const auto FV = face_table(elem_type);
+  for (int64_t e = 0; e < n_elements; ++e)
+    for (int f = 0; f < nf; ++f) {
+      int64_t a = G->ev[e * nvpe + FV[f][0]], b = G->ev[e * nvpe + FV[f][1]];
+      if (a > b) std::swap(a, b);
+      rec[e * nf + f] = {a, b, e * nf + f};
+    }
+  std::sort(rec.begin(), rec.end(), [](const Rec& x, const Rec& y) {
+    return x.a != y.a ? x.a < y.a : (x.b != y.b ? x.b < y.b : x.ef < y.ef);
+  });
+  const int64_t bcode = boundary == HDD_BOUNDARY_ALL_NEUMANN ? HDD_NBR_NEUMANN : HDD_NBR_DIRICHLET;
+  G->nbr.assign(n_elements * nf, bcode);
+  G->finfo.assign(n_elements, 0u);
+  for (size_t i = 0; i < rec.size();) {
+    size_t j = i + 1;
+    while (j < rec.size() && rec[j].a == rec[i].a && rec[j].b == rec[i].b) ++j;
+    if (j - i > 2) return set_error(HDD_ERR_INVALID, "hdd_grid_create_from_connectivity: non-manifold face");
+    if (j - i == 2) {
+      const int64_t p = rec[i].ef, q = rec[i + 1].ef;
+      const int64_t ep = p / nf, eq = q / nf;
+      const int fp = int(p % nf), fq = int(q % nf);
+      const bool rev = G->ev[ep * nvpe + FV[fp][0]] != G->ev[eq * nvpe + FV[fq][0]];
+      G->nbr[p] = eq;
+      G->nbr[q] = ep;
+      G->finfo[ep] |= (uint32_t(fq) | (rev ? 8u : 0u)) << (4 * fp);
+      G->finfo[eq] |= (uint32_t(fp) | (rev ? 8u : 0u)) << (4 * fq);
+    }
+    i = j;
+  }
+  auto* g = new hdd_grid;
+  g->impl = std::move(G);
+  *out = g;
+  return HDD_OK;
+}
+
+extern "C" void hdd_grid_destroy(hdd_grid* g) { delete g; }
+
+extern "C" int hdd_grid_get_info(const hdd_grid* g, hdd_grid_info* out)
+{
+  if (!g || !out) return set_error(HDD_ERR_INVALID, "hdd_grid_get_info: null argument");
+  const Grid& G = *g->impl;
+  out->elem_type = G.elem_type;
+  out->nb = G.nb;
+  out->nfaces = G.nf;
+  out->nvpe = G.nvpe;
+  out->n_elements = G.ne;
+  out->n_vertices = G.nv;
+  out->n_subdomains = G.n_sub;
+  out->pad = 0;
+  return HDD_OK;
+}
+
+extern "C" int hdd_grid_subdomain_range(const hdd_grid* g, int32_t s_begin, int32_t s_end, int64_t* first,
+                                        int64_t* last)
+{
+  if (!g || !first || !last) return set_error(HDD_ERR_INVALID, "hdd_grid_subdomain_range: null argument");
+  const Grid& G = *g->impl;
+  if (s_begin < 0 || s_end > G.n_sub || s_begin >= s_end)
+    return set_error(HDD_ERR_RANGE, "hdd_grid_subdomain_range: 0 <= s_begin < s_end <= num_subdomains violated");
+  *first = G.sub_first[s_begin];
+  *last = G.sub_first[s_end];
+  return HDD_OK;
+}
+
+extern "C" int hdd_grid_connectivity(const hdd_grid* g, double* vertex_coords, int32_t* elem_vert, int32_t* subdomain)
+{
+  if (!g) return set_error(HDD_ERR_INVALID, "hdd_grid_connectivity: null grid");
+  const Grid& G = *g->impl;
+  if (vertex_coords)
+    for (int64_t v = 0; v < G.nv; ++v) G.vertex_coord(v, vertex_coords + 2 * v);
+  int64_t vv[4];
+  for (int64_t e = 0; e < G.ne; ++e) {
+    if (elem_vert) {
+      G.vertices(e, vv);
+      for (int k = 0; k < G.nvpe; ++k) elem_vert[e * G.nvpe + k] = int32_t(vv[k]);
+    }
+    if (subdomain) subdomain[e] = G.subdomain(e);
+  }
+  return HDD_OK;
+}
+
+extern "C" int hdd_local_create(const hdd_grid* g, int32_t s_begin, int32_t s_end, hdd_local** out)
+{
+  if (!g || !out) return set_error(HDD_ERR_INVALID, "hdd_local_create: null argument");
+  const Grid& G = *g->impl;
+  if (s_begin < 0 || s_end > G.n_sub || s_begin >= s_end)
+    return set_error(HDD_ERR_RANGE, "hdd_local_create: 0 <= s_begin < s_end <= num_subdomains violated");
+  auto* l = new hdd_local;
+  Local& L = l->impl;
+  L.g = &G;
+  L.s_begin = s_begin;
+  L.s_end = s_end;
+  L.g0 = G.sub_first[s_begin];
+  L.g1 = G.sub_first[s_end];
+  for (int64_t e = L.g0; e < L.g1; ++e)
+    for (int f = 0; f < G.nf; ++f) {
+      const int64_t n = G.neighbor(e, f);
+      if (n < 0) continue;
+      if (n < L.g0) L.ghost_lo.push_back(n);
+      else if (n >= L.g1) L.ghost_hi.push_back(n);
+    }
+  for (auto* v : {&L.ghost_lo, &L.ghost_hi}) {
+    std::sort(v->begin(), v->end());
+    v->erase(std::unique(v->begin(), v->end()), v->end());
+  }
+  *out = l;
+  return HDD_OK;
+}
+
+extern "C" void hdd_local_destroy(hdd_local* l) { delete l; }
+
+extern "C" int hdd_local_get_info(const hdd_local* l, hdd_local_info* out)
+{
+  if (!l || !out) return set_error(HDD_ERR_INVALID, "hdd_local_get_info: null argument");
+  const Local& L = l->impl;
+  out->n_local = L.n_local();
+  out->own_begin = L.own_begin();
+  out->own_end = L.own_end();
+  out->n_ghost = int64_t(L.ghost_lo.size() + L.ghost_hi.size());
+  out->global_first = L.g0;
+  return HDD_OK;
+}
+
+extern "C" int hdd_local_fill(const hdd_local* l, double* coords, int32_t* neighbors, uint32_t* face_info,
+                              int64_t* global_id, int32_t* subdomain)
+{
+  if (!l) return set_error(HDD_ERR_INVALID, "hdd_local_fill: null local");
+  const Local& L = l->impl;
+  const Grid& G = *L.g;
+  const int64_t nl = L.n_local();
+  int64_t vv[4];
+  double xy[2];
+  for (int64_t e = 0; e < nl; ++e) {
+    const int64_t gid = L.global_of(e);
+    const bool owned = e >= L.own_begin() && e < L.own_end();
+    if (coords) {
+      G.vertices(gid, vv);
+      for (int k = 0; k < G.nvpe; ++k) {
+        G.vertex_coord(vv[k], xy);
+        coords[(2 * k) * nl + e] = xy[0];
+        coords[(2 * k + 1) * nl + e] = xy[1];
+      }
+    }
+    if (neighbors)
+      for (int f = 0; f < G.nf; ++f) {
+        int64_t v = -3;
+        if (owned) {
+          const int64_t n = G.neighbor(gid, f);
+          v = n >= 0 ? L.local_of(n) : n;
+          if (n >= 0 && v < 0) return set_error(HDD_ERR_INVALID, "hdd_local_fill: ghost missing (internal)");
+        }
+        neighbors[f * nl + e] = int32_t(v);
+      }
+    if (face_info) face_info[e] = owned ? G.face_info(gid) : 0u;
+    if (global_id) global_id[e] = gid;
+    if (subdomain) subdomain[e] = G.subdomain(gid);
+  }
+  return HDD_OK;
+}
+
+extern "C" int hdd_local_centers(const hdd_local* l, double* centers)
+{
+  if (!l || !centers) return set_error(HDD_ERR_INVALID, "hdd_local_centers: null argument");
+  const Local& L = l->impl;
+  const Grid& G = *L.g;
+  const int64_t nl = L.n_local();
+  int64_t vv[4];
+  double xy[2];
+  for (int64_t e = 0; e < nl; ++e) {
+    G.vertices(L.global_of(e), vv);
+    double sx = 0.0, sy = 0.0;
+    for (int k = 0; k < G.nvpe; ++k) {
+      G.vertex_coord(vv[k], xy);
+      sx += xy[0];
+      sy += xy[1];
+    }
+    centers[e] = sx / G.nvpe;
+    centers[nl + e] = sy / G.nvpe;
+  }
+  return HDD_OK;
+}
+
+static int ghost_owner(const Local& L, const int32_t* owner, int64_t gid)
+{
+  return owner[L.g->subdomain(gid)];
+}
+
+extern "C" int hdd_local_halo_plan(const hdd_local* l, const int32_t* owner, int32_t my_rank, int32_t* n_peers,
+                                   int32_t* peers, int64_t* send_count, int64_t* recv_offset, int64_t* recv_count)
+{
+  if (!l || !owner || !n_peers) return set_error(HDD_ERR_INVALID, "hdd_local_halo_plan: null argument");
+  const Local& L = l->impl;
+  const Grid& G = *L.g;
+  for (int32_t s = L.s_begin; s < L.s_end; ++s)
+    if (owner[s] != my_rank) return set_error(HDD_ERR_INVALID, "hdd_local_halo_plan: owned subdomain not mine");
+  // receive side: ghosts grouped by owner (contiguous because owners hold contiguous subdomain ranges)
+  std::vector<int32_t> pr;
+  std::vector<int64_t> roff, rcnt;
+  const int64_t nl = L.n_local();
+  for (int64_t e = 0; e < nl; ++e) {
+    if (e >= L.own_begin() && e < L.own_end()) continue;
+    const int r = ghost_owner(L, owner, L.global_of(e));
+    if (r == my_rank) return set_error(HDD_ERR_INVALID, "hdd_local_halo_plan: ghost owned by this rank");
+    if (!pr.empty() && pr.back() == r && roff.back() + rcnt.back() == e) {
+      rcnt.back()++;
+      continue;
+    }
+    if (std::find(pr.begin(), pr.end(), r) != pr.end())
+      return set_error(HDD_ERR_UNSUPPORTED, "hdd_local_halo_plan: ghosts of one owner are not contiguous");
+    pr.push_back(r);
+    roff.push_back(e);
+    rcnt.push_back(1);
+  }
+  // send side: owned elements with a face neighbour owned by the peer (the peer's ghosts, same order)
+  std::vector<int64_t> scnt(pr.size(), 0);
+  for (int64_t e = L.g0; e < L.g1; ++e) {
+    std::vector<int> seen;
+    for (int f = 0; f < G.nf; ++f) {
+      const int64_t n = G.neighbor(e, f);
+      if (n < 0 || (n >= L.g0 && n < L.g1)) continue;
+      const int r = ghost_owner(L, owner, n);
+      if (std::find(seen.begin(), seen.end(), r) != seen.end()) continue;
+      seen.push_back(r);
+      const auto it = std::find(pr.begin(), pr.end(), r);
+      scnt[it - pr.begin()]++;
+    }
+  }
+  // sort peers ascending (ghost groups already ascend with owner rank when ranks ascend with subdomains)
+  std::vector<size_t> idx(pr.size());
+  std::iota(idx.begin(), idx.end(), 0);
+  std::sort(idx.begin(), idx.end(), [&](size_t a, size_t b) { return pr[a] < pr[b]; });
+  *n_peers = int32_t(pr.size());
+  if (peers)
+    for (size_t k = 0; k < idx.size(); ++k) {
+      peers[k] = pr[idx[k]];
+      if (send_count) send_count[k] = scnt[idx[k]];
+      if (recv_offset) recv_offset[k] = roff[idx[k]];
+      if (recv_count) recv_count[k] = rcnt[idx[k]];
+    }
+  return HDD_OK;
+}
+
+extern "C" int hdd_local_send_list(const hdd_local* l, const int32_t* owner, int32_t my_rank, int32_t peer_index,
+                                   int32_t* local_ids)
+{
+  if (!l || !owner || !local_ids) return set_error(HDD_ERR_INVALID, "hdd_local_send_list: null argument");
+  int32_t np = 0;
+  int rc = hdd_local_halo_plan(l, owner, my_rank, &np, nullptr, nullptr, nullptr, nullptr);
+  if (rc) return rc;
+  if (peer_index < 0 || peer_index >= np) return set_error(HDD_ERR_RANGE, "hdd_local_send_list: bad peer index");
+  std::vector<int32_t> peers(np);
+  std::vector<int64_t> sc(np), ro(np), rcv(np);
+  rc = hdd_local_halo_plan(l, owner, my_rank, &np, peers.data(), sc.data(), ro.data(), rcv.data());
+  if (rc) return rc;
+  const int32_t peer = peers[peer_index];
+  const Local& L = l->impl;
+  const Grid& G = *L.g;
+  int64_t k = 0;
+  for (int64_t e = L.g0; e < L.g1; ++e)
+    for (int f = 0; f < G.nf; ++f) {
+      const int64_t n = G.neighbor(e, f);
+      if (n < 0 || (n >= L.g0 && n < L.g1)) continue;
+      if (ghost_owner(L, owner, n) == peer) {
+        local_ids[k++] = int32_t(L.local_of(e));
+        break;
+      }
+    }
+  return HDD_OK;
+}
+
+extern "C" int hdd_checkerboard(int64_t n, const double* centers, const double lower[2], const double upper[2],
+                                int32_t ncx, int32_t ncy, const double* cell_values, double* out)
+{
+  if (!centers || !lower || !upper || !cell_values || !out || ncx < 1 || ncy < 1)
+    return set_error(HDD_ERR_INVALID, "hdd_checkerboard: invalid argument");
+  for (int64_t e = 0; e < n; ++e) {
+    int64_t cx = int64_t((centers[e] - lower[0]) / (upper[0] - lower[0]) * ncx);
+    int64_t cy = int64_t((centers[n + e] - lower[1]) / (upper[1] - lower[1]) * ncy);
+    cx = std::min<int64_t>(std::max<int64_t>(cx, 0), ncx - 1);
+    cy = std::min<int64_t>(std::max<int64_t>(cy, 0), ncy - 1);
+    out[e] = cell_values[cy * ncx + cx];
+  }
+  return HDD_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+// pattern
+// ------------------------------------------------------------------------------------------------
+static int nb_of(int32_t et) { return et == HDD_SIMPLEX ? 3 : (et == HDD_CUBE ? 4 : 0); }
+
+extern "C" int hdd_pattern_count(int32_t elem_type, int64_t n_local, int64_t own_begin, int64_t own_end,
+                                 const int32_t* neighbors, int64_t* nnz)
+{
+  const int nb = nb_of(elem_type);
+  if (!nb) return set_error(HDD_ERR_UNSUPPORTED, "hdd_pattern_count: unknown element type");
+  if (!neighbors || !nnz || own_begin < 0 || own_end > n_local || own_begin > own_end)
+    return set_error(HDD_ERR_INVALID, "hdd_pattern_count: invalid argument");
+  const int nf = nb;
+  int64_t total = 0;
+  for (int64_t e = own_begin; e < own_end; ++e) {
+    int blocks = 1;
+    for (int f = 0; f < nf; ++f) blocks += neighbors[f * n_local + e] >= 0;
+    total += int64_t(nb) * nb * blocks;
+  }
+  *nnz = total;
+  return HDD_OK;
+}
+
+extern "C" int hdd_pattern_fill(int32_t elem_type, int64_t n_local, int64_t own_begin, int64_t own_end,
+                                const int32_t* neighbors, const int64_t* global_id, int64_t* row_ptr, int32_t* col,
+                                int64_t* elem_ptr)
+{
+  const int nb = nb_of(elem_type);
+  if (!nb) return set_error(HDD_ERR_UNSUPPORTED, "hdd_pattern_fill: unknown element type");
+  if (!neighbors || !row_ptr || !col || own_begin < 0 || own_end > n_local || own_begin > own_end)
+    return set_error(HDD_ERR_INVALID, "hdd_pattern_fill: invalid argument");
+  const int nf = nb;
+  int64_t off = 0;
+  row_ptr[0] = 0;
+  for (int64_t e = own_begin; e < own_end; ++e) {
+    const int64_t k = e - own_begin;
+    int64_t blk[5];
+    int nblk = 0;
+    blk[nblk++] = global_id ? global_id[e] : e;
+    for (int f = 0; f < nf; ++f) {
+      const int32_t n = neighbors[f * n_local + e];
+      if (n >= 0) {
+        if (n >= n_local) return set_error(HDD_ERR_RANGE, "hdd_pattern_fill: neighbour out of range");
+        blk[nblk++] = global_id ? global_id[n] : n;
+      }
+    }
+    std::sort(blk, blk + nblk);
+    if (elem_ptr) elem_ptr[k] = off;
+    for (int i = 0; i < nb; ++i) {
+      for (int b = 0; b < nblk; ++b)
+        for (int j = 0; j < nb; ++j) col[off++] = int32_t(blk[b] * nb + j);
+      row_ptr[k * nb + i + 1] = off;
+    }
+  }
+  if (elem_ptr) elem_ptr[own_end - own_begin] = off;
+  return HDD_OK;
+}

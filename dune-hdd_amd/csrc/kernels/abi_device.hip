@@ -1,0 +1,294 @@
+// dune-hdd_amd/csrc/kernels/abi_device.hip
+//
+// Device half of the C ABI: context, SWIPDG assembly dispatch, the theta-lincomb of affine components
+// (AffinelyDecomposedContainer::freeze_parameter, base.hh:338-341) and the SoA halo gather/scatter used
+// around the RCCL face-halo exchange of a sharded BlockSWIPDG.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+
+#include "hdd.h"
+#include "../host/hdd_internal.hh"
+#include "swipdg_kernels.hh"
+
+struct hdd_ctx {
+  int device = 0;
+};
+
+using hdd::set_error;
+
+static int hip_fail(hipError_t e, const char* where)
+{
+  return set_error(HDD_ERR_HIP, std::string(where) + ": " + hipGetErrorString(e));
+}
+
+extern "C" int hdd_ctx_create(int hip_device, hdd_ctx** out)
+{
+  if (!out) return set_error(HDD_ERR_INVALID, "hdd_ctx_create: null out");
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) return hip_fail(e, "hdd_ctx_create: hipGetDeviceCount");
+  if (hip_device < 0 || hip_device >= n) return set_error(HDD_ERR_RANGE, "hdd_ctx_create: no such HIP device");
+  e = hipSetDevice(hip_device);
+  if (e != hipSuccess) return hip_fail(e, "hdd_ctx_create: hipSetDevice");
+  auto* c = new hdd_ctx;
+  c->device = hip_device;
+  *out = c;
+  return HDD_OK;
+}
+
+extern "C" void hdd_ctx_destroy(hdd_ctx* ctx) { delete ctx; }
+
+static int fn_order(const hdd_scalar_fn& f) { return f.kind == HDD_FN_SINUSOID ? f.order : 0; }
+
+extern "C" int hdd_swipdg_assemble(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_fn* kappa, int32_t n_comp,
+                                   const hdd_tensor_fn* tensor, const hdd_swipdg_params* p, const hdd_csr* pattern,
+                                   double* const* d_vals, void* stream)
+{
+  using namespace hdd::dev;
+  if (!ctx || !m || !kappa || !tensor || !p || !pattern || !d_vals)
+    return set_error(HDD_ERR_INVALID, "hdd_swipdg_assemble: null argument");
+  if (n_comp < 1 || n_comp > HDD_MAX_COMP)
+    return set_error(HDD_ERR_INVALID, "hdd_swipdg_assemble: need 1 <= n_comp <= HDD_MAX_COMP");
+  if (m->elem_type != HDD_SIMPLEX && m->elem_type != HDD_CUBE)
+    return set_error(HDD_ERR_UNSUPPORTED, "hdd_swipdg_assemble: unknown element type");
+  if (!m->coords || !m->neighbors || !m->face_info || !pattern->elem_ptr)
+    return set_error(HDD_ERR_INVALID, "hdd_swipdg_assemble: mesh / pattern arrays missing");
+  if (m->own_begin < 0 || m->own_end > m->n_local || m->own_begin > m->own_end)
+    return set_error(HDD_ERR_RANGE, "hdd_swipdg_assemble: 0 <= own_begin <= own_end <= n_local violated");
+  if (m->n_local >= int64_t(INT32_MAX))
+    return set_error(HDD_ERR_RANGE, "hdd_swipdg_assemble: n_local must fit int32 neighbour ids");
+  const int nb = m->elem_type == HDD_SIMPLEX ? 3 : 4;
+  if (pattern->n_rows != int64_t(nb) * (m->own_end - m->own_begin))
+    return set_error(HDD_ERR_INVALID, "hdd_swipdg_assemble: pattern rows != nb * owned elements");
+  // The reference requires a non-parametric, non-empty tensor (swipdg.hh:173-176); here the tensor is a
+  // plain function, so only its kind is checked.
+  if (tensor->kind != HDD_TENSOR_CONST && tensor->kind != HDD_TENSOR_ISO_PER_ELEM &&
+      tensor->kind != HDD_TENSOR_SYM_PER_ELEM)
+    return set_error(HDD_ERR_UNSUPPORTED, "hdd_swipdg_assemble: unknown tensor kind");
+  if (tensor->kind != HDD_TENSOR_CONST && !tensor->per_elem)
+    return set_error(HDD_ERR_INVALID, "hdd_swipdg_assemble: tensor per_elem missing");
+  AssembleArgs a{};
+  a.elem_type = m->elem_type;
+  a.n_comp = n_comp;
+  a.n_local = m->n_local;
+  a.own_begin = m->own_begin;
+  a.own_end = m->own_end;
+  a.coords = m->coords;
+  a.nbrs = m->neighbors;
+  a.finfo = m->face_info;
+  a.elem_ptr = pattern->elem_ptr;
+  a.tkind = tensor->kind;
+  a.tc0 = tensor->c[0];
+  a.tc1 = tensor->c[1];
+  a.tc2 = tensor->c[2];
+  a.tper = tensor->per_elem;
+  a.sigma_inner = p->sigma_inner;
+  a.sigma_boundary = p->sigma_boundary;
+  a.beta = p->beta;
+  // integrand orders of LocalEvaluation::Elliptic / SWIPDG::Inner / BoundaryLHS at p = 1 (piecewise
+  // constant tensors): volume ord(kappa); faces ord(kappa) + 2.  One kernel serves components of equal
+  // order -- the caller splits mixed-order component sets.
+  const int ko = fn_order(kappa[0]);
+  for (int c = 0; c < n_comp; ++c) {
+    const hdd_scalar_fn& k = kappa[c];
+    if (k.kind != HDD_FN_CONST && k.kind != HDD_FN_PER_ELEM && k.kind != HDD_FN_SINUSOID)
+      return set_error(HDD_ERR_UNSUPPORTED, "hdd_swipdg_assemble: unknown diffusion factor kind");
+    if (k.kind == HDD_FN_PER_ELEM && !k.per_elem)
+      return set_error(HDD_ERR_INVALID, "hdd_swipdg_assemble: diffusion factor per_elem missing");
+    if (fn_order(k) != ko)
+      return set_error(HDD_ERR_UNSUPPORTED, "hdd_swipdg_assemble: components of different integration order");
+    if (!d_vals[c]) return set_error(HDD_ERR_INVALID, "hdd_swipdg_assemble: null value array");
+    a.kappa[c] = KappaArg{k.kind, k.order, k.c, k.b, k.kx, k.ky, k.per_elem};
+    a.vals[c] = d_vals[c];
+  }
+  const int vol_order = p->vol_order >= 0 ? p->vol_order : ko;
+  const int face_order = p->face_order >= 0 ? p->face_order : ko + 2;
+  const int nqv = volume_points(m->elem_type, vol_order);
+  const int nqf = face_points(face_order);
+  bool supported = false;
+  hipError_t e = hipSetDevice(ctx->device);
+  if (e != hipSuccess) return hip_fail(e, "hdd_swipdg_assemble: hipSetDevice");
+  e = launch_assemble(a, nqv, nqf, static_cast<hipStream_t>(stream), &supported);
+  if (!supported)
+    return set_error(HDD_ERR_UNSUPPORTED, "hdd_swipdg_assemble: no kernel for volume order " + std::to_string(vol_order) +
+                                              " / face order " + std::to_string(face_order));
+  if (e != hipSuccess) return hip_fail(e, "hdd_swipdg_assemble: launch");
+  return HDD_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+// theta-lincomb: out[s][k] = sum_q theta[s][q] v_q[k]; up to LC_S samples per launch, 2 values per lane
+// ------------------------------------------------------------------------------------------------
+namespace {
+constexpr int LC_S = 16;
+struct LincombArgs {
+  const double* v[HDD_MAX_COMP];
+  double theta[LC_S][HDD_MAX_COMP];
+  double* out;
+  int64_t nnz, stride;
+  int32_t n_comp, n_s;
+};
+
+__global__ void __launch_bounds__(256) lincomb_kernel(const LincombArgs a)
+{
+  const int64_t n2 = a.nnz >> 1;
+  for (int64_t k = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; k < n2; k += int64_t(gridDim.x) * blockDim.x) {
+    double2 v[HDD_MAX_COMP];
+#pragma unroll
+    for (int c = 0; c < HDD_MAX_COMP; ++c)
+      v[c] = c < a.n_comp ? reinterpret_cast<const double2*>(a.v[c])[k] : make_double2(0.0, 0.0);
+    for (int s = 0; s < a.n_s; ++s) {
+      double2 r = make_double2(0.0, 0.0);
+#pragma unroll
+      for (int c = 0; c < HDD_MAX_COMP; ++c) {
+        if (c < a.n_comp) {
+          r.x += a.theta[s][c] * v[c].x;
+          r.y += a.theta[s][c] * v[c].y;
+        }
+      }
+      __builtin_nontemporal_store(r.x, a.out + s * a.stride + 2 * k);
+      __builtin_nontemporal_store(r.y, a.out + s * a.stride + 2 * k + 1);
+    }
+  }
+  if ((a.nnz & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+    const int64_t k = a.nnz - 1;
+    for (int s = 0; s < a.n_s; ++s) {
+      double r = 0.0;
+      for (int c = 0; c < a.n_comp; ++c) r += a.theta[s][c] * a.v[c][k];
+      a.out[s * a.stride + k] = r;
+    }
+  }
+}
+}  // namespace
+
+extern "C" int hdd_affine_lincomb(hdd_ctx* ctx, int64_t nnz, const double* const* d_vals, int32_t n_comp,
+                                  const double* theta, int32_t n_samples, double* d_out, int64_t out_stride,
+                                  void* stream)
+{
+  if (!ctx || !d_vals || !theta || !d_out) return set_error(HDD_ERR_INVALID, "hdd_affine_lincomb: null argument");
+  if (n_comp < 1 || n_comp > HDD_MAX_COMP || n_samples < 0 || nnz < 0 || out_stride < nnz)
+    return set_error(HDD_ERR_INVALID, "hdd_affine_lincomb: invalid sizes");
+  bool aligned = true;
+  for (int c = 0; c < n_comp; ++c) aligned &= d_vals[c] && (reinterpret_cast<uintptr_t>(d_vals[c]) % 16 == 0);
+  aligned &= reinterpret_cast<uintptr_t>(d_out) % 16 == 0 && (out_stride % 2 == 0);
+  if (!aligned) return set_error(HDD_ERR_INVALID, "hdd_affine_lincomb: arrays must be 16-byte aligned, stride even");
+  hipError_t e = hipSetDevice(ctx->device);
+  if (e != hipSuccess) return hip_fail(e, "hdd_affine_lincomb: hipSetDevice");
+  const int64_t n2 = (nnz + 1) / 2;
+  const unsigned grid = unsigned(std::min<int64_t>(std::max<int64_t>((n2 + 255) / 256, 1), 256 * 16));
+  for (int s0 = 0; s0 < n_samples; s0 += LC_S) {
+    LincombArgs a{};
+    for (int c = 0; c < n_comp; ++c) a.v[c] = d_vals[c];
+    a.n_comp = n_comp;
+    a.n_s = std::min(LC_S, n_samples - s0);
+    for (int s = 0; s < a.n_s; ++s)
+      for (int c = 0; c < n_comp; ++c) a.theta[s][c] = theta[(s0 + s) * n_comp + c];
+    a.out = d_out + int64_t(s0) * out_stride;
+    a.nnz = nnz;
+    a.stride = out_stride;
+    hipLaunchKernelGGL(lincomb_kernel, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream), a);
+    e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "hdd_affine_lincomb: launch");
+  }
+  return HDD_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+// SoA gather / scatter of element columns (halo records)
+// ------------------------------------------------------------------------------------------------
+namespace {
+constexpr int SOA_MAX = 16;
+struct SoaArgs {
+  const double* src[SOA_MAX];
+  double* dst[SOA_MAX];
+  int32_t rows[SOA_MAX];
+  int32_t row_first[SOA_MAX + 1];
+  int32_t n_arrays;
+  int64_t ld, n, offset;
+  const int32_t* idx;
+  const double* buf_in;
+  double* buf_out;
+};
+
+__global__ void __launch_bounds__(256) soa_gather_kernel(const SoaArgs a)
+{
+  const int64_t total = int64_t(a.row_first[a.n_arrays]) * a.n;
+  for (int64_t t = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; t < total; t += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t r = t / a.n, i = t - r * a.n;
+    int arr = 0;
+    while (arr + 1 < a.n_arrays && a.row_first[arr + 1] <= r) ++arr;
+    const int64_t rr = r - a.row_first[arr];
+    a.buf_out[t] = a.src[arr][rr * a.ld + a.idx[i]];
+  }
+}
+
+__global__ void __launch_bounds__(256) soa_scatter_kernel(const SoaArgs a)
+{
+  const int64_t total = int64_t(a.row_first[a.n_arrays]) * a.n;
+  for (int64_t t = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; t < total; t += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t r = t / a.n, i = t - r * a.n;
+    int arr = 0;
+    while (arr + 1 < a.n_arrays && a.row_first[arr + 1] <= r) ++arr;
+    const int64_t rr = r - a.row_first[arr];
+    a.dst[arr][rr * a.ld + a.offset + i] = a.buf_in[t];
+  }
+}
+
+int soa_args(SoaArgs& a, const int32_t* rows, int32_t n_arrays, int64_t ld, int64_t n)
+{
+  if (n_arrays < 1 || n_arrays > SOA_MAX || !rows || ld < 0 || n < 0)
+    return set_error(HDD_ERR_INVALID, "hdd_soa_*: invalid sizes (1 <= n_arrays <= 16)");
+  a.n_arrays = n_arrays;
+  a.row_first[0] = 0;
+  for (int k = 0; k < n_arrays; ++k) {
+    if (rows[k] < 1) return set_error(HDD_ERR_INVALID, "hdd_soa_*: rows must be >= 1");
+    a.rows[k] = rows[k];
+    a.row_first[k + 1] = a.row_first[k] + rows[k];
+  }
+  a.ld = ld;
+  a.n = n;
+  return HDD_OK;
+}
+}  // namespace
+
+extern "C" int hdd_soa_gather(hdd_ctx* ctx, const double* const* arrays, const int32_t* rows, int32_t n_arrays,
+                              int64_t ld, const int32_t* d_idx, int64_t n, double* d_buf, void* stream)
+{
+  if (!ctx || !arrays || !d_idx || !d_buf) return set_error(HDD_ERR_INVALID, "hdd_soa_gather: null argument");
+  SoaArgs a{};
+  int rc = soa_args(a, rows, n_arrays, ld, n);
+  if (rc) return rc;
+  for (int k = 0; k < n_arrays; ++k) a.src[k] = arrays[k];
+  a.idx = d_idx;
+  a.buf_out = d_buf;
+  if (n == 0) return HDD_OK;
+  hipError_t e = hipSetDevice(ctx->device);
+  if (e != hipSuccess) return hip_fail(e, "hdd_soa_gather: hipSetDevice");
+  const int64_t total = int64_t(a.row_first[n_arrays]) * n;
+  const unsigned grid = unsigned(std::min<int64_t>((total + 255) / 256, 4096));
+  hipLaunchKernelGGL(soa_gather_kernel, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream), a);
+  e = hipGetLastError();
+  return e == hipSuccess ? HDD_OK : hip_fail(e, "hdd_soa_gather: launch");
+}
+
+extern "C" int hdd_soa_scatter(hdd_ctx* ctx, double* const* arrays, const int32_t* rows, int32_t n_arrays, int64_t ld,
+                               int64_t dst_offset, int64_t n, const double* d_buf, void* stream)
+{
+  if (!ctx || !arrays || !d_buf) return set_error(HDD_ERR_INVALID, "hdd_soa_scatter: null argument");
+  SoaArgs a{};
+  int rc = soa_args(a, rows, n_arrays, ld, n);
+  if (rc) return rc;
+  for (int k = 0; k < n_arrays; ++k) a.dst[k] = arrays[k];
+  a.offset = dst_offset;
+  a.buf_in = d_buf;
+  if (n == 0) return HDD_OK;
+  hipError_t e = hipSetDevice(ctx->device);
+  if (e != hipSuccess) return hip_fail(e, "hdd_soa_scatter: hipSetDevice");
+  const int64_t total = int64_t(a.row_first[n_arrays]) * n;
+  const unsigned grid = unsigned(std::min<int64_t>((total + 255) / 256, 4096));
+  hipLaunchKernelGGL(soa_scatter_kernel, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream), a);
+  e = hipGetLastError();
+  return e == hipSuccess ? HDD_OK : hip_fail(e, "hdd_soa_scatter: launch");
+}

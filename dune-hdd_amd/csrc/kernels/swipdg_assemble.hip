@@ -1,0 +1,639 @@
+// dune-hdd_amd/csrc/kernels/swipdg_assemble.hip
+//
+// CDNA4 (gfx950) kernels of the SWIPDG stiffness assembly -- the MI355X replacement of dune-gdt's
+// SystemAssembler::walk() over Operators::EllipticSWIPDG (reference call sites:
+// dune/hdd/linearelliptic/discretizations/swipdg.hh:218-249, 485; block-swipdg.hh:1136-1179, 1270-1326).
+//
+// Design:
+//   * owner-computes: the rows of an element are written by the lanes that own the element; every face
+//     term is evaluated by the row owner on its side (entity/entity + entity/neighbour blocks), so each
+//     CSR value is written exactly once, with no atomics and no zero-fill, in one pass over the mesh;
+//   * a workgroup = one tile of 64 consecutive owned elements; WPE waves per tile, wave w owns the local
+//     test functions (rows) [w*RPT, (w+1)*RPT) of the 64 elements, lane = element (coalesced SoA loads);
+//   * the row block of an element is contiguous in the CSR value array (sorted blocks, element-blocked
+//     DoFs), so each wave stages one row of its 64 elements in LDS and streams it out with consecutive
+//     lanes on consecutive values (6-12 cache lines per store instruction instead of 64);
+//   * reference-element basis/quadrature tables are compile-time constants (immediates), not LDS: at
+//     p = 1 they are a handful of numbers per rule;
+//   * the neighbour geometry is rebuilt from the shared face vertices plus the neighbour's non-face
+//     vertices (twin face / orientation from face_info), so a face gathers 2 (triangle) or 4 (quad)
+//     coordinates, the neighbour's tensor and coefficient;
+//   * XCD-aware tile order: consecutive tiles run on one XCD so the neighbour rows above/below a tile
+//     hit that XCD's L2.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <type_traits>
+
+#include "hdd.h"
+#include "swipdg_kernels.hh"
+
+#ifndef HDD_MIN_WAVES_PER_EU
+#define HDD_MIN_WAVES_PER_EU 4
+#endif
+
+namespace hdd {
+namespace dev {
+
+// ------------------------------------------------------------------------------------------------
+// reference elements (Dune numbering) and shape functions
+// ------------------------------------------------------------------------------------------------
+struct Simplex {
+  static constexpr int NV = 3, NF = 3, NB = 3;
+  // vertex k of the reference simplex: (0,0), (1,0), (0,1)
+  __host__ __device__ static constexpr double rv(int k, int d) { return (k == 1 + d) ? 1.0 : 0.0; }
+  // faces 0:(0,1) 1:(0,2) 2:(1,2)
+  __host__ __device__ static constexpr int fv(int f, int k) { return f == 0 ? k : (f == 1 ? 2 * k : 1 + k); }
+  // orientation of (t_y, -t_x) w.r.t. the outer normal on the reference element
+  __host__ __device__ static constexpr double face_sign(int f) { return f == 1 ? -1.0 : 1.0; }
+  __device__ static inline void shape(double x, double y, double* phi, double* gx, double* gy)
+  {
+    phi[0] = 1.0 - x - y; phi[1] = x; phi[2] = y;
+    gx[0] = -1.0; gy[0] = -1.0;
+    gx[1] = 1.0;  gy[1] = 0.0;
+    gx[2] = 0.0;  gy[2] = 1.0;
+  }
+};
+
+struct Cube {
+  static constexpr int NV = 4, NF = 4, NB = 4;
+  // vertex k: (k & 1, k >> 1)
+  __host__ __device__ static constexpr double rv(int k, int d) { return double((k >> d) & 1); }
+  // faces 0:(0,2) 1:(1,3) 2:(0,1) 3:(2,3)
+  __host__ __device__ static constexpr int fv(int f, int k)
+  {
+    return f == 0 ? 2 * k : (f == 1 ? 1 + 2 * k : (f == 2 ? k : 2 + k));
+  }
+  __host__ __device__ static constexpr double face_sign(int f) { return (f == 0 || f == 3) ? -1.0 : 1.0; }
+  __device__ static inline void shape(double x, double y, double* phi, double* gx, double* gy)
+  {
+    phi[0] = (1 - x) * (1 - y); phi[1] = x * (1 - y); phi[2] = (1 - x) * y; phi[3] = x * y;
+    gx[0] = -(1 - y); gy[0] = -(1 - x);
+    gx[1] = (1 - y);  gy[1] = -x;
+    gx[2] = -y;       gy[2] = (1 - x);
+    gx[3] = y;        gy[3] = x;
+  }
+};
+
+// ------------------------------------------------------------------------------------------------
+// quadrature (compile-time): Gauss-Legendre on [0,1]; simplex centroid / 3-point / Dunavant-6
+// ------------------------------------------------------------------------------------------------
+template <int N>
+struct Gauss01;
+template <>
+struct Gauss01<1> {
+  __device__ static constexpr double s(int) { return 0.5; }
+  __device__ static constexpr double w(int) { return 1.0; }
+};
+template <>
+struct Gauss01<2> {
+  __device__ static constexpr double s(int q) { return q == 0 ? 0.21132486540518711775 : 0.78867513459481288225; }
+  __device__ static constexpr double w(int) { return 0.5; }
+};
+template <>
+struct Gauss01<3> {
+  __device__ static constexpr double s(int q)
+  {
+    return q == 0 ? 0.11270166537925831148 : (q == 1 ? 0.5 : 0.88729833462074168852);
+  }
+  __device__ static constexpr double w(int q) { return q == 1 ? 8.0 / 18.0 : 5.0 / 18.0; }
+};
+
+template <class E, int NQ>
+struct VolRule;
+template <>
+struct VolRule<Simplex, 1> {
+  __device__ static constexpr double x(int) { return 1.0 / 3.0; }
+  __device__ static constexpr double y(int) { return 1.0 / 3.0; }
+  __device__ static constexpr double w(int) { return 0.5; }
+};
+template <>
+struct VolRule<Simplex, 3> {
+  __device__ static constexpr double x(int q) { return q == 1 ? 2.0 / 3.0 : 1.0 / 6.0; }
+  __device__ static constexpr double y(int q) { return q == 2 ? 2.0 / 3.0 : 1.0 / 6.0; }
+  __device__ static constexpr double w(int) { return 1.0 / 6.0; }
+};
+template <>
+struct VolRule<Simplex, 6> {  // Dunavant degree 4 (used for integrand orders 3 and 4)
+  static constexpr double A = 0.44594849091596488632, WA = 0.22338158967801146570;
+  static constexpr double B = 0.091576213509770743460, WB = 0.10995174365532186764;
+  __device__ static constexpr double pa(int k, int d) { return k == 0 ? A : ((k == 1) == (d == 0) ? 1 - 2 * A : A); }
+  __device__ static constexpr double pb(int k, int d) { return k == 0 ? B : ((k == 1) == (d == 0) ? 1 - 2 * B : B); }
+  __device__ static constexpr double x(int q) { return q < 3 ? pa(q, 0) : pb(q - 3, 0); }
+  __device__ static constexpr double y(int q) { return q < 3 ? pa(q, 1) : pb(q - 3, 1); }
+  __device__ static constexpr double w(int q) { return q < 3 ? 0.5 * WA : 0.5 * WB; }
+};
+template <int NQ>
+struct VolRule<Cube, NQ> {   // tensor Gauss, NQ = n*n, point q = j*n + i
+  static constexpr int N = NQ == 1 ? 1 : (NQ == 4 ? 2 : 3);
+  __device__ static constexpr double x(int q) { return Gauss01<N>::s(q % N); }
+  __device__ static constexpr double y(int q) { return Gauss01<N>::s(q / N); }
+  __device__ static constexpr double w(int q) { return Gauss01<N>::w(q % N) * Gauss01<N>::w(q / N); }
+};
+
+// ------------------------------------------------------------------------------------------------
+// coefficients
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ double kappa_elem(const KappaArg& k, int64_t e)
+{
+  return k.kind == HDD_FN_PER_ELEM ? k.per_elem[e] : k.c;
+}
+__device__ __forceinline__ double kappa_at(const KappaArg& k, double pe, double x, double y)
+{
+  return k.kind == HDD_FN_SINUSOID ? k.c + k.b * sin(k.kx * x + k.ky * y) : pe;
+}
+
+typedef double dvec2 __attribute__((ext_vector_type(2)));
+
+struct Tensor {
+  double a00, a01, a11;
+};
+__device__ __forceinline__ Tensor tensor_of(const AssembleArgs& a, int64_t e)
+{
+  Tensor t;
+  if (a.tkind == HDD_TENSOR_ISO_PER_ELEM) {
+    const double v = a.tper[e];
+    t.a00 = v; t.a01 = 0.0; t.a11 = v;
+  } else if (a.tkind == HDD_TENSOR_SYM_PER_ELEM) {
+    t.a00 = a.tper[e]; t.a01 = a.tper[a.n_local + e]; t.a11 = a.tper[2 * a.n_local + e];
+  } else {
+    t.a00 = a.tc0; t.a01 = a.tc1; t.a11 = a.tc2;
+  }
+  return t;
+}
+// (A g) . n
+__device__ __forceinline__ double agn(const Tensor& A, double gx, double gy, double nx, double ny)
+{
+  return (A.a00 * gx + A.a01 * gy) * nx + (A.a01 * gx + A.a11 * gy) * ny;
+}
+
+// affine geometry x = v0 + J xh;  J^{-T} for the gradients
+struct Geom {
+  double x0, y0, j00, j01, j10, j11, det, i00, i01, i10, i11;   // i = J^{-1}
+  __device__ __forceinline__ void init(double ax, double ay, double bx, double by, double cx, double cy)
+  {
+    x0 = ax; y0 = ay;
+    j00 = bx - ax; j01 = cx - ax; j10 = by - ay; j11 = cy - ay;
+    det = j00 * j11 - j01 * j10;
+    const double id = 1.0 / det;
+    i00 = j11 * id; i01 = -j01 * id; i10 = -j10 * id; i11 = j00 * id;
+  }
+  __device__ __forceinline__ void grad(double ghx, double ghy, double& gx, double& gy) const
+  {
+    gx = i00 * ghx + i10 * ghy;
+    gy = i01 * ghx + i11 * ghy;
+  }
+  __device__ __forceinline__ void global(double xh, double yh, double& x, double& y) const
+  {
+    x = x0 + j00 * xh + j01 * yh;
+    y = y0 + j10 * xh + j11 * yh;
+  }
+};
+
+// ------------------------------------------------------------------------------------------------
+// per-thread element context (loaded once, shared by all components)
+// ------------------------------------------------------------------------------------------------
+template <class E>
+struct ElemCtx {
+  double X[E::NV], Y[E::NV];
+  int32_t nbr[E::NF];
+  uint32_t finfo;
+  Tensor A;
+  Geom G;
+  double adet, osgn;
+  int64_t e;
+  int pos_self, pos[E::NF], rowlen;
+  double* img;   // LDS image of this element's row block
+};
+
+// geometry of the neighbour across face f: shared face vertices + the neighbour's non-face vertices
+template <class E>
+struct NbrFace {
+  Geom H;
+  Tensor A;
+  int ta, tb, to;   // neighbour local vertices on the face (matching my fv(f,0) / fv(f,1) unless rev)
+  bool rev;
+};
+
+template <class E, int F>
+__device__ __forceinline__ void load_neighbor(const AssembleArgs& a, const ElemCtx<E>& c, int32_t n, NbrFace<E>& nf)
+{
+  const int64_t ne = a.n_local;
+  constexpr int fa = E::fv(F, 0), fb = E::fv(F, 1);
+  const uint32_t inf = (c.finfo >> (4 * F)) & 15u;
+  const int tw = int(inf & 7u);
+  nf.rev = (inf & 8u) != 0u;
+  nf.ta = E::fv(tw, 0);
+  nf.tb = E::fv(tw, 1);
+  const double PAx = nf.rev ? c.X[fb] : c.X[fa], PAy = nf.rev ? c.Y[fb] : c.Y[fa];
+  const double PBx = nf.rev ? c.X[fa] : c.X[fb], PBy = nf.rev ? c.Y[fa] : c.Y[fb];
+  double NX[E::NV], NY[E::NV];
+  if constexpr (E::NV == 3) {
+    nf.to = 3 - nf.ta - nf.tb;
+    const double Ox = a.coords[(2 * nf.to) * ne + n], Oy = a.coords[(2 * nf.to + 1) * ne + n];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      NX[k] = k == nf.ta ? PAx : (k == nf.tb ? PBx : Ox);
+      NY[k] = k == nf.ta ? PAy : (k == nf.tb ? PBy : Oy);
+    }
+  } else {
+    nf.to = -1;
+    const int tc = E::fv(tw ^ 1, 0), td = E::fv(tw ^ 1, 1);
+    const double Cx = a.coords[(2 * tc) * ne + n], Cy = a.coords[(2 * tc + 1) * ne + n];
+    const double Dx = a.coords[(2 * td) * ne + n], Dy = a.coords[(2 * td + 1) * ne + n];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      NX[k] = k == nf.ta ? PAx : (k == nf.tb ? PBx : (k == tc ? Cx : Dx));
+      NY[k] = k == nf.ta ? PAy : (k == nf.tb ? PBy : (k == tc ? Cy : Dy));
+    }
+  }
+  nf.H.init(NX[0], NY[0], NX[1], NY[1], NX[2], NY[2]);
+  nf.A = tensor_of(a, n);
+}
+
+struct FaceGeo {
+  double len, nx, ny, hpow, tx, ty, xa, ya;
+};
+
+template <class E, int F>
+__device__ __forceinline__ FaceGeo face_geo(const AssembleArgs& a, const ElemCtx<E>& c)
+{
+  constexpr int fa = E::fv(F, 0), fb = E::fv(F, 1);
+  FaceGeo g;
+  g.xa = c.X[fa];
+  g.ya = c.Y[fa];
+  g.tx = c.X[fb] - c.X[fa];
+  g.ty = c.Y[fb] - c.Y[fa];
+  g.len = sqrt(g.tx * g.tx + g.ty * g.ty);
+  const double nsc = E::face_sign(F) * c.osgn / g.len;
+  g.nx = g.ty * nsc;
+  g.ny = -g.tx * nsc;
+  g.hpow = a.beta == 1.0 ? g.len : pow(g.len, a.beta);
+  return g;
+}
+
+// ------------------------------------------------------------------------------------------------
+// row I of one component, P1 simplex with piecewise-constant coefficients: closed-form face integrals
+// (exactly what the reference's order-2 Gauss rule integrates: int phi = |F|/2, int phi phi = |F|/6 (1+d_ij))
+// ------------------------------------------------------------------------------------------------
+template <int I>
+__device__ __forceinline__ void row_simplex_pwc(const AssembleArgs& a, const ElemCtx<Simplex>& c, const KappaArg& K)
+{
+  using E = Simplex;
+  const double ke = kappa_elem(K, c.e);
+  double g[3][2];
+  {
+    double phi[3], ghx[3], ghy[3];
+    E::shape(1.0 / 3.0, 1.0 / 3.0, phi, ghx, ghy);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) c.G.grad(ghx[k], ghy[k], g[k][0], g[k][1]);
+  }
+  double self[3];
+  {
+    const double fac = 0.5 * c.adet;   // 1-point rule: weight 1/2 * |det J|
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const double Agx = c.A.a00 * g[j][0] + c.A.a01 * g[j][1];
+      const double Agy = c.A.a01 * g[j][0] + c.A.a11 * g[j][1];
+      self[j] = fac * ke * (Agx * g[I][0] + Agy * g[I][1]);
+    }
+  }
+#pragma unroll
+  for (int f = 0; f < 3; ++f) {
+    const int32_t n = c.nbr[f];
+    if (n <= HDD_NBR_NEUMANN) continue;
+    FaceGeo fg;
+    double Ae[3];
+    // face f as a compile-time constant for the helpers
+    if (f == 0) fg = face_geo<E, 0>(a, c);
+    else if (f == 1) fg = face_geo<E, 1>(a, c);
+    else fg = face_geo<E, 2>(a, c);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) Ae[k] = agn(c.A, g[k][0], g[k][1], fg.nx, fg.ny);
+    const int fa = E::fv(f, 0), fb = E::fv(f, 1), fc = 3 - fa - fb;
+    const double half = 0.5 * fg.len, third = fg.len / 3.0, sixth = fg.len / 6.0;
+    const double M1I = I == fc ? 0.0 : half;
+    const double dm = agn(c.A, fg.nx, fg.ny, fg.nx, fg.ny);
+    if (n >= 0) {
+      NbrFace<E> nf;
+      if (f == 0) load_neighbor<E, 0>(a, c, n, nf);
+      else if (f == 1) load_neighbor<E, 1>(a, c, n, nf);
+      else load_neighbor<E, 2>(a, c, n, nf);
+      const double kn = kappa_elem(K, n);
+      const double dp = agn(nf.A, fg.nx, fg.ny, fg.nx, fg.ny);
+      const double gamma = (dp * dm) / (dp + dm);
+      const double w_plus = dm / (dp + dm);
+      const double w_minus = dp / (dp + dm);
+      const double pen = (ke * kn * a.sigma_inner * gamma) / fg.hpow;
+      double An[3];
+      {
+        double phi[3], ghx[3], ghy[3];
+        E::shape(1.0 / 3.0, 1.0 / 3.0, phi, ghx, ghy);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          double hx, hy;
+          nf.H.grad(ghx[k], ghy[k], hx, hy);
+          An[k] = agn(nf.A, hx, hy, fg.nx, fg.ny);
+        }
+      }
+      // neighbour vertex matching my vertex I (only meaningful if I is on the face)
+      const int mI = (I == fa) ? (nf.rev ? nf.tb : nf.ta) : (nf.rev ? nf.ta : nf.tb);
+      double* out = c.img + c.pos[f] * 3;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const double M1j = j == nf.to ? 0.0 : half;
+        const double Mx = I == fc ? 0.0 : (j == mI ? third : (j == nf.to ? 0.0 : sixth));
+        out[j] = -w_plus * kn * An[j] * M1I + w_minus * ke * Ae[I] * M1j - pen * Mx;
+      }
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const double M1j = j == fc ? 0.0 : half;
+        const double Mm = (I == fc || j == fc) ? 0.0 : (I == j ? third : sixth);
+        self[j] += -w_minus * ke * (Ae[j] * M1I + Ae[I] * M1j) + pen * Mm;
+      }
+    } else {   // Dirichlet: SWIPDG::BoundaryLHS
+      const double pen = (a.sigma_boundary * ke * dm) / fg.hpow;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const double M1j = j == fc ? 0.0 : half;
+        const double Mm = (I == fc || j == fc) ? 0.0 : (I == j ? third : sixth);
+        self[j] += -ke * (Ae[j] * M1I + Ae[I] * M1j) + pen * Mm;
+      }
+    }
+  }
+  double* out = c.img + c.pos_self * 3;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) out[j] = self[j];
+}
+
+// ------------------------------------------------------------------------------------------------
+// row I of one component, generic quadrature (Q1 quads; smooth coefficients on either element)
+// ------------------------------------------------------------------------------------------------
+template <class E, int NQV, int NQF, int I>
+__device__ __forceinline__ void row_quadrature(const AssembleArgs& a, const ElemCtx<E>& c, const KappaArg& K)
+{
+  constexpr int NB = E::NB, NF = E::NF;
+  const double ke = kappa_elem(K, c.e);
+  double self[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) self[j] = 0.0;
+  // ---- LocalEvaluation::Elliptic ----
+#pragma unroll
+  for (int q = 0; q < NQV; ++q) {
+    double phi[NB], ghx[NB], ghy[NB], gx[NB], gy[NB];
+    E::shape(VolRule<E, NQV>::x(q), VolRule<E, NQV>::y(q), phi, ghx, ghy);
+#pragma unroll
+    for (int k = 0; k < NB; ++k) c.G.grad(ghx[k], ghy[k], gx[k], gy[k]);
+    double px = 0.0, py = 0.0;
+    if (K.kind == HDD_FN_SINUSOID) c.G.global(VolRule<E, NQV>::x(q), VolRule<E, NQV>::y(q), px, py);
+    const double kap = kappa_at(K, ke, px, py);
+    const double fac = VolRule<E, NQV>::w(q) * c.adet;
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const double Agx = c.A.a00 * gx[j] + c.A.a01 * gy[j];
+      const double Agy = c.A.a01 * gx[j] + c.A.a11 * gy[j];
+      self[j] += fac * kap * (Agx * gx[I] + Agy * gy[I]);
+    }
+  }
+  // ---- faces ----
+#pragma unroll
+  for (int f = 0; f < NF; ++f) {
+    const int32_t n = c.nbr[f];
+    if (n <= HDD_NBR_NEUMANN) continue;
+    FaceGeo fg;
+    if (f == 0) fg = face_geo<E, 0>(a, c);
+    else if (f == 1) fg = face_geo<E, 1>(a, c);
+    else if (f == 2) fg = face_geo<E, 2 % NF>(a, c);
+    else fg = face_geo<E, 3 % NF>(a, c);
+    const int fa = E::fv(f, 0), fb = E::fv(f, 1);
+    const double rax = E::rv(fa, 0), ray = E::rv(fa, 1), rbx = E::rv(fb, 0), rby = E::rv(fb, 1);
+    const double dm = agn(c.A, fg.nx, fg.ny, fg.nx, fg.ny);
+    if (n >= 0) {
+      NbrFace<E> nf;
+      if (f == 0) load_neighbor<E, 0>(a, c, n, nf);
+      else if (f == 1) load_neighbor<E, 1>(a, c, n, nf);
+      else if (f == 2) load_neighbor<E, 2 % NF>(a, c, n, nf);
+      else load_neighbor<E, 3 % NF>(a, c, n, nf);
+      const double kn = kappa_elem(K, n);
+      const double dp = agn(nf.A, fg.nx, fg.ny, fg.nx, fg.ny);
+      const double gamma = (dp * dm) / (dp + dm);
+      const double w_plus = dm / (dp + dm);
+      const double w_minus = dp / (dp + dm);
+      const double sax = E::rv(nf.ta, 0), say = E::rv(nf.ta, 1), sbx = E::rv(nf.tb, 0), sby = E::rv(nf.tb, 1);
+      double nbv[NB];
+#pragma unroll
+      for (int j = 0; j < NB; ++j) nbv[j] = 0.0;
+#pragma unroll
+      for (int q = 0; q < NQF; ++q) {
+        const double s = Gauss01<NQF>::s(q);
+        double pe[NB], ghx[NB], ghy[NB], gex[NB], gey[NB];
+        E::shape(rax + s * (rbx - rax), ray + s * (rby - ray), pe, ghx, ghy);
+#pragma unroll
+        for (int k = 0; k < NB; ++k) c.G.grad(ghx[k], ghy[k], gex[k], gey[k]);
+        const double sn = nf.rev ? 1.0 - s : s;
+        double pn[NB], hhx[NB], hhy[NB], gnx[NB], gny[NB];
+        E::shape(sax + sn * (sbx - sax), say + sn * (sby - say), pn, hhx, hhy);
+#pragma unroll
+        for (int k = 0; k < NB; ++k) nf.H.grad(hhx[k], hhy[k], gnx[k], gny[k]);
+        double kme = ke, knb = kn;
+        if (K.kind == HDD_FN_SINUSOID) {
+          kme = kappa_at(K, ke, fg.xa + s * fg.tx, fg.ya + s * fg.ty);
+          knb = kme;
+        }
+        const double pen = (kme * knb * a.sigma_inner * gamma) / fg.hpow;
+        const double fac = Gauss01<NQF>::w(q) * fg.len;
+        double Ae[NB], An[NB];
+#pragma unroll
+        for (int k = 0; k < NB; ++k) {
+          Ae[k] = agn(c.A, gex[k], gey[k], fg.nx, fg.ny);
+          An[k] = agn(nf.A, gnx[k], gny[k], fg.nx, fg.ny);
+        }
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+          self[j] += fac * (-w_minus * kme * Ae[j] * pe[I] - w_minus * kme * pe[j] * Ae[I] + pen * pe[j] * pe[I]);
+          nbv[j] += fac * (-w_plus * knb * An[j] * pe[I] + w_minus * kme * pn[j] * Ae[I] - pen * pn[j] * pe[I]);
+        }
+      }
+      double* out = c.img + c.pos[f] * NB;
+#pragma unroll
+      for (int j = 0; j < NB; ++j) out[j] = nbv[j];
+    } else {   // Dirichlet
+#pragma unroll
+      for (int q = 0; q < NQF; ++q) {
+        const double s = Gauss01<NQF>::s(q);
+        double pe[NB], ghx[NB], ghy[NB], gex[NB], gey[NB];
+        E::shape(rax + s * (rbx - rax), ray + s * (rby - ray), pe, ghx, ghy);
+#pragma unroll
+        for (int k = 0; k < NB; ++k) c.G.grad(ghx[k], ghy[k], gex[k], gey[k]);
+        double kme = ke;
+        if (K.kind == HDD_FN_SINUSOID) kme = kappa_at(K, ke, fg.xa + s * fg.tx, fg.ya + s * fg.ty);
+        const double pen = (a.sigma_boundary * kme * dm) / fg.hpow;
+        const double fac = Gauss01<NQF>::w(q) * fg.len;
+        double Ae[NB];
+#pragma unroll
+        for (int k = 0; k < NB; ++k) Ae[k] = agn(c.A, gex[k], gey[k], fg.nx, fg.ny);
+#pragma unroll
+        for (int j = 0; j < NB; ++j) self[j] += fac * (-kme * Ae[j] * pe[I] - kme * pe[j] * Ae[I] + pen * pe[j] * pe[I]);
+      }
+    }
+  }
+  double* out = c.img + c.pos_self * NB;
+#pragma unroll
+  for (int j = 0; j < NB; ++j) out[j] = self[j];
+}
+
+template <class E, int NQV, int NQF, bool PWC, int I>
+__device__ __forceinline__ void row(const AssembleArgs& a, const ElemCtx<E>& c, const KappaArg& K)
+{
+  if constexpr (PWC && std::is_same<E, Simplex>::value && NQV == 1 && NQF == 2)
+    row_simplex_pwc<I>(a, c, K);
+  else
+    row_quadrature<E, NQV, NQF, I>(a, c, K);
+}
+
+// ------------------------------------------------------------------------------------------------
+// the kernel: one workgroup = 64 consecutive owned elements x NB waves (wave w = local row w)
+// ------------------------------------------------------------------------------------------------
+template <class E, int NQV, int NQF, bool PWC>
+__global__ void __launch_bounds__(64 * E::NB, HDD_MIN_WAVES_PER_EU)
+swipdg_assemble_kernel(const AssembleArgs a)
+{
+  constexpr int NB = E::NB, NF = E::NF, NV = E::NV;
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+
+  // XCD-aware tile order (bijective): hardware block b runs on XCD b % 8; each XCD gets a contiguous
+  // range of tiles so the element rows above / below a tile sit in the same L2.
+  const int64_t nwg = gridDim.x;
+  const int64_t b = blockIdx.x;
+  const int64_t q8 = nwg >> 3, r8 = nwg & 7, xcd = b & 7;
+  const int64_t tile = xcd * q8 + (xcd < r8 ? xcd : r8) + (b >> 3);
+
+  const int64_t t0 = a.own_begin + tile * 64;
+  const int64_t tend = t0 + 64 < a.own_end ? t0 + 64 : a.own_end;
+  const int64_t e = t0 + lane;
+  const bool active = e < tend;
+  const int64_t ne = a.n_local;
+  const int64_t* eptr = a.elem_ptr - a.own_begin;
+  const int64_t base = eptr[t0];
+  const int64_t base_al = base & ~int64_t(1);          // 16-byte aligned image origin
+  const int64_t tile_end = eptr[tend];
+
+  ElemCtx<E> c;
+  c.e = active ? e : t0;   // inactive tail lanes shadow a valid element; their LDS writes are skipped
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    c.X[k] = a.coords[(2 * k) * ne + c.e];
+    c.Y[k] = a.coords[(2 * k + 1) * ne + c.e];
+  }
+#pragma unroll
+  for (int f = 0; f < NF; ++f) c.nbr[f] = a.nbrs[f * ne + c.e];
+  c.finfo = a.finfo[c.e];
+  c.A = tensor_of(a, c.e);
+  const int64_t my_off = eptr[c.e];
+  c.G.init(c.X[0], c.Y[0], c.X[1], c.Y[1], c.X[2], c.Y[2]);
+  c.adet = fabs(c.G.det);
+  c.osgn = c.G.det > 0.0 ? 1.0 : -1.0;
+  int nblk = 1;
+  c.pos_self = 0;
+#pragma unroll
+  for (int f = 0; f < NF; ++f) {
+    nblk += c.nbr[f] >= 0;
+    c.pos_self += (c.nbr[f] >= 0 && c.nbr[f] < c.e);
+  }
+#pragma unroll
+  for (int f = 0; f < NF; ++f) {
+    int p = (c.e < c.nbr[f]) ? 1 : 0;
+#pragma unroll
+    for (int g = 0; g < NF; ++g) p += (c.nbr[g] >= 0 && c.nbr[g] < c.nbr[f]);
+    c.pos[f] = p;
+  }
+  c.rowlen = nblk * NB;
+  // lanes past the tile end write to a scratch row after the image
+  c.img = active ? lds + (my_off - base_al) + int64_t(wave) * c.rowlen
+                 : lds + 64 * NB * (NF + 1) * NB + 2;
+
+  // one component per launch (the host loops over the affine components): a component loop in here
+  // would let the compiler hoist every component-invariant face quantity of all faces above the loop
+  {
+    const KappaArg K = a.kappa[0];
+    double* out = a.vals[0];
+    switch (wave) {
+      case 0: row<E, NQV, NQF, PWC, 0>(a, c, K); break;
+      case 1: row<E, NQV, NQF, PWC, 1>(a, c, K); break;
+      case 2: row<E, NQV, NQF, PWC, 2>(a, c, K); break;
+      default: if constexpr (NB > 3) row<E, NQV, NQF, PWC, NB - 1>(a, c, K); break;
+    }
+    __syncthreads();
+    // stream the tile's contiguous row blocks [base, tile_end) out of LDS, 16 bytes per lane
+    const int64_t lo = base_al, hi = tile_end;
+    const int64_t n2 = (hi - lo) >> 1;
+    for (int64_t k = threadIdx.x; k < n2; k += blockDim.x) {
+      const int64_t gi = lo + 2 * k;
+      const dvec2 v = *reinterpret_cast<const dvec2*>(lds + 2 * k);
+      if (gi >= base) {
+        __builtin_nontemporal_store(v, reinterpret_cast<dvec2*>(out + gi));
+      } else {   // first pair straddles the tile start: only the upper value is ours
+        out[gi + 1] = v.y;
+      }
+    }
+    if (((hi - lo) & 1) && threadIdx.x == 0) out[hi - 1] = lds[hi - 1 - lo];
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// host-side launch
+// ------------------------------------------------------------------------------------------------
+template <class E, int NQV, int NQF, bool PWC>
+static hipError_t launch_t(const AssembleArgs& a, hipStream_t s)
+{
+  const int64_t n_own = a.own_end - a.own_begin;
+  if (n_own <= 0) return hipSuccess;
+  const int64_t tiles = (n_own + 63) / 64;
+  // tile image (64 elements x full row blocks) + 1 alignment slot + a scratch row for tail lanes
+  const size_t lds = (size_t(64) * E::NB * (E::NF + 1) * E::NB + 2 + (E::NF + 1) * E::NB) * sizeof(double);
+  for (int c = 0; c < a.n_comp; ++c) {
+    AssembleArgs ac = a;
+    ac.n_comp = 1;
+    ac.kappa[0] = a.kappa[c];
+    ac.vals[0] = a.vals[c];
+    hipLaunchKernelGGL((swipdg_assemble_kernel<E, NQV, NQF, PWC>), dim3(unsigned(tiles)), dim3(64 * E::NB), lds, s, ac);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+int volume_points(int elem_type, int order)
+{
+  if (elem_type == HDD_SIMPLEX) return order <= 1 ? 1 : (order == 2 ? 3 : (order <= 4 ? 6 : -1));
+  const int n = (order + 2) / 2;
+  return n <= 3 ? n * n : -1;
+}
+int face_points(int order)
+{
+  const int n = (order + 2) / 2;
+  return n <= 3 ? n : -1;
+}
+
+hipError_t launch_assemble(const AssembleArgs& a, int nqv, int nqf, hipStream_t s, bool* supported)
+{
+  *supported = true;
+  bool pwc = true;
+  for (int c = 0; c < a.n_comp; ++c) pwc &= a.kappa[c].kind != HDD_FN_SINUSOID;
+  if (a.elem_type == HDD_SIMPLEX) {
+    if (nqv == 1 && nqf == 2) return pwc ? launch_t<Simplex, 1, 2, true>(a, s) : launch_t<Simplex, 1, 2, false>(a, s);
+    if (nqv == 6 && nqf == 3) return launch_t<Simplex, 6, 3, false>(a, s);
+    if (nqv == 3 && nqf == 2) return launch_t<Simplex, 3, 2, false>(a, s);
+  } else {
+    if (nqv == 1 && nqf == 2) return launch_t<Cube, 1, 2, false>(a, s);
+    if (nqv == 4 && nqf == 3) return launch_t<Cube, 4, 3, false>(a, s);
+    if (nqv == 4 && nqf == 2) return launch_t<Cube, 4, 2, false>(a, s);
+  }
+  *supported = false;
+  return hipSuccess;
+}
+
+}  // namespace dev
+}  // namespace hdd

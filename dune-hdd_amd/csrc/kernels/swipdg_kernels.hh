@@ -1,0 +1,38 @@
+// dune-hdd_amd/csrc/kernels/swipdg_kernels.hh -- kernel argument blocks shared by the ABI and the kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "hdd.h"
+
+namespace hdd {
+namespace dev {
+
+struct KappaArg {
+  int32_t kind, order;
+  double c, b, kx, ky;
+  const double* per_elem;
+};
+
+struct AssembleArgs {
+  int32_t elem_type, n_comp;
+  int64_t n_local, own_begin, own_end;
+  const double* coords;
+  const int32_t* nbrs;
+  const uint32_t* finfo;
+  const int64_t* elem_ptr;
+  int32_t tkind, pad;
+  double tc0, tc1, tc2;
+  const double* tper;
+  double sigma_inner, sigma_boundary, beta;
+  KappaArg kappa[HDD_MAX_COMP];
+  double* vals[HDD_MAX_COMP];
+};
+
+int volume_points(int elem_type, int order);
+int face_points(int order);
+hipError_t launch_assemble(const AssembleArgs& a, int nqv, int nqf, hipStream_t s, bool* supported);
+
+}  // namespace dev
+}  // namespace hdd

@@ -1,0 +1,405 @@
+"""hdd_amd -- Python front-end of the MI355X SWIPDG assembly engine (C ABI: include/hdd.h).
+
+The product is ``dune-hdd_amd/lib/libhdd_amd.so`` (HIP kernels for gfx950 + host C++).  This module only
+binds it with ctypes; PyTorch is used for device memory, streams and torch.distributed (plumbing).  There
+is no CPU fallback: every device entry point raises if the library or a GPU is missing.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.abspath(os.path.join(_PKG, "..", ".."))          # dune-hdd_amd/
+LIB_PATH = os.path.join(ROOT, "lib", "libhdd_amd.so")
+HEADER = os.path.abspath(os.path.join(ROOT, "..", "include", "hdd.h"))
+
+SIMPLEX, CUBE = 0, 1
+NBR_DIRICHLET, NBR_NEUMANN = -1, -2
+FN_CONST, FN_PER_ELEM, FN_SINUSOID = 0, 1, 2
+TENSOR_CONST, TENSOR_ISO_PER_ELEM, TENSOR_SYM_PER_ELEM = 0, 1, 2
+BOUNDARY_ALL_DIRICHLET, BOUNDARY_ALL_NEUMANN = 0, 1
+MAX_COMP = 8
+
+# dune-gdt LocalEvaluation::SWIPDG::internal defaults at p = 1 (pinned by the ESV2007 expectation tables)
+SIGMA_INNER_P1 = 8.0
+SIGMA_BOUNDARY_P1 = 14.0
+
+
+class HddError(RuntimeError):
+    pass
+
+
+class StructuredDesc(C.Structure):
+    _fields_ = [("elem_type", C.c_int32), ("nx", C.c_int32), ("ny", C.c_int32), ("px", C.c_int32),
+                ("py", C.c_int32), ("boundary", C.c_int32), ("pad", C.c_int32),
+                ("lower", C.c_double * 2), ("upper", C.c_double * 2)]
+
+
+class GridInfo(C.Structure):
+    _fields_ = [("elem_type", C.c_int32), ("nb", C.c_int32), ("nfaces", C.c_int32), ("nvpe", C.c_int32),
+                ("n_elements", C.c_int64), ("n_vertices", C.c_int64), ("n_subdomains", C.c_int32),
+                ("pad", C.c_int32)]
+
+
+class LocalInfo(C.Structure):
+    _fields_ = [("n_local", C.c_int64), ("own_begin", C.c_int64), ("own_end", C.c_int64),
+                ("n_ghost", C.c_int64), ("global_first", C.c_int64)]
+
+
+class MeshT(C.Structure):
+    _fields_ = [("elem_type", C.c_int32), ("pad", C.c_int32), ("n_local", C.c_int64), ("own_begin", C.c_int64),
+                ("own_end", C.c_int64), ("coords", C.c_void_p), ("neighbors", C.c_void_p),
+                ("face_info", C.c_void_p)]
+
+
+class ScalarFn(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("order", C.c_int32), ("c", C.c_double), ("b", C.c_double),
+                ("kx", C.c_double), ("ky", C.c_double), ("per_elem", C.c_void_p)]
+
+
+class TensorFn(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("pad", C.c_int32), ("c", C.c_double * 3), ("per_elem", C.c_void_p)]
+
+
+class Params(C.Structure):
+    _fields_ = [("sigma_inner", C.c_double), ("sigma_boundary", C.c_double), ("beta", C.c_double),
+                ("vol_order", C.c_int32), ("face_order", C.c_int32)]
+
+
+class CsrT(C.Structure):
+    _fields_ = [("n_rows", C.c_int64), ("n_cols", C.c_int64), ("nnz", C.c_int64), ("row_ptr", C.c_void_p),
+                ("col", C.c_void_p), ("elem_ptr", C.c_void_p)]
+
+
+_LIB = None
+_VP, _I32, _I64, _D = C.c_void_p, C.c_int32, C.c_int64, C.c_double
+
+
+def build(jobs=8):
+    subprocess.check_call(["make", "-s", "-j%d" % jobs, "-C", ROOT])
+
+
+def lib():
+    """Load libhdd_amd.so (fails loudly when the HIP extension has not been built)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise HddError("libhdd_amd.so missing at %s -- build it with `make -C dune-hdd_amd` "
+                       "(there is no CPU fallback)" % LIB_PATH)
+    L = C.CDLL(LIB_PATH)
+    sig = {
+        "hdd_abi_version": (_I32, []),
+        "hdd_ctx_create": (_I32, [C.c_int, _VP]),
+        "hdd_ctx_destroy": (None, [_VP]),
+        "hdd_last_error": (C.c_char_p, [_VP]),
+        "hdd_grid_create_structured": (_I32, [C.POINTER(StructuredDesc), _VP]),
+        "hdd_grid_create_from_connectivity": (_I32, [_I32, _I64, _VP, _I64, _VP, _VP, _I32, _I32, _VP]),
+        "hdd_grid_destroy": (None, [_VP]),
+        "hdd_grid_get_info": (_I32, [_VP, C.POINTER(GridInfo)]),
+        "hdd_grid_subdomain_range": (_I32, [_VP, _I32, _I32, C.POINTER(_I64), C.POINTER(_I64)]),
+        "hdd_grid_connectivity": (_I32, [_VP, _VP, _VP, _VP]),
+        "hdd_local_create": (_I32, [_VP, _I32, _I32, _VP]),
+        "hdd_local_destroy": (None, [_VP]),
+        "hdd_local_get_info": (_I32, [_VP, C.POINTER(LocalInfo)]),
+        "hdd_local_fill": (_I32, [_VP, _VP, _VP, _VP, _VP, _VP]),
+        "hdd_local_centers": (_I32, [_VP, _VP]),
+        "hdd_local_halo_plan": (_I32, [_VP, _VP, _I32, C.POINTER(_I32), _VP, _VP, _VP, _VP]),
+        "hdd_local_send_list": (_I32, [_VP, _VP, _I32, _I32, _VP]),
+        "hdd_checkerboard": (_I32, [_I64, _VP, _VP, _VP, _I32, _I32, _VP, _VP]),
+        "hdd_pattern_count": (_I32, [_I32, _I64, _I64, _I64, _VP, C.POINTER(_I64)]),
+        "hdd_pattern_fill": (_I32, [_I32, _I64, _I64, _I64, _VP, _VP, _VP, _VP, _VP]),
+        "hdd_swipdg_assemble": (_I32, [_VP, C.POINTER(MeshT), C.POINTER(ScalarFn), _I32, C.POINTER(TensorFn),
+                                       C.POINTER(Params), C.POINTER(CsrT), _VP, _VP]),
+        "hdd_affine_lincomb": (_I32, [_VP, _I64, _VP, _I32, _VP, _I32, _VP, _I64, _VP]),
+        "hdd_soa_gather": (_I32, [_VP, _VP, _VP, _I32, _I64, _VP, _I64, _VP, _VP]),
+        "hdd_soa_scatter": (_I32, [_VP, _VP, _VP, _I32, _I64, _I64, _I64, _VP, _VP]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _LIB = L
+    return L
+
+
+def _check(rc, what=""):
+    if rc != 0:
+        msg = lib().hdd_last_error(None)
+        raise HddError("%s failed (status %d): %s" % (what, rc, msg.decode() if msg else ""))
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data
+
+
+def declared_symbols(header=HEADER):
+    """Names of the functions include/hdd.h declares (for the ABI export test)."""
+    import re
+    txt = open(header).read()
+    return sorted(set(re.findall(r"\b(hdd_[a-z0-9_]+)\s*\(", txt)))
+
+
+# ----------------------------------------------------------------------------------------------------
+# host grids
+# ----------------------------------------------------------------------------------------------------
+class Grid:
+    """Host grid (hdd_grid): structured rectangle (SGrid-like quads or Kuhn triangles) with an optional
+    px x py subdomain partition, or a general conforming mesh from connectivity."""
+
+    def __init__(self, handle):
+        self.h = handle
+        info = GridInfo()
+        _check(lib().hdd_grid_get_info(self.h, C.byref(info)), "hdd_grid_get_info")
+        self.elem_type = info.elem_type
+        self.nb = info.nb
+        self.nf = info.nfaces
+        self.nvpe = info.nvpe
+        self.ne = info.n_elements
+        self.nv = info.n_vertices
+        self.n_sub = info.n_subdomains
+
+    @classmethod
+    def structured(cls, elem_type, nx, ny, lower=(0.0, 0.0), upper=(1.0, 1.0), px=1, py=1,
+                   boundary=BOUNDARY_ALL_DIRICHLET):
+        d = StructuredDesc(elem_type, nx, ny, px, py, boundary, 0, (C.c_double * 2)(*lower),
+                           (C.c_double * 2)(*upper))
+        h = C.c_void_p()
+        _check(lib().hdd_grid_create_structured(C.byref(d), C.byref(h)), "hdd_grid_create_structured")
+        return cls(h)
+
+    @classmethod
+    def from_connectivity(cls, elem_type, coords, elem_vert, subdomain=None, n_sub=1,
+                          boundary=BOUNDARY_ALL_DIRICHLET):
+        coords = np.ascontiguousarray(coords, np.float64)
+        ev = np.ascontiguousarray(elem_vert, np.int32)
+        sd = None if subdomain is None else np.ascontiguousarray(subdomain, np.int32)
+        h = C.c_void_p()
+        _check(lib().hdd_grid_create_from_connectivity(elem_type, coords.shape[0], _p(coords), ev.shape[0],
+                                                       _p(ev), _p(sd), n_sub, boundary, C.byref(h)),
+               "hdd_grid_create_from_connectivity")
+        return cls(h)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().hdd_grid_destroy(self.h)
+            self.h = None
+
+    def connectivity(self):
+        coords = np.empty((self.nv, 2))
+        ev = np.empty((self.ne, self.nvpe), np.int32)
+        sd = np.empty(self.ne, np.int32)
+        _check(lib().hdd_grid_connectivity(self.h, _p(coords), _p(ev), _p(sd)), "hdd_grid_connectivity")
+        return coords, ev, sd
+
+    def subdomain_range(self, s0, s1):
+        a, b = C.c_int64(), C.c_int64()
+        _check(lib().hdd_grid_subdomain_range(self.h, s0, s1, C.byref(a), C.byref(b)), "hdd_grid_subdomain_range")
+        return a.value, b.value
+
+    def local(self, s0=0, s1=None):
+        return LocalMesh(self, s0, self.n_sub if s1 is None else s1)
+
+
+class LocalMesh:
+    """Rank-local view (hdd_local): owned subdomains [s0, s1) + face ghosts, host SoA arrays."""
+
+    def __init__(self, grid, s0, s1):
+        self.grid = grid
+        self.s0, self.s1 = s0, s1
+        h = C.c_void_p()
+        _check(lib().hdd_local_create(grid.h, s0, s1, C.byref(h)), "hdd_local_create")
+        self.h = h
+        info = LocalInfo()
+        _check(lib().hdd_local_get_info(self.h, C.byref(info)), "hdd_local_get_info")
+        self.n_local, self.own_begin, self.own_end = info.n_local, info.own_begin, info.own_end
+        self.n_ghost, self.global_first = info.n_ghost, info.global_first
+        self.elem_type, self.nb, self.nf, self.nvpe = grid.elem_type, grid.nb, grid.nf, grid.nvpe
+        n = self.n_local
+        self.coords = np.empty((2 * self.nvpe, n))
+        self.neighbors = np.empty((self.nf, n), np.int32)
+        self.face_info = np.empty(n, np.uint32)
+        self.global_id = np.empty(n, np.int64)
+        self.subdomain = np.empty(n, np.int32)
+        _check(lib().hdd_local_fill(self.h, _p(self.coords), _p(self.neighbors), _p(self.face_info),
+                                    _p(self.global_id), _p(self.subdomain)), "hdd_local_fill")
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().hdd_local_destroy(self.h)
+            self.h = None
+
+    @property
+    def n_own(self):
+        return self.own_end - self.own_begin
+
+    def centers(self):
+        c = np.empty((2, self.n_local))
+        _check(lib().hdd_local_centers(self.h, _p(c)), "hdd_local_centers")
+        return c
+
+    def checkerboard(self, lower, upper, ncx, ncy, values):
+        """dune-stuff Checkerboard at the element barycentres (problems/spe10.hh:151-156 tensor field)."""
+        c = self.centers()
+        vals = np.ascontiguousarray(values, np.float64)
+        out = np.empty(self.n_local)
+        lo = (C.c_double * 2)(*lower)
+        up = (C.c_double * 2)(*upper)
+        _check(lib().hdd_checkerboard(self.n_local, _p(c), lo, up, ncx, ncy, _p(vals), _p(out)), "hdd_checkerboard")
+        return out
+
+    def halo_plan(self, owner, my_rank):
+        owner = np.ascontiguousarray(owner, np.int32)
+        npeers = C.c_int32()
+        _check(lib().hdd_local_halo_plan(self.h, _p(owner), my_rank, C.byref(npeers), None, None, None, None),
+               "hdd_local_halo_plan")
+        k = npeers.value
+        peers = np.empty(k, np.int32)
+        sc, ro, rc = np.empty(k, np.int64), np.empty(k, np.int64), np.empty(k, np.int64)
+        _check(lib().hdd_local_halo_plan(self.h, _p(owner), my_rank, C.byref(npeers), _p(peers), _p(sc), _p(ro),
+                                         _p(rc)), "hdd_local_halo_plan")
+        plan = []
+        for i in range(k):
+            ids = np.empty(sc[i], np.int32)
+            _check(lib().hdd_local_send_list(self.h, _p(owner), my_rank, i, _p(ids)), "hdd_local_send_list")
+            plan.append(dict(peer=int(peers[i]), send=ids, recv_offset=int(ro[i]), recv_count=int(rc[i])))
+        return plan
+
+    def pattern(self):
+        """Host CSR pattern of the owned rows (global columns): row_ptr, col, elem_ptr."""
+        nnz = C.c_int64()
+        nbrs = np.ascontiguousarray(self.neighbors)
+        _check(lib().hdd_pattern_count(self.elem_type, self.n_local, self.own_begin, self.own_end, _p(nbrs),
+                                       C.byref(nnz)), "hdd_pattern_count")
+        row_ptr = np.empty(self.nb * self.n_own + 1, np.int64)
+        col = np.empty(nnz.value, np.int32)
+        elem_ptr = np.empty(self.n_own + 1, np.int64)
+        _check(lib().hdd_pattern_fill(self.elem_type, self.n_local, self.own_begin, self.own_end, _p(nbrs),
+                                      _p(self.global_id), _p(row_ptr), _p(col), _p(elem_ptr)), "hdd_pattern_fill")
+        return row_ptr, col, elem_ptr
+
+
+# ----------------------------------------------------------------------------------------------------
+# device side (torch = plumbing for memory and streams)
+# ----------------------------------------------------------------------------------------------------
+def _torch():
+    import torch
+    if not torch.cuda.is_available():
+        raise HddError("no HIP device visible: the hdd_amd device path has no CPU fallback")
+    return torch
+
+
+class Context:
+    def __init__(self, device=0):
+        self.device = device
+        h = C.c_void_p()
+        _check(lib().hdd_ctx_create(device, C.byref(h)), "hdd_ctx_create")
+        self.h = h
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().hdd_ctx_destroy(self.h)
+            self.h = None
+
+
+def scalar_fn(kind=FN_CONST, c=1.0, b=0.0, kx=0.0, ky=0.0, per_elem=None, order=0):
+    """A diffusion-factor component; per_elem is a device tensor (kept alive by the returned object)."""
+    f = ScalarFn(kind, order, c, b, kx, ky, None if per_elem is None else per_elem.data_ptr())
+    f._keep = per_elem
+    return f
+
+
+def tensor_fn(kind=TENSOR_CONST, c=(1.0, 0.0, 1.0), per_elem=None):
+    t = TensorFn(kind, 0, (C.c_double * 3)(*c), None if per_elem is None else per_elem.data_ptr())
+    t._keep = per_elem
+    return t
+
+
+def params(sigma_inner=SIGMA_INNER_P1, sigma_boundary=SIGMA_BOUNDARY_P1, beta=1.0, vol_order=-1, face_order=-1):
+    return Params(sigma_inner, sigma_boundary, beta, vol_order, face_order)
+
+
+class DeviceMesh:
+    """Device copy of a LocalMesh (SoA arrays in HBM)."""
+
+    def __init__(self, local, device=0, zero_ghosts=False):
+        torch = _torch()
+        dev = torch.device("cuda", device)
+        coords = torch.from_numpy(local.coords).to(dev)
+        if zero_ghosts:   # ghost columns then come only from the halo exchange
+            coords[:, :local.own_begin] = 0
+            coords[:, local.own_end:] = 0
+        self.coords = coords.contiguous()
+        self.neighbors = torch.from_numpy(local.neighbors).to(dev).contiguous()
+        self.face_info = torch.from_numpy(local.face_info.view(np.int32)).to(dev).contiguous()
+        self.local = local
+        self.t = MeshT(local.elem_type, 0, local.n_local, local.own_begin, local.own_end, self.coords.data_ptr(),
+                       self.neighbors.data_ptr(), self.face_info.data_ptr())
+
+
+class DevicePattern:
+    def __init__(self, local, device=0, host=None):
+        torch = _torch()
+        dev = torch.device("cuda", device)
+        row_ptr, col, elem_ptr = host if host is not None else local.pattern()
+        self.host = (row_ptr, col, elem_ptr)
+        self.row_ptr = torch.from_numpy(row_ptr).to(dev)
+        self.col = torch.from_numpy(col).to(dev)
+        self.elem_ptr = torch.from_numpy(elem_ptr).to(dev)
+        self.nnz = int(col.shape[0])
+        n_cols = int(local.grid.ne) * local.nb
+        self.t = CsrT(row_ptr.shape[0] - 1, n_cols, self.nnz, self.row_ptr.data_ptr(), self.col.data_ptr(),
+                      self.elem_ptr.data_ptr())
+
+
+def assemble(ctx, dmesh, dpattern, kappas, tensor, prm=None, vals=None, stream=None):
+    """hdd_swipdg_assemble: returns a list of device value tensors (one per diffusion-factor component)."""
+    torch = _torch()
+    kappas = list(kappas)
+    n = len(kappas)
+    if vals is None:
+        vals = [torch.empty(dpattern.nnz, dtype=torch.float64, device=dmesh.coords.device) for _ in range(n)]
+    arr = (ScalarFn * n)(*kappas)
+    ptrs = (C.c_void_p * n)(*[v.data_ptr() for v in vals])
+    prm = prm or params()
+    s = stream if stream is not None else torch.cuda.current_stream(dmesh.coords.device).cuda_stream
+    _check(lib().hdd_swipdg_assemble(ctx.h, C.byref(dmesh.t), arr, n, C.byref(tensor), C.byref(prm),
+                                     C.byref(dpattern.t), ptrs, C.c_void_p(s)), "hdd_swipdg_assemble")
+    return vals
+
+
+def affine_lincomb(ctx, comps, theta, out=None, stream=None):
+    """out[s] = sum_q theta[s, q] * comps[q]  (hdd_affine_lincomb)."""
+    torch = _torch()
+    theta = np.ascontiguousarray(theta, np.float64)
+    ns, nc = theta.shape
+    nnz = comps[0].numel()
+    if out is None:
+        out = torch.empty((ns, nnz), dtype=torch.float64, device=comps[0].device)
+    ptrs = (C.c_void_p * nc)(*[c.data_ptr() for c in comps])
+    s = stream if stream is not None else torch.cuda.current_stream(comps[0].device).cuda_stream
+    _check(lib().hdd_affine_lincomb(ctx.h, nnz, ptrs, nc, _p(theta), ns, out.data_ptr(), out.stride(0),
+                                    C.c_void_p(s)), "hdd_affine_lincomb")
+    return out
+
+
+def soa_gather(ctx, arrays, rows, ld, idx, buf, stream=None):
+    torch = _torch()
+    n = len(arrays)
+    ptrs = (C.c_void_p * n)(*[a.data_ptr() for a in arrays])
+    r = (C.c_int32 * n)(*rows)
+    s = stream if stream is not None else torch.cuda.current_stream(buf.device).cuda_stream
+    _check(lib().hdd_soa_gather(ctx.h, ptrs, r, n, ld, idx.data_ptr(), idx.numel(), buf.data_ptr(),
+                                C.c_void_p(s)), "hdd_soa_gather")
+
+
+def soa_scatter(ctx, arrays, rows, ld, offset, n_items, buf, stream=None):
+    torch = _torch()
+    n = len(arrays)
+    ptrs = (C.c_void_p * n)(*[a.data_ptr() for a in arrays])
+    r = (C.c_int32 * n)(*rows)
+    s = stream if stream is not None else torch.cuda.current_stream(buf.device).cuda_stream
+    _check(lib().hdd_soa_scatter(ctx.h, ptrs, r, n, ld, offset, n_items, buf.data_ptr(), C.c_void_p(s)),
+           "hdd_soa_scatter")

@@ -1,0 +1,82 @@
+"""Face-halo exchange of a sharded (Block)SWIPDG assembly.
+
+Each rank owns a contiguous range of subdomains (block-swipdg.hh:355-382: the owner of subdomain ss writes
+A_ss and A_ss,nn) and assembles only its own rows.  The rows need the element records (vertex coordinates,
+diffusion tensor, per-element coefficients) of the face neighbours owned by other ranks: those ghost
+columns are filled here by a pack (hdd_soa_gather) -> RCCL send/recv (torch.distributed, backend "nccl"
+is RCCL on ROCm, point-to-point over xGMI) -> unpack (hdd_soa_scatter) sequence.  No reduction is ever
+needed (rows are owned), so there is no all-reduce on the data path.
+"""
+import numpy as np
+
+from . import soa_gather, soa_scatter, _torch
+
+
+class HaloExchange:
+    """arrays: list of (device tensor [rows][n_local] contiguous, rows).  owner: subdomain -> rank map."""
+
+    def __init__(self, ctx, local, arrays, owner, rank, host_staging=False):
+        torch = _torch()
+        import torch.distributed as dist
+        self.dist = dist
+        self.ctx = ctx
+        self.local = local
+        self.arrays = [a for a, _ in arrays]
+        self.rows = [int(r) for _, r in arrays]
+        self.total_rows = sum(self.rows)
+        self.ld = local.n_local
+        self.host_staging = host_staging
+        dev = self.arrays[0].device
+        self.plan = local.halo_plan(owner, rank)
+        self.peers = []
+        for p in self.plan:
+            send_idx = torch.from_numpy(p["send"]).to(dev)
+            sbuf = torch.empty((self.total_rows, len(p["send"])), dtype=torch.float64, device=dev)
+            rbuf = torch.empty((self.total_rows, p["recv_count"]), dtype=torch.float64, device=dev)
+            hs = hr = None
+            if host_staging:
+                hs = torch.empty(sbuf.shape, dtype=torch.float64).pin_memory() if torch.cuda.is_available() else None
+                hr = torch.empty(rbuf.shape, dtype=torch.float64)
+            self.peers.append(dict(peer=p["peer"], idx=send_idx, sbuf=sbuf, rbuf=rbuf, off=p["recv_offset"],
+                                   n_recv=p["recv_count"], hs=hs, hr=hr))
+
+    @property
+    def halo_bytes(self):
+        return sum(8 * self.total_rows * (p["idx"].numel() + p["n_recv"]) for p in self.peers)
+
+    def exchange(self):
+        dist = self.dist
+        for p in self.peers:
+            if p["idx"].numel():
+                soa_gather(self.ctx, self.arrays, self.rows, self.ld, p["idx"], p["sbuf"])
+        if self.host_staging:
+            ops = []
+            for p in self.peers:
+                p["hs"].copy_(p["sbuf"])
+            for p in self.peers:
+                ops.append(dist.P2POp(dist.isend, p["hs"], p["peer"]))
+                ops.append(dist.P2POp(dist.irecv, p["hr"], p["peer"]))
+            for r in dist.batch_isend_irecv(ops):
+                r.wait()
+            for p in self.peers:
+                p["rbuf"].copy_(p["hr"])
+        else:
+            ops = []
+            for p in self.peers:
+                ops.append(dist.P2POp(dist.isend, p["sbuf"], p["peer"]))
+                ops.append(dist.P2POp(dist.irecv, p["rbuf"], p["peer"]))
+            if ops:
+                for r in dist.batch_isend_irecv(ops):
+                    r.wait()
+        for p in self.peers:
+            if p["n_recv"]:
+                soa_scatter(self.ctx, self.arrays, self.rows, self.ld, p["off"], p["n_recv"], p["rbuf"])
+
+
+def strip_owner(n_sub, world):
+    """subdomain -> rank for `world` ranks owning contiguous, near-equal subdomain ranges."""
+    own = np.empty(n_sub, np.int32)
+    for r in range(world):
+        a, b = (r * n_sub) // world, ((r + 1) * n_sub) // world
+        own[a:b] = r
+    return own

@@ -1,0 +1,218 @@
+/*
+ * include/hdd.h -- C ABI of the MI355X SWIPDG assembly engine (libhdd_amd.so).
+ *
+ * Drop-in boundary for dune-hdd's linearelliptic SWIPDG / BlockSWIPDG hot path.  The reference has no
+ * C ABI (its boundary is C++ templates over dune-gdt's SystemAssembler); every entry point below names
+ * the reference interface it replaces.  Conventions:
+ *   - plain C types and pointers only; "device" pointers are HIP device memory owned by the caller;
+ *   - every function returns HDD_OK (0) or an HDD_ERR_* code, never throws; hdd_last_error(ctx) (or
+ *     hdd_last_error(NULL) for functions without a context) returns the message of the last failure
+ *     of the calling thread;
+ *   - device work is enqueued on the hipStream_t passed as `stream` (NULL = legacy default stream) and
+ *     is NOT synchronised; no allocation or synchronisation happens inside hdd_swipdg_assemble /
+ *     hdd_affine_lincomb / hdd_soa_gather / hdd_soa_scatter, so they are hipGraph-capturable;
+ *   - one context per thread at a time (thread-compatible, like the reference's single-threaded init()).
+ *
+ * Numbering: DoF (row / column) of local basis function i of element g is g*nb + i (element-blocked,
+ * as dune-fem's DG mapper); a CSR row holds the DoFs of its element and of every face neighbour, sorted
+ * ascending (the EllipticSWIPDG pattern, swipdg.hh:169).  Block-SWIPDG numbering is the same rule applied
+ * to a subdomain-major element order (Spaces::Block::mapToGlobal(ss, ii) = offset(ss) + ii,
+ * block-swipdg.hh:1042, 1093), which all hdd_grid_* builders produce.
+ */
+#ifndef HDD_H
+#define HDD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HDD_ABI_VERSION 1
+#define HDD_MAX_COMP 8
+
+typedef enum {
+  HDD_OK = 0,
+  HDD_ERR_INVALID = 1,      /* wrong input given (Stuff::Exceptions::wrong_input_given) */
+  HDD_ERR_HIP = 2,          /* HIP runtime failure */
+  HDD_ERR_UNSUPPORTED = 3,  /* NotImplemented in the reference's sense */
+  HDD_ERR_NOMEM = 4,
+  HDD_ERR_RANGE = 5         /* index_out_of_range */
+} hdd_status;
+
+enum { HDD_SIMPLEX = 0, HDD_CUBE = 1 };                      /* P1 triangles / Q1 parallelograms (2d) */
+enum { HDD_NBR_DIRICHLET = -1, HDD_NBR_NEUMANN = -2 };       /* neighbour codes of domain-boundary faces */
+enum { HDD_FN_CONST = 0, HDD_FN_PER_ELEM = 1, HDD_FN_SINUSOID = 2 };
+enum { HDD_TENSOR_CONST = 0, HDD_TENSOR_ISO_PER_ELEM = 1, HDD_TENSOR_SYM_PER_ELEM = 2 };
+enum { HDD_BOUNDARY_ALL_DIRICHLET = 0, HDD_BOUNDARY_ALL_NEUMANN = 1 };
+
+typedef struct hdd_ctx hdd_ctx;
+typedef struct hdd_grid hdd_grid;
+typedef struct hdd_local hdd_local;
+
+/* ---------------------------------------------------------------------------------------------- */
+/* context                                                                                         */
+/* ---------------------------------------------------------------------------------------------- */
+int hdd_abi_version(void);
+/* binds `hip_device`; replaces nothing in the reference (DUNE is host-only) */
+int hdd_ctx_create(int hip_device, hdd_ctx** out);
+void hdd_ctx_destroy(hdd_ctx* ctx);
+/* message of the last failure on this thread (ctx may be NULL); never NULL */
+const char* hdd_last_error(const hdd_ctx* ctx);
+
+/* ---------------------------------------------------------------------------------------------- */
+/* grids (host) -- replace the grid providers the reference builds its spaces on:                  */
+/*   Stuff::Grid::Providers::Cube (testcases/ESV2007.hh:123-129, testcases/spe10.hh:301-307) and     */
+/*   grid::Multiscale::Providers::Cube with num_partitions (testcases/base.hh:150-191)             */
+/* ---------------------------------------------------------------------------------------------- */
+typedef struct {
+  int32_t elem_type;          /* HDD_SIMPLEX: Kuhn split of every square (createSimplexGrid); HDD_CUBE */
+  int32_t nx, ny;             /* squares per direction */
+  int32_t px, py;             /* subdomain partition ("num_partitions" [px py 1]); 1,1 = monolithic */
+  int32_t boundary;           /* HDD_BOUNDARY_* applied to every domain-boundary face */
+  int32_t pad;
+  double lower[2], upper[2];
+} hdd_structured_desc;
+
+typedef struct {
+  int32_t elem_type, nb, nfaces, nvpe;
+  int64_t n_elements, n_vertices;
+  int32_t n_subdomains, pad;
+} hdd_grid_info;
+
+int hdd_grid_create_structured(const hdd_structured_desc* desc, hdd_grid** out);
+/* general conforming 2d mesh from connectivity (vertex order = Dune reference element order);
+ * `subdomain` (nullable) assigns elements to subdomains, elements are then renumbered subdomain-major */
+int hdd_grid_create_from_connectivity(int32_t elem_type, int64_t n_vertices, const double* vertex_coords,
+                                      int64_t n_elements, const int32_t* elem_vert, const int32_t* subdomain,
+                                      int32_t n_subdomains, int32_t boundary, hdd_grid** out);
+void hdd_grid_destroy(hdd_grid* g);
+int hdd_grid_get_info(const hdd_grid* g, hdd_grid_info* out);
+/* element range [first, last) of the subdomains [s_begin, s_end) in the (subdomain-major) numbering */
+int hdd_grid_subdomain_range(const hdd_grid* g, int32_t s_begin, int32_t s_end, int64_t* first, int64_t* last);
+/* global element -> (vertex ids [nvpe]) and subdomain ids, for tests / visualisation (host arrays) */
+int hdd_grid_connectivity(const hdd_grid* g, double* vertex_coords, int32_t* elem_vert, int32_t* subdomain);
+
+/* Rank-local view: the elements of subdomains [s_begin, s_end) ("owned") plus the ghost elements that
+ * share a face with them, laid out [ghosts with smaller global id][owned][ghosts with larger global id]
+ * so that local order == global order (owner-computes rows, block-swipdg.hh:355-382). */
+typedef struct {
+  int64_t n_local, own_begin, own_end, n_ghost;
+  int64_t global_first;       /* global id of the first owned element */
+} hdd_local_info;
+
+int hdd_local_create(const hdd_grid* g, int32_t s_begin, int32_t s_end, hdd_local** out);
+void hdd_local_destroy(hdd_local* l);
+int hdd_local_get_info(const hdd_local* l, hdd_local_info* out);
+/* host SoA arrays, n_local columns each:
+ *   coords    [2*nvpe][n_local] : x of vertex k at (2k)*n_local+e, y at (2k+1)*n_local+e (ghost rows too)
+ *   neighbors [nfaces][n_local] : local neighbour id or HDD_NBR_* (ghost columns: -3)
+ *   face_info [n_local]         : 4 bits per face: twin local face (bits 0-2), reversed (bit 3)
+ *   global_id [n_local]         : global element id
+ *   subdomain [n_local]         : subdomain of the element
+ * any pointer may be NULL */
+int hdd_local_fill(const hdd_local* l, double* coords, int32_t* neighbors, uint32_t* face_info,
+                   int64_t* global_id, int32_t* subdomain);
+/* element barycentres [2][n_local] (coefficient lookup, e.g. the Spe10 checkerboard) */
+int hdd_local_centers(const hdd_local* l, double* centers);
+/* halo plan with the subdomain -> rank map `owner` [n_subdomains]:
+ *   peers[n_peers] ranks this rank exchanges with (ascending); for peer p: send_count[p] owned elements
+ *   whose local ids are listed by hdd_local_send_list(l, p, ...), and recv_count[p] ghost slots starting
+ *   at local id recv_offset[p] (ghosts of one owner are contiguous).  Call with peers == NULL to query
+ *   n_peers. */
+int hdd_local_halo_plan(const hdd_local* l, const int32_t* owner, int32_t my_rank, int32_t* n_peers,
+                        int32_t* peers, int64_t* send_count, int64_t* recv_offset, int64_t* recv_count);
+int hdd_local_send_list(const hdd_local* l, const int32_t* owner, int32_t my_rank, int32_t peer_index,
+                        int32_t* local_ids);
+
+/* dune-stuff Checkerboard evaluated at element barycentres: value of cell (cx, cy), x fastest */
+int hdd_checkerboard(int64_t n, const double* centers /*[2][n]*/, const double lower[2], const double upper[2],
+                     int32_t ncx, int32_t ncy, const double* cell_values, double* out);
+
+/* ---------------------------------------------------------------------------------------------- */
+/* sparsity pattern (host) -- replaces EllipticSWIPDG::pattern(test, ansatz) (swipdg.hh:169) and the */
+/* block pattern of add_local_to_global_pattern / compute_face_pattern (block-swipdg.hh:304-325,     */
+/* 1036-1049).  Rows of the owned elements, global columns.                                          */
+/* ---------------------------------------------------------------------------------------------- */
+int hdd_pattern_count(int32_t elem_type, int64_t n_local, int64_t own_begin, int64_t own_end,
+                      const int32_t* neighbors, int64_t* nnz);
+/* row_ptr [nb*(own_end-own_begin)+1], col [nnz], elem_ptr [own_end-own_begin+1] (= row_ptr[k*nb]);
+ * global_id may be NULL (local == global) */
+int hdd_pattern_fill(int32_t elem_type, int64_t n_local, int64_t own_begin, int64_t own_end,
+                     const int32_t* neighbors, const int64_t* global_id, int64_t* row_ptr, int32_t* col,
+                     int64_t* elem_ptr);
+
+/* ---------------------------------------------------------------------------------------------- */
+/* device assembly -- replaces the LHS part of SWIPDG::init() (swipdg.hh:222-249 + walk() at 485):   */
+/* one GDT::Operators::EllipticSWIPDG per diffusion-factor component = LocalEvaluation::Elliptic +    */
+/* SWIPDG::Inner + SWIPDG::BoundaryLHS, scattered into Q+1 CSR value arrays on one pattern; and the  */
+/* BlockSWIPDG boundary / coupling assemblers (block-swipdg.hh:1136-1179, 1270-1326).                */
+/* ---------------------------------------------------------------------------------------------- */
+typedef struct {
+  int32_t elem_type;          /* HDD_SIMPLEX | HDD_CUBE */
+  int32_t pad;
+  int64_t n_local;            /* columns of the SoA arrays (owned + ghosts) */
+  int64_t own_begin, own_end; /* elements whose rows are assembled */
+  const double* coords;       /* device, layout of hdd_local_fill */
+  const int32_t* neighbors;   /* device */
+  const uint32_t* face_info;  /* device */
+} hdd_mesh;
+
+typedef struct {              /* one diffusion-factor component kappa_q (a Stuff::LocalizableFunction) */
+  int32_t kind;               /* HDD_FN_* */
+  int32_t order;              /* integration order of the function (Expression: integration_order) */
+  double c;                   /* CONST value, SINUSOID offset a */
+  double b, kx, ky;           /* SINUSOID: a + b*sin(kx*x + ky*y) */
+  const double* per_elem;     /* PER_ELEM: device [n_local] */
+} hdd_scalar_fn;
+
+typedef struct {              /* the (non-parametric) diffusion tensor A */
+  int32_t kind;               /* HDD_TENSOR_* */
+  int32_t pad;
+  double c[3];                /* CONST: a11, a12, a22 */
+  const double* per_elem;     /* ISO: device [n_local]; SYM: device [3][n_local] */
+} hdd_tensor_fn;
+
+typedef struct {
+  double sigma_inner;         /* LocalEvaluation::SWIPDG::internal::inner_sigma(p)    (8 at p=1) */
+  double sigma_boundary;      /* LocalEvaluation::SWIPDG::internal::boundary_sigma(p) (14 at p=1) */
+  double beta;                /* LocalEvaluation::SWIPDG::internal::default_beta(d) = 1/(d-1) (swipdg.hh:168) */
+  int32_t vol_order;          /* -1: the reference's integrand order (ord kappa + ord A + 2(p-1)) */
+  int32_t face_order;         /* -1: ord kappa + ord A + 2p */
+} hdd_swipdg_params;
+
+typedef struct {
+  int64_t n_rows, n_cols, nnz;
+  const int64_t* row_ptr;     /* device [n_rows+1] */
+  const int32_t* col;         /* device [nnz] */
+  const int64_t* elem_ptr;    /* device [n_owned+1]: first value of each owned element's row block */
+} hdd_csr;
+
+/* Writes d_vals[q][0..nnz) for q < n_comp (each value exactly once, no atomics, no zero-fill needed).
+ * Face terms are evaluated by the row owner on both sides of each face (owner-computes). */
+int hdd_swipdg_assemble(hdd_ctx* ctx, const hdd_mesh* mesh, const hdd_scalar_fn* kappa, int32_t n_comp,
+                        const hdd_tensor_fn* tensor, const hdd_swipdg_params* params, const hdd_csr* pattern,
+                        double* const* d_vals, void* stream);
+
+/* theta-lincomb of affine components on a shared pattern -- replaces
+ * AffinelyDecomposedContainer::freeze_parameter(mu) as used by ContainerBasedDefault::uncached_solve
+ * (base.hh:338-341, 357-361):  out[s][k] = sum_q theta[s*n_comp+q] * d_vals[q][k]  (theta on host) */
+int hdd_affine_lincomb(hdd_ctx* ctx, int64_t nnz, const double* const* d_vals, int32_t n_comp,
+                       const double* theta, int32_t n_samples, double* d_out, int64_t out_stride, void* stream);
+
+/* ---------------------------------------------------------------------------------------------- */
+/* halo records (face-coupling ghosts of a sharded BlockSWIPDG) -- SoA gather / scatter of element    */
+/* columns; the transport itself is RCCL send/recv (torch.distributed) between the two calls.         */
+/* ---------------------------------------------------------------------------------------------- */
+/* buf[(r)*n + i] = arrays[a][row(a,r)*ld + idx[i]] for the concatenated rows of all arrays */
+int hdd_soa_gather(hdd_ctx* ctx, const double* const* arrays, const int32_t* rows, int32_t n_arrays, int64_t ld,
+                   const int32_t* d_idx, int64_t n, double* d_buf, void* stream);
+/* arrays[a][row*ld + dst_offset + i] = buf[r*n + i] */
+int hdd_soa_scatter(hdd_ctx* ctx, double* const* arrays, const int32_t* rows, int32_t n_arrays, int64_t ld,
+                    int64_t dst_offset, int64_t n, const double* d_buf, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HDD_H */

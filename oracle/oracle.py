@@ -1,0 +1,250 @@
+"""oracle/oracle.py -- TEST INFRASTRUCTURE ONLY.
+
+ctypes front-end of the CPU oracle (``swipdg_oracle.c``), a restatement of dune-hdd's SWIPDG /
+BlockSWIPDG stiffness assembly (reference: dune/hdd/linearelliptic/discretizations/swipdg.hh:206-512,
+block-swipdg.hh:262-551).  Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s
+``cpu_baseline`` leg may import this module, and only as the checker / timed CPU baseline.
+
+Also holds the oracle-side structured grid builders (the reference's Stuff::Grid::Providers::Cube /
+StructuredGridFactory meshes, testcases/ESV2007.hh:123-129, testcases/spe10.hh:301-307) and the problem
+data of the BASELINE configs (problems/ESV2007.hh:75-81, problems/OS2014.hh:63-76, problems/spe10.hh:
+141-179) so that tests can build inputs without touching the product.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+SIMPLEX, CUBE = 0, 1
+FN_CONST, FN_PER_ELEM, FN_SINUSOID = 0, 1, 2
+TENSOR_CONST, TENSOR_ISO_PER_ELEM, TENSOR_SYM_PER_ELEM = 0, 1, 2
+BOUNDARY_DIRICHLET, BOUNDARY_NEUMANN = 0, 1
+
+# dune-gdt LocalEvaluation::SWIPDG::internal defaults for p = 1 (restated)
+SIGMA_INNER_P1 = 8.0
+SIGMA_BOUNDARY_P1 = 14.0
+
+
+class MeshT(C.Structure):
+    _fields_ = [("elem_type", C.c_int32), ("pad", C.c_int32), ("n_vertices", C.c_int64),
+                ("coords", C.c_void_p), ("n_elements", C.c_int64), ("elem_vert", C.c_void_p)]
+
+
+class ScalarT(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("order", C.c_int32), ("c", C.c_double), ("b", C.c_double),
+                ("kx", C.c_double), ("ky", C.c_double), ("per_elem", C.c_void_p)]
+
+
+class TensorT(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("pad", C.c_int32), ("c", C.c_double * 3), ("per_elem", C.c_void_p)]
+
+
+class ParamsT(C.Structure):
+    _fields_ = [("sigma_inner", C.c_double), ("sigma_boundary", C.c_double), ("beta", C.c_double),
+                ("boundary_kind", C.c_int32), ("vol_order_override", C.c_int32),
+                ("face_order_override", C.c_int32), ("pad", C.c_int32)]
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", _HERE])
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, "liboracle.so")
+        if not os.path.exists(path):
+            build()
+        L = C.CDLL(path)
+        L.or_grid_create.restype = C.c_void_p
+        L.or_grid_create.argtypes = [C.POINTER(MeshT)]
+        L.or_grid_destroy.argtypes = [C.c_void_p]
+        L.or_grid_neighbor.restype = C.c_int64
+        L.or_grid_neighbor.argtypes = [C.c_void_p, C.c_int64, C.c_int]
+        L.or_grid_neighbor_face.argtypes = [C.c_void_p, C.c_int64, C.c_int]
+        L.or_pattern_nnz.restype = C.c_int64
+        L.or_pattern_nnz.argtypes = [C.c_void_p]
+        L.or_pattern.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.or_assemble_swipdg.argtypes = [C.c_void_p, C.POINTER(ScalarT), C.POINTER(TensorT),
+                                         C.POINTER(ParamsT), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.or_block_numbering.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]
+        L.or_assemble_block_swipdg.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(ScalarT),
+                                               C.POINTER(TensorT), C.POINTER(ParamsT), C.c_void_p,
+                                               C.c_void_p, C.c_void_p, C.c_void_p]
+        L.or_rhs_l2.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
+        L.or_error_norms_esv2007.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
+                                             C.POINTER(C.c_double), C.POINTER(C.c_double)]
+        L.or_quadrature.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_void_p]
+        _LIB = L
+    return _LIB
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data
+
+
+# ----------------------------------------------------------------------------------------------------
+# structured grids (oracle side)
+# ----------------------------------------------------------------------------------------------------
+def cube_grid(nx, ny, lower=(0.0, 0.0), upper=(1.0, 1.0)):
+    """SGrid-like nx x ny quads, lexicographic elements, Dune cube vertex order (00,10,01,11)."""
+    xs = np.linspace(lower[0], upper[0], nx + 1)
+    ys = np.linspace(lower[1], upper[1], ny + 1)
+    X, Y = np.meshgrid(xs, ys)                       # [ny+1][nx+1]
+    coords = np.stack([X.ravel(), Y.ravel()], axis=1).copy()
+    j, i = np.meshgrid(np.arange(ny), np.arange(nx), indexing="ij")
+    v00 = (j * (nx + 1) + i).ravel()
+    ev = np.stack([v00, v00 + 1, v00 + nx + 1, v00 + nx + 2], axis=1).astype(np.int32)
+    return CUBE, coords, ev
+
+
+def kuhn_grid(nx, ny, lower=(0.0, 0.0), upper=(1.0, 1.0)):
+    """Kuhn triangulation (StructuredGridFactory::createSimplexGrid): per square (00,10,11),(00,01,11)."""
+    _, coords, q = cube_grid(nx, ny, lower, upper)
+    t0 = np.stack([q[:, 0], q[:, 1], q[:, 3]], axis=1)
+    t1 = np.stack([q[:, 0], q[:, 2], q[:, 3]], axis=1)
+    ev = np.stack([t0, t1], axis=1).reshape(-1, 3).astype(np.int32)
+    return SIMPLEX, coords, ev
+
+
+def element_centers(coords, ev):
+    return coords[ev].mean(axis=1)
+
+
+def checkerboard(centers, lower, upper, nxc, nyc, values):
+    """dune-stuff Checkerboard: cell of the element centre (row-major x fastest)."""
+    cx = np.clip(((centers[:, 0] - lower[0]) / (upper[0] - lower[0]) * nxc).astype(np.int64), 0, nxc - 1)
+    cy = np.clip(((centers[:, 1] - lower[1]) / (upper[1] - lower[1]) * nyc).astype(np.int64), 0, nyc - 1)
+    return values[cy * nxc + cx]
+
+
+def spe10_synthetic_permeability(nxc=100, nyc=20, seed=10):
+    """Stand-in for perm_case1.dat (absent): log10 k ~ U(-3, 3) on the 100x20 Model1 checkerboard."""
+    rng = np.random.default_rng(seed)
+    return 10.0 ** rng.uniform(-3.0, 3.0, size=nxc * nyc)
+
+
+# ----------------------------------------------------------------------------------------------------
+# oracle calls
+# ----------------------------------------------------------------------------------------------------
+class Grid:
+    def __init__(self, elem_type, coords, ev):
+        self.elem_type = int(elem_type)
+        self.coords = np.ascontiguousarray(coords, dtype=np.float64)
+        self.ev = np.ascontiguousarray(ev, dtype=np.int32)
+        self.nb = 3 if self.elem_type == SIMPLEX else 4
+        self.nf = self.nb
+        self.ne = self.ev.shape[0]
+        self._m = MeshT(self.elem_type, 0, self.coords.shape[0], _ptr(self.coords), self.ne, _ptr(self.ev))
+        self.h = lib().or_grid_create(C.byref(self._m))
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().or_grid_destroy(self.h)
+            self.h = None
+
+    def neighbors(self):
+        L = lib()
+        out = np.empty((self.ne, self.nf), np.int64)
+        nf = np.empty((self.ne, self.nf), np.int64)
+        for e in range(self.ne):
+            for f in range(self.nf):
+                out[e, f] = L.or_grid_neighbor(self.h, e, f)
+                nf[e, f] = L.or_grid_neighbor_face(self.h, e, f)
+        return out, nf
+
+    def pattern(self, elem_index=None):
+        L = lib()
+        nnz = L.or_pattern_nnz(self.h)
+        row_ptr = np.empty(self.ne * self.nb + 1, np.int64)
+        col = np.empty(nnz, np.int32)
+        ei = None if elem_index is None else np.ascontiguousarray(elem_index, np.int64)
+        L.or_pattern(self.h, _ptr(ei), _ptr(row_ptr), _ptr(col))
+        return row_ptr, col
+
+
+def scalar(kind=FN_CONST, c=1.0, b=0.0, kx=0.0, ky=0.0, per_elem=None, order=0):
+    s = ScalarT(kind, order, c, b, kx, ky, _ptr(per_elem))
+    s._keep = per_elem
+    return s
+
+
+def tensor(kind=TENSOR_CONST, c=(1.0, 0.0, 1.0), per_elem=None):
+    t = TensorT(kind, 0, (C.c_double * 3)(*c), _ptr(per_elem))
+    t._keep = per_elem
+    return t
+
+
+def params(boundary=BOUNDARY_DIRICHLET, sigma_inner=SIGMA_INNER_P1, sigma_boundary=SIGMA_BOUNDARY_P1,
+           beta=1.0, vol_order=-1, face_order=-1):
+    return ParamsT(sigma_inner, sigma_boundary, beta, boundary, vol_order, face_order, 0)
+
+
+def assemble(grid, kappa, A, prm, elem_index=None, pattern=None):
+    """Monolithic SWIPDG component matrix (CSR arrays).  elem_index permutes element numbering."""
+    ei = None if elem_index is None else np.ascontiguousarray(elem_index, np.int64)
+    row_ptr, col = pattern if pattern is not None else grid.pattern(ei)
+    val = np.empty(col.shape[0], np.float64)
+    lib().or_assemble_swipdg(grid.h, C.byref(kappa), C.byref(A), C.byref(prm), _ptr(ei), _ptr(row_ptr),
+                             _ptr(col), _ptr(val))
+    return row_ptr, col, val
+
+
+def block_numbering(grid, subdomain, n_sub):
+    sd = np.ascontiguousarray(subdomain, np.int32)
+    ei = np.empty(grid.ne, np.int64)
+    lib().or_block_numbering(grid.h, _ptr(sd), int(n_sub), _ptr(ei))
+    return ei
+
+
+def assemble_block(grid, subdomain, n_sub, kappa, A, prm):
+    """BlockSWIPDG global matrix in block numbering; returns (elem_index, row_ptr, col, val)."""
+    sd = np.ascontiguousarray(subdomain, np.int32)
+    ei = block_numbering(grid, sd, n_sub)
+    row_ptr, col = grid.pattern(ei)
+    val = np.empty(col.shape[0], np.float64)
+    lib().or_assemble_block_swipdg(grid.h, _ptr(sd), int(n_sub), C.byref(kappa), C.byref(A), C.byref(prm),
+                                   _ptr(ei), _ptr(row_ptr), _ptr(col), _ptr(val))
+    return ei, row_ptr, col, val
+
+
+def rhs_esv2007(grid, elem_index=None, force_order=3):
+    b = np.empty(grid.ne * grid.nb, np.float64)
+    ei = None if elem_index is None else np.ascontiguousarray(elem_index, np.int64)
+    lib().or_rhs_l2(grid.h, 0, force_order, _ptr(ei), _ptr(b))
+    return b
+
+
+def error_norms_esv2007(grid, u, elem_index=None, order=10):
+    u = np.ascontiguousarray(u, np.float64)
+    ei = None if elem_index is None else np.ascontiguousarray(elem_index, np.int64)
+    l2, h1 = C.c_double(), C.c_double()
+    lib().or_error_norms_esv2007(grid.h, _ptr(u), _ptr(ei), order, C.byref(l2), C.byref(h1))
+    return l2.value, h1.value
+
+
+def quadrature(elem_type, order):
+    x = np.empty((256, 2)); w = np.empty(256)
+    n = lib().or_quadrature(elem_type, order, _ptr(x), _ptr(w))
+    return x[:n].copy(), w[:n].copy()
+
+
+def to_scipy(row_ptr, col, val, n=None):
+    import scipy.sparse as sp
+    n = n or (row_ptr.shape[0] - 1)
+    return sp.csr_matrix((val, col, row_ptr), shape=(row_ptr.shape[0] - 1, n))
+
+
+def esv2007_eoc(grid, prm, elem_index=None):
+    """Assemble + solve ESV2007 (kappa=1, A=I, f = 1/2 pi^2 cos cos, AllDirichlet) and return the error
+    norms (L2, H1 semi) -- the solution-level quantities test/linearelliptic-swipdg.hh:267-290 computes."""
+    import scipy.sparse.linalg as spla
+    rp, col, val = assemble(grid, scalar(FN_CONST, 1.0), tensor(TENSOR_CONST), prm, elem_index)
+    A = to_scipy(rp, col, val)
+    b = rhs_esv2007(grid, elem_index)
+    u = spla.spsolve(A.tocsc(), b)
+    return error_norms_esv2007(grid, u, elem_index)

@@ -1,0 +1,706 @@
+/*
+ * oracle/swipdg_oracle.c -- CPU restatement of dune-hdd's SWIPDG stiffness assembly.
+ *
+ *   *** TEST INFRASTRUCTURE ONLY ***
+ *   Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this library,
+ *   and only as the checker / the timed CPU baseline.  The product (dune-hdd_amd/) never links it.
+ *
+ * What it restates (reference paths under /root/reference):
+ *   - SWIPDG::init() LHS part: one EllipticSWIPDG operator per diffusion-factor component, all on one
+ *     shared pattern, walked by SystemAssembler::walk()
+ *       dune/hdd/linearelliptic/discretizations/swipdg.hh:222-249, 485
+ *   - the pattern: volume + face couplings of every element   swipdg.hh:169
+ *   - BlockSWIPDG::init(): local SWIPDG per subdomain (all-Neumann), Dirichlet boundary terms on
+ *     domain-boundary subdomains, SWIPDG::Inner coupling terms written into 4 matrices, copied to
+ *     the global block numbering
+ *       dune/hdd/linearelliptic/discretizations/block-swipdg.hh:262-390, 1036-1099, 1136-1179, 1270-1379
+ *   - the third-party integrands the reference delegates to (dune-gdt >= 0.2, version unpinned:
+ *     dune.module:9-10), restated from the SWIPDG method definition:
+ *       LocalEvaluation::Elliptic         (volume)
+ *       LocalEvaluation::SWIPDG::Inner    (interior face, 4 blocks)      block-swipdg.hh:1292-1294
+ *       LocalEvaluation::SWIPDG::BoundaryLHS (Dirichlet face)            block-swipdg.hh:1158-1160
+ *   - the RHS L2 volume functional and error norms, used ONLY to pin this oracle against the
+ *     reference's expectation tables (test/linearelliptic-swipdg-expectations_*.cxx).
+ *
+ * Algorithmic style deliberately follows the reference: a sequential element walk, per-element and
+ * per-intersection local matrices evaluated by quadrature with basis functions evaluated at points
+ * mapped through the element geometries (geometryInInside / geometryInOutside), and a scatter of every
+ * local entry through add_to_entry() = a binary search in the sorted CSR row (Eigen coeffRef-like).
+ * Face adjacency is derived here from element->vertex connectivity (independent of the product's face
+ * tables).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "swipdg_oracle.h"
+
+/* ------------------------------------------------------------------------------------------------ */
+/* Dune reference elements (dune-geometry numbering)                                                 */
+/* ------------------------------------------------------------------------------------------------ */
+/* simplex 2d: vertices (0,0),(1,0),(0,1); faces 0:(0,1) 1:(0,2) 2:(1,2) */
+static const double SIMPLEX_V[3][2] = {{0, 0}, {1, 0}, {0, 1}};
+static const int SIMPLEX_F[3][2] = {{0, 1}, {0, 2}, {1, 2}};
+/* cube 2d: vertices (0,0),(1,0),(0,1),(1,1); faces 0:(0,2) x=0, 1:(1,3) x=1, 2:(0,1) y=0, 3:(2,3) y=1 */
+static const double CUBE_V[4][2] = {{0, 0}, {1, 0}, {0, 1}, {1, 1}};
+static const int CUBE_F[4][2] = {{0, 2}, {1, 3}, {0, 1}, {2, 3}};
+/* reference outer normals (unnormalised) */
+static const double SIMPLEX_N[3][2] = {{0, -1}, {-1, 0}, {1, 1}};
+static const double CUBE_N[4][2] = {{-1, 0}, {1, 0}, {0, -1}, {0, 1}};
+
+static int nvpe_of(int t) { return t == OR_SIMPLEX ? 3 : 4; }
+static int nfaces_of(int t) { return t == OR_SIMPLEX ? 3 : 4; }
+
+/* P1 / Q1 Lagrange shape functions on the reference element (dune-fem ordering = vertex ordering). */
+static void shape(int t, const double* xh, double* phi, double (*grad)[2])
+{
+  const double x = xh[0], y = xh[1];
+  if (t == OR_SIMPLEX) {
+    phi[0] = 1.0 - x - y; phi[1] = x; phi[2] = y;
+    grad[0][0] = -1; grad[0][1] = -1;
+    grad[1][0] = 1;  grad[1][1] = 0;
+    grad[2][0] = 0;  grad[2][1] = 1;
+  } else {
+    phi[0] = (1 - x) * (1 - y); phi[1] = x * (1 - y); phi[2] = (1 - x) * y; phi[3] = x * y;
+    grad[0][0] = -(1 - y); grad[0][1] = -(1 - x);
+    grad[1][0] = (1 - y);  grad[1][1] = -x;
+    grad[2][0] = -y;       grad[2][1] = (1 - x);
+    grad[3][0] = y;        grad[3][1] = x;
+  }
+}
+
+/* ------------------------------------------------------------------------------------------------ */
+/* Quadrature                                                                                         */
+/* ------------------------------------------------------------------------------------------------ */
+#define OR_MAXQ 256
+typedef struct { int n; double x[OR_MAXQ][2]; double w[OR_MAXQ]; } quad2_t;
+typedef struct { int n; double s[32]; double w[32]; } quad1_t;
+
+/* Gauss-Legendre on [0,1] with n points (Newton on P_n) */
+static void gauss_legendre01(int n, double* s, double* w)
+{
+  for (int i = 0; i < n; ++i) {
+    double x = cos(M_PI * (i + 0.75) / (n + 0.5));
+    for (int it = 0; it < 100; ++it) {
+      double p0 = 1.0, p1 = x;
+      for (int k = 2; k <= n; ++k) { double p2 = ((2.0 * k - 1) * x * p1 - (k - 1.0) * p0) / k; p0 = p1; p1 = p2; }
+      if (n == 1) { p1 = x; p0 = 1.0; }
+      const double dp = n * (x * p1 - p0) / (x * x - 1.0);
+      const double dx = p1 / dp;
+      x -= dx;
+      if (fabs(dx) < 1e-16) break;
+    }
+    double p0 = 1.0, p1 = x;
+    for (int k = 2; k <= n; ++k) { double p2 = ((2.0 * k - 1) * x * p1 - (k - 1.0) * p0) / k; p0 = p1; p1 = p2; }
+    if (n == 1) { p1 = x; p0 = 1.0; }
+    const double dp = n * (x * p1 - p0) / (x * x - 1.0);
+    s[n - 1 - i] = 0.5 * (x + 1.0);
+    w[n - 1 - i] = 1.0 / ((1.0 - x * x) * dp * dp);   /* 2/((1-x^2)P'^2) scaled by 1/2 */
+  }
+}
+
+/* line rule of given polynomial order: Gauss with ceil((order+1)/2) points (Dune's Gauss-Legendre family) */
+static void line_rule(int order, quad1_t* q)
+{
+  int n = (order + 2) / 2;
+  if (n < 1) n = 1;
+  q->n = n;
+  gauss_legendre01(n, q->s, q->w);
+}
+
+/* simplex rules (reference triangle, area 1/2):
+ *   order <= 1 : centroid (exact for P1 gradients, Dune's order-0/1 choice)
+ *   order == 2 : 3-point interior rule
+ *   order 3..4 : 6-point degree-4 rule (Dunavant)
+ *   higher     : collapsed (Duffy) Gauss-Legendre product rule
+ * The Dune simplex tables for order >= 2 are not available here; for the path's p=1 / piecewise-constant
+ * coefficient configurations only the centroid and line rules matter (all exact).  For OS2014's smooth
+ * coefficient, parity is declared against THIS rule (SURVEY.md 8(c) hard part (ii)). */
+static const double DUN4_A = 0.44594849091596488632, DUN4_WA = 0.22338158967801146570;
+static const double DUN4_B = 0.091576213509770743460, DUN4_WB = 0.10995174365532186764;
+
+static void simplex_rule(int order, quad2_t* q)
+{
+  if (order <= 1) {
+    q->n = 1; q->x[0][0] = q->x[0][1] = 1.0 / 3.0; q->w[0] = 0.5;
+  } else if (order == 2) {
+    q->n = 3;
+    const double a = 1.0 / 6.0, b = 2.0 / 3.0;
+    q->x[0][0] = a; q->x[0][1] = a;
+    q->x[1][0] = b; q->x[1][1] = a;
+    q->x[2][0] = a; q->x[2][1] = b;
+    q->w[0] = q->w[1] = q->w[2] = 1.0 / 6.0;
+  } else if (order <= 4) {
+    q->n = 6;
+    const double a = DUN4_A, b = DUN4_B;
+    const double pa[3][2] = {{a, a}, {1 - 2 * a, a}, {a, 1 - 2 * a}};
+    const double pb[3][2] = {{b, b}, {1 - 2 * b, b}, {b, 1 - 2 * b}};
+    for (int k = 0; k < 3; ++k) {
+      q->x[k][0] = pa[k][0]; q->x[k][1] = pa[k][1]; q->w[k] = 0.5 * DUN4_WA;
+      q->x[3 + k][0] = pb[k][0]; q->x[3 + k][1] = pb[k][1]; q->w[3 + k] = 0.5 * DUN4_WB;
+    }
+  } else {
+    int n = (order + 3) / 2;
+    if (n > 16) n = 16;
+    double s[32], w[32];
+    gauss_legendre01(n, s, w);
+    q->n = n * n;
+    int k = 0;
+    for (int i = 0; i < n; ++i)
+      for (int j = 0; j < n; ++j, ++k) {
+        /* Duffy: x = u, y = v (1-u) */
+        q->x[k][0] = s[i];
+        q->x[k][1] = s[j] * (1.0 - s[i]);
+        q->w[k] = w[i] * w[j] * (1.0 - s[i]);
+      }
+  }
+}
+
+static void cube_rule(int order, quad2_t* q)
+{
+  quad1_t l;
+  line_rule(order, &l);
+  if (l.n > 16) l.n = 16;
+  q->n = l.n * l.n;
+  int k = 0;
+  for (int j = 0; j < l.n; ++j)
+    for (int i = 0; i < l.n; ++i, ++k) {
+      q->x[k][0] = l.s[i]; q->x[k][1] = l.s[j]; q->w[k] = l.w[i] * l.w[j];
+    }
+}
+
+static void volume_rule(int t, int order, quad2_t* q)
+{
+  if (t == OR_SIMPLEX) simplex_rule(order, q); else cube_rule(order, q);
+}
+
+int or_quadrature(int elem_type, int order, double* x, double* w)
+{
+  quad2_t q;
+  volume_rule(elem_type, order, &q);
+  for (int k = 0; k < q.n; ++k) { x[2 * k] = q.x[k][0]; x[2 * k + 1] = q.x[k][1]; w[k] = q.w[k]; }
+  return q.n;
+}
+
+/* ------------------------------------------------------------------------------------------------ */
+/* Grid: geometry and intersections derived from element->vertex connectivity                        */
+/* ------------------------------------------------------------------------------------------------ */
+typedef struct {
+  int type, nvpe, nf, nb;
+  int64_t nv, ne;
+  const double* coords;
+  const int32_t* ev;
+  int64_t* nbr;       /* [ne*nf] neighbour element or -1 on the domain boundary */
+  int8_t* nbr_face;   /* [ne*nf] local face index inside the neighbour */
+} grid_t;
+
+typedef struct { int64_t key; int64_t ef; } edge_rec_t;
+
+static int cmp_edge(const void* a, const void* b)
+{
+  const edge_rec_t* x = (const edge_rec_t*)a; const edge_rec_t* y = (const edge_rec_t*)b;
+  if (x->key != y->key) return x->key < y->key ? -1 : 1;
+  return x->ef < y->ef ? -1 : (x->ef > y->ef);
+}
+
+void* or_grid_create(const or_mesh_t* m)
+{
+  grid_t* g = (grid_t*)calloc(1, sizeof(grid_t));
+  g->type = m->elem_type;
+  g->nvpe = nvpe_of(m->elem_type);
+  g->nf = nfaces_of(m->elem_type);
+  g->nb = g->nvpe;                              /* p = 1 Lagrange: one DoF per vertex */
+  g->nv = m->n_vertices; g->ne = m->n_elements;
+  g->coords = m->coords; g->ev = m->elem_vert;
+  const int (*F)[2] = g->type == OR_SIMPLEX ? SIMPLEX_F : CUBE_F;
+  const int64_t nrec = g->ne * g->nf;
+  edge_rec_t* rec = (edge_rec_t*)malloc(sizeof(edge_rec_t) * (size_t)nrec);
+  for (int64_t e = 0; e < g->ne; ++e)
+    for (int f = 0; f < g->nf; ++f) {
+      int64_t a = g->ev[e * g->nvpe + F[f][0]], b = g->ev[e * g->nvpe + F[f][1]];
+      if (a > b) { int64_t t = a; a = b; b = t; }
+      rec[e * g->nf + f].key = a * g->nv + b;
+      rec[e * g->nf + f].ef = e * g->nf + f;
+    }
+  qsort(rec, (size_t)nrec, sizeof(edge_rec_t), cmp_edge);
+  g->nbr = (int64_t*)malloc(sizeof(int64_t) * (size_t)nrec);
+  g->nbr_face = (int8_t*)malloc((size_t)nrec);
+  for (int64_t i = 0; i < nrec; ++i) { g->nbr[i] = -1; g->nbr_face[i] = -1; }
+  for (int64_t i = 0; i < nrec;) {
+    int64_t j = i + 1;
+    while (j < nrec && rec[j].key == rec[i].key) ++j;
+    if (j - i == 2) {
+      const int64_t p = rec[i].ef, q = rec[i + 1].ef;
+      g->nbr[p] = q / g->nf; g->nbr_face[p] = (int8_t)(q % g->nf);
+      g->nbr[q] = p / g->nf; g->nbr_face[q] = (int8_t)(p % g->nf);
+    }
+    i = j;
+  }
+  free(rec);
+  return g;
+}
+
+void or_grid_destroy(void* gp)
+{
+  grid_t* g = (grid_t*)gp;
+  if (!g) return;
+  free(g->nbr); free(g->nbr_face); free(g);
+}
+
+int64_t or_grid_neighbor(void* gp, int64_t e, int f) { grid_t* g = (grid_t*)gp; return g->nbr[e * g->nf + f]; }
+int or_grid_neighbor_face(void* gp, int64_t e, int f) { grid_t* g = (grid_t*)gp; return g->nbr_face[e * g->nf + f]; }
+
+/* affine geometry of element e: x = v0 + J xh (J columns: v1-v0, v2-v0; parallelograms for cubes) */
+typedef struct { double v0[2]; double J[2][2]; double Jinv[2][2]; double det; } geom_t;
+
+static void geometry(const grid_t* g, int64_t e, geom_t* G)
+{
+  const int32_t* v = g->ev + e * g->nvpe;
+  const double* c0 = g->coords + 2 * (int64_t)v[0];
+  const double* c1 = g->coords + 2 * (int64_t)v[1];
+  const double* c2 = g->coords + 2 * (int64_t)v[2];
+  G->v0[0] = c0[0]; G->v0[1] = c0[1];
+  G->J[0][0] = c1[0] - c0[0]; G->J[0][1] = c2[0] - c0[0];
+  G->J[1][0] = c1[1] - c0[1]; G->J[1][1] = c2[1] - c0[1];
+  G->det = G->J[0][0] * G->J[1][1] - G->J[0][1] * G->J[1][0];
+  const double id = 1.0 / G->det;
+  G->Jinv[0][0] = G->J[1][1] * id; G->Jinv[0][1] = -G->J[0][1] * id;
+  G->Jinv[1][0] = -G->J[1][0] * id; G->Jinv[1][1] = G->J[0][0] * id;
+}
+
+static void global_pt(const geom_t* G, const double* xh, double* x)
+{
+  x[0] = G->v0[0] + G->J[0][0] * xh[0] + G->J[0][1] * xh[1];
+  x[1] = G->v0[1] + G->J[1][0] * xh[0] + G->J[1][1] * xh[1];
+}
+
+static void local_pt(const geom_t* G, const double* x, double* xh)
+{
+  const double d0 = x[0] - G->v0[0], d1 = x[1] - G->v0[1];
+  xh[0] = G->Jinv[0][0] * d0 + G->Jinv[0][1] * d1;
+  xh[1] = G->Jinv[1][0] * d0 + G->Jinv[1][1] * d1;
+}
+
+/* physical gradient = J^{-T} reference gradient */
+static void map_grad(const geom_t* G, const double* gh, double* gp)
+{
+  gp[0] = G->Jinv[0][0] * gh[0] + G->Jinv[1][0] * gh[1];
+  gp[1] = G->Jinv[0][1] * gh[0] + G->Jinv[1][1] * gh[1];
+}
+
+/* ------------------------------------------------------------------------------------------------ */
+/* Coefficient evaluation (dune-stuff local functions)                                               */
+/* ------------------------------------------------------------------------------------------------ */
+static double eval_scalar(const or_scalar_t* s, int64_t e, const double* x)
+{
+  switch (s->kind) {
+    case OR_FN_CONST: return s->c;
+    case OR_FN_PER_ELEM: return s->per_elem[e];
+    case OR_FN_SINUSOID: return s->c + s->b * sin(s->kx * x[0] + s->ky * x[1]);
+    default: return 0.0;
+  }
+}
+
+static void eval_tensor(const or_tensor_t* t, int64_t e, double A[2][2])
+{
+  switch (t->kind) {
+    case OR_TENSOR_CONST: A[0][0] = t->c[0]; A[0][1] = A[1][0] = t->c[1]; A[1][1] = t->c[2]; break;
+    case OR_TENSOR_ISO_PER_ELEM: A[0][0] = A[1][1] = t->per_elem[e]; A[0][1] = A[1][0] = 0.0; break;
+    case OR_TENSOR_SYM_PER_ELEM:
+      A[0][0] = t->per_elem[3 * e]; A[0][1] = A[1][0] = t->per_elem[3 * e + 1]; A[1][1] = t->per_elem[3 * e + 2];
+      break;
+    default: A[0][0] = A[1][1] = 1.0; A[0][1] = A[1][0] = 0.0;
+  }
+}
+
+static int scalar_order(const or_scalar_t* s) { return s->kind == OR_FN_SINUSOID ? s->order : 0; }
+static const int TENSOR_ORDER = 0;   /* all supported tensors are piecewise constant */
+
+/* ------------------------------------------------------------------------------------------------ */
+/* Pattern and scatter                                                                                */
+/* ------------------------------------------------------------------------------------------------ */
+static inline int64_t gid_of(const int64_t* elem_index, int64_t e) { return elem_index ? elem_index[e] : e; }
+
+/* rows = DoFs (gid*nb + i); row of element e: DoFs of e and of every face neighbour, sorted ascending */
+int64_t or_pattern_nnz(void* gp)
+{
+  grid_t* g = (grid_t*)gp;
+  int64_t nnz = 0;
+  for (int64_t e = 0; e < g->ne; ++e) {
+    int blocks = 1;
+    for (int f = 0; f < g->nf; ++f) blocks += g->nbr[e * g->nf + f] >= 0;
+    nnz += (int64_t)g->nb * g->nb * blocks;
+  }
+  return nnz;
+}
+
+int or_pattern(void* gp, const int64_t* elem_index, int64_t* row_ptr, int32_t* col)
+{
+  grid_t* g = (grid_t*)gp;
+  const int nb = g->nb;
+  /* row lengths in gid order */
+  int64_t* len = (int64_t*)calloc((size_t)g->ne, sizeof(int64_t));
+  int64_t* inv = (int64_t*)malloc(sizeof(int64_t) * (size_t)g->ne);
+  for (int64_t e = 0; e < g->ne; ++e) {
+    int blocks = 1;
+    for (int f = 0; f < g->nf; ++f) blocks += g->nbr[e * g->nf + f] >= 0;
+    len[gid_of(elem_index, e)] = blocks;
+    inv[gid_of(elem_index, e)] = e;
+  }
+  row_ptr[0] = 0;
+  for (int64_t k = 0; k < g->ne; ++k)
+    for (int i = 0; i < nb; ++i)
+      row_ptr[k * nb + i + 1] = row_ptr[k * nb + i] + len[k] * nb;
+  for (int64_t k = 0; k < g->ne; ++k) {
+    const int64_t e = inv[k];
+    int64_t blk[9]; int nblk = 0;
+    blk[nblk++] = k;
+    for (int f = 0; f < g->nf; ++f) {
+      const int64_t n = g->nbr[e * g->nf + f];
+      if (n >= 0) blk[nblk++] = gid_of(elem_index, n);
+    }
+    for (int a = 1; a < nblk; ++a)          /* insertion sort */
+      for (int b = a; b > 0 && blk[b - 1] > blk[b]; --b) { int64_t t = blk[b]; blk[b] = blk[b - 1]; blk[b - 1] = t; }
+    for (int i = 0; i < nb; ++i) {
+      int32_t* c = col + row_ptr[k * nb + i];
+      for (int b = 0; b < nblk; ++b)
+        for (int j = 0; j < nb; ++j) *c++ = (int32_t)(blk[b] * nb + j);
+    }
+  }
+  free(len); free(inv);
+  return 0;
+}
+
+/* Stuff::LA add_to_entry: locate (row, col) in the sorted CSR row and accumulate */
+static inline void add_to_entry(const int64_t* row_ptr, const int32_t* col, double* val, int64_t r, int64_t c,
+                                double v)
+{
+  int64_t lo = row_ptr[r], hi = row_ptr[r + 1] - 1;
+  while (lo <= hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (col[mid] == c) { val[mid] += v; return; }
+    if (col[mid] < c) lo = mid + 1; else hi = mid - 1;
+  }
+  /* not in pattern: the reference throws here; the oracle records it as NaN to make tests fail loudly */
+  val[row_ptr[r]] = NAN;
+}
+
+/* ------------------------------------------------------------------------------------------------ */
+/* Local integrands                                                                                  */
+/* ------------------------------------------------------------------------------------------------ */
+typedef struct {
+  const grid_t* g;
+  const or_scalar_t* kappa;
+  const or_tensor_t* A;
+  const or_params_t* p;
+  const int64_t* elem_index;
+  const int64_t* row_ptr;
+  const int32_t* col;
+  double* val;
+} ctx_t;
+
+static void scatter(const ctx_t* c, int64_t te, int64_t ae, double L[4][4])
+{
+  const int nb = c->g->nb;
+  const int64_t tg = gid_of(c->elem_index, te), ag = gid_of(c->elem_index, ae);
+  for (int i = 0; i < nb; ++i)
+    for (int j = 0; j < nb; ++j) add_to_entry(c->row_ptr, c->col, c->val, tg * nb + i, ag * nb + j, L[i][j]);
+}
+
+/* LocalEvaluation::Elliptic: a_ij = sum_q w_q |det J| kappa(x_q) (A grad phi_j) . grad phi_i
+ * integrand order = ord(kappa) + ord(A) + (p-1) + (p-1)  [p = 1] */
+static void local_volume(const ctx_t* c, int64_t e, double L[4][4])
+{
+  const grid_t* g = c->g;
+  geom_t G; geometry(g, e, &G);
+  double A[2][2]; eval_tensor(c->A, e, A);
+  int order = scalar_order(c->kappa) + TENSOR_ORDER + 0 + 0;
+  if (c->p->vol_order_override >= 0) order = c->p->vol_order_override;
+  quad2_t q; volume_rule(g->type, order, &q);
+  memset(L, 0, sizeof(double) * 16);
+  for (int k = 0; k < q.n; ++k) {
+    double phi[4], gh[4][2], gp[4][2], x[2];
+    shape(g->type, q.x[k], phi, gh);
+    global_pt(&G, q.x[k], x);
+    for (int i = 0; i < g->nb; ++i) map_grad(&G, gh[i], gp[i]);
+    const double kap = eval_scalar(c->kappa, e, x);
+    const double fac = q.w[k] * fabs(G.det);
+    for (int i = 0; i < g->nb; ++i)
+      for (int j = 0; j < g->nb; ++j) {
+        const double Agj0 = A[0][0] * gp[j][0] + A[0][1] * gp[j][1];
+        const double Agj1 = A[1][0] * gp[j][0] + A[1][1] * gp[j][1];
+        L[i][j] += fac * kap * (Agj0 * gp[i][0] + Agj1 * gp[i][1]);
+      }
+  }
+}
+
+/* face geometry seen from the inside element e, local face f */
+typedef struct { double xa[2], xb[2]; double len; double n[2]; double ra[2], rb[2]; } face_t;
+
+static void face_geometry(const grid_t* g, const geom_t* G, int f, face_t* F)
+{
+  const double (*RV)[2] = g->type == OR_SIMPLEX ? SIMPLEX_V : CUBE_V;
+  const int (*FV)[2] = g->type == OR_SIMPLEX ? SIMPLEX_F : CUBE_F;
+  const double (*RN)[2] = g->type == OR_SIMPLEX ? SIMPLEX_N : CUBE_N;
+  F->ra[0] = RV[FV[f][0]][0]; F->ra[1] = RV[FV[f][0]][1];
+  F->rb[0] = RV[FV[f][1]][0]; F->rb[1] = RV[FV[f][1]][1];
+  global_pt(G, F->ra, F->xa);
+  global_pt(G, F->rb, F->xb);
+  F->len = hypot(F->xb[0] - F->xa[0], F->xb[1] - F->xa[1]);
+  double n[2]; map_grad(G, RN[f], n);     /* normals transform with J^{-T} */
+  const double nn = hypot(n[0], n[1]);
+  F->n[0] = n[0] / nn; F->n[1] = n[1] / nn;
+}
+
+/* SWIPDG::Inner on the face f of entity e with neighbour ne; returns the 4 local blocks */
+static void local_inner(const ctx_t* c, int64_t e, int f, int64_t ne, double EE[4][4], double EN[4][4],
+                        double NE[4][4], double NN[4][4])
+{
+  const grid_t* g = c->g;
+  const int nb = g->nb;
+  geom_t Gi, Go; geometry(g, e, &Gi); geometry(g, ne, &Go);
+  face_t F; face_geometry(g, &Gi, f, &F);
+  double Ai[2][2], Ao[2][2]; eval_tensor(c->A, e, Ai); eval_tensor(c->A, ne, Ao);
+  /* integrand order: max(ord kappa) + max(ord A) + max(test order) + max(ansatz order) */
+  int order = scalar_order(c->kappa) + TENSOR_ORDER + 1 + 1;
+  if (c->p->face_order_override >= 0) order = c->p->face_order_override;
+  quad1_t q; line_rule(order, &q);
+  memset(EE, 0, sizeof(double) * 16); memset(EN, 0, sizeof(double) * 16);
+  memset(NE, 0, sizeof(double) * 16); memset(NN, 0, sizeof(double) * 16);
+  const double sigma = c->p->sigma_inner;
+  const double* n = F.n;
+  /* weights (Ern, Stephansen, Zunino 2007) */
+  const double delta_plus = n[0] * (Ao[0][0] * n[0] + Ao[0][1] * n[1]) + n[1] * (Ao[1][0] * n[0] + Ao[1][1] * n[1]);
+  const double delta_minus = n[0] * (Ai[0][0] * n[0] + Ai[0][1] * n[1]) + n[1] * (Ai[1][0] * n[0] + Ai[1][1] * n[1]);
+  const double gamma = (delta_plus * delta_minus) / (delta_plus + delta_minus);
+  const double weight_plus = delta_minus / (delta_plus + delta_minus);
+  const double weight_minus = delta_plus / (delta_plus + delta_minus);
+  const double hpow = pow(F.len, c->p->beta);
+  for (int k = 0; k < q.n; ++k) {
+    const double s = q.s[k];
+    /* geometryInInside / geometryInOutside */
+    double xin[2] = {F.ra[0] + s * (F.rb[0] - F.ra[0]), F.ra[1] + s * (F.rb[1] - F.ra[1])};
+    double x[2]; global_pt(&Gi, xin, x);
+    double xout[2]; local_pt(&Go, x, xout);
+    double pe[4], ge_h[4][2], ge[4][2], pn[4], gn_h[4][2], gn[4][2];
+    shape(g->type, xin, pe, ge_h);
+    shape(g->type, xout, pn, gn_h);
+    for (int i = 0; i < nb; ++i) { map_grad(&Gi, ge_h[i], ge[i]); map_grad(&Go, gn_h[i], gn[i]); }
+    const double ke = eval_scalar(c->kappa, e, x), kn = eval_scalar(c->kappa, ne, x);
+    const double penalty = (ke * kn * sigma * gamma) / hpow;
+    const double fac = q.w[k] * F.len;    /* quadrature weight * integration element */
+    double Age_n[4], Agn_n[4];            /* (A grad phi) . n */
+    for (int i = 0; i < nb; ++i) {
+      Age_n[i] = (Ai[0][0] * ge[i][0] + Ai[0][1] * ge[i][1]) * n[0] + (Ai[1][0] * ge[i][0] + Ai[1][1] * ge[i][1]) * n[1];
+      Agn_n[i] = (Ao[0][0] * gn[i][0] + Ao[0][1] * gn[i][1]) * n[0] + (Ao[1][0] * gn[i][0] + Ao[1][1] * gn[i][1]) * n[1];
+    }
+    for (int i = 0; i < nb; ++i)
+      for (int j = 0; j < nb; ++j) {
+        /* entity/entity: consistency, symmetry, penalty */
+        EE[i][j] += fac * (-weight_minus * ke * Age_n[j] * pe[i] - weight_minus * ke * pe[j] * Age_n[i] + penalty * pe[j] * pe[i]);
+        /* entity/neighbour (test on entity, ansatz on neighbour) */
+        EN[i][j] += fac * (-weight_plus * kn * Agn_n[j] * pe[i] + weight_minus * ke * pn[j] * Age_n[i] - penalty * pn[j] * pe[i]);
+        /* neighbour/entity */
+        NE[i][j] += fac * (weight_minus * ke * Age_n[j] * pn[i] - weight_plus * kn * pe[j] * Agn_n[i] - penalty * pe[j] * pn[i]);
+        /* neighbour/neighbour */
+        NN[i][j] += fac * (weight_plus * kn * Agn_n[j] * pn[i] + weight_plus * kn * pn[j] * Agn_n[i] + penalty * pn[j] * pn[i]);
+      }
+  }
+}
+
+/* SWIPDG::BoundaryLHS on the Dirichlet face f of e */
+static void local_boundary(const ctx_t* c, int64_t e, int f, double L[4][4])
+{
+  const grid_t* g = c->g;
+  const int nb = g->nb;
+  geom_t G; geometry(g, e, &G);
+  face_t F; face_geometry(g, &G, f, &F);
+  double A[2][2]; eval_tensor(c->A, e, A);
+  int order = scalar_order(c->kappa) + TENSOR_ORDER + 1 + 1;
+  if (c->p->face_order_override >= 0) order = c->p->face_order_override;
+  quad1_t q; line_rule(order, &q);
+  memset(L, 0, sizeof(double) * 16);
+  const double* n = F.n;
+  const double gamma = n[0] * (A[0][0] * n[0] + A[0][1] * n[1]) + n[1] * (A[1][0] * n[0] + A[1][1] * n[1]);
+  const double hpow = pow(F.len, c->p->beta);
+  for (int k = 0; k < q.n; ++k) {
+    const double s = q.s[k];
+    double xin[2] = {F.ra[0] + s * (F.rb[0] - F.ra[0]), F.ra[1] + s * (F.rb[1] - F.ra[1])};
+    double x[2]; global_pt(&G, xin, x);
+    double ph[4], gh[4][2], gp[4][2];
+    shape(g->type, xin, ph, gh);
+    for (int i = 0; i < nb; ++i) map_grad(&G, gh[i], gp[i]);
+    const double kap = eval_scalar(c->kappa, e, x);
+    const double penalty = (c->p->sigma_boundary * kap * gamma) / hpow;
+    const double fac = q.w[k] * F.len;
+    double Ag_n[4];
+    for (int i = 0; i < nb; ++i)
+      Ag_n[i] = (A[0][0] * gp[i][0] + A[0][1] * gp[i][1]) * n[0] + (A[1][0] * gp[i][0] + A[1][1] * gp[i][1]) * n[1];
+    for (int i = 0; i < nb; ++i)
+      for (int j = 0; j < nb; ++j)
+        L[i][j] += fac * (-kap * Ag_n[j] * ph[i] - kap * ph[j] * Ag_n[i] + penalty * ph[j] * ph[i]);
+  }
+}
+
+/* ------------------------------------------------------------------------------------------------ */
+/* Monolithic SWIPDG walk (SystemAssembler::walk with EllipticSWIPDG, swipdg.hh:218-249, 485)         */
+/* ------------------------------------------------------------------------------------------------ */
+int or_assemble_swipdg(void* gp, const or_scalar_t* kappa, const or_tensor_t* A, const or_params_t* p,
+                       const int64_t* elem_index, const int64_t* row_ptr, const int32_t* col, double* val)
+{
+  grid_t* g = (grid_t*)gp;
+  ctx_t c = {g, kappa, A, p, elem_index, row_ptr, col, val};
+  memset(val, 0, sizeof(double) * (size_t)row_ptr[g->ne * g->nb]);
+  double L[4][4], EN[4][4], NE[4][4], NN[4][4];
+  for (int64_t e = 0; e < g->ne; ++e) {
+    local_volume(&c, e, L);                               /* codim 0 */
+    scatter(&c, e, e, L);
+    for (int f = 0; f < g->nf; ++f) {                      /* codim 1 */
+      const int64_t ne = g->nbr[e * g->nf + f];
+      if (ne >= 0) {
+        /* ApplyOn::InnerIntersectionsPrimally: inside index < outside index */
+        if (e < ne) {
+          local_inner(&c, e, f, ne, L, EN, NE, NN);
+          scatter(&c, e, e, L); scatter(&c, e, ne, EN); scatter(&c, ne, e, NE); scatter(&c, ne, ne, NN);
+        }
+      } else if (p->boundary_kind == OR_BOUNDARY_DIRICHLET) {
+        local_boundary(&c, e, f, L);
+        scatter(&c, e, e, L);
+      }
+    }
+  }
+  return 0;
+}
+
+/* ------------------------------------------------------------------------------------------------ */
+/* BlockSWIPDG (block-swipdg.hh:262-390): local all-Neumann SWIPDG per subdomain + boundary + coupling */
+/* ------------------------------------------------------------------------------------------------ */
+/* block numbering: subdomain offsets, local index = order of the element inside its subdomain's grid
+ * part (which preserves the global element order); mapToGlobal(ss, ii) = offset(ss) + ii. */
+int or_block_numbering(void* gp, const int32_t* subdomain, int32_t n_sub, int64_t* elem_index)
+{
+  grid_t* g = (grid_t*)gp;
+  int64_t* cnt = (int64_t*)calloc((size_t)n_sub + 1, sizeof(int64_t));
+  for (int64_t e = 0; e < g->ne; ++e) cnt[subdomain[e] + 1]++;
+  for (int32_t s = 0; s < n_sub; ++s) cnt[s + 1] += cnt[s];
+  for (int64_t e = 0; e < g->ne; ++e) elem_index[e] = cnt[subdomain[e]]++;
+  free(cnt);
+  return 0;
+}
+
+int or_assemble_block_swipdg(void* gp, const int32_t* subdomain, int32_t n_sub, const or_scalar_t* kappa,
+                             const or_tensor_t* A, const or_params_t* p, const int64_t* elem_index,
+                             const int64_t* row_ptr, const int32_t* col, double* val)
+{
+  grid_t* g = (grid_t*)gp;
+  ctx_t c = {g, kappa, A, p, elem_index, row_ptr, col, val};
+  memset(val, 0, sizeof(double) * (size_t)row_ptr[g->ne * g->nb]);
+  double L[4][4], EN[4][4], NE[4][4], NN[4][4];
+  /* walk 1: local discretizations (volume + faces inside the subdomain; the local boundary is
+   * all-Neumann => no boundary terms), block-swipdg.hh:271-327 / 106-129 */
+  for (int32_t ss = 0; ss < n_sub; ++ss)
+    for (int64_t e = 0; e < g->ne; ++e) {
+      if (subdomain[e] != ss) continue;
+      local_volume(&c, e, L);
+      scatter(&c, e, e, L);
+      for (int f = 0; f < g->nf; ++f) {
+        const int64_t ne = g->nbr[e * g->nf + f];
+        if (ne >= 0 && subdomain[ne] == ss && e < ne) {
+          local_inner(&c, e, f, ne, L, EN, NE, NN);
+          scatter(&c, e, e, L); scatter(&c, e, ne, EN); scatter(&c, ne, e, NE); scatter(&c, ne, ne, NN);
+        }
+      }
+    }
+  /* walk 2: Dirichlet boundary contributions of boundary subdomains (1136-1179) and coupling
+   * contributions for every neighbouring pair ss < nn, entity in ss (1270-1326) */
+  for (int32_t ss = 0; ss < n_sub; ++ss) {
+    for (int64_t e = 0; e < g->ne; ++e) {
+      if (subdomain[e] != ss) continue;
+      for (int f = 0; f < g->nf; ++f) {
+        const int64_t ne = g->nbr[e * g->nf + f];
+        if (ne < 0 && p->boundary_kind == OR_BOUNDARY_DIRICHLET) {
+          local_boundary(&c, e, f, L);
+          scatter(&c, e, e, L);
+        }
+      }
+    }
+    for (int32_t nn = ss + 1; nn < n_sub; ++nn)
+      for (int64_t e = 0; e < g->ne; ++e) {
+        if (subdomain[e] != ss) continue;
+        for (int f = 0; f < g->nf; ++f) {
+          const int64_t ne = g->nbr[e * g->nf + f];
+          if (ne >= 0 && subdomain[ne] == nn) {
+            local_inner(&c, e, f, ne, L, EN, NE, NN);
+            /* in_in -> local_matrices_[ss], in_out, out_in -> coupling, out_out -> local_matrices_[nn];
+             * build_global_containers() copies all of them into the global block matrix */
+            scatter(&c, e, e, L); scatter(&c, e, ne, EN); scatter(&c, ne, e, NE); scatter(&c, ne, ne, NN);
+          }
+        }
+      }
+  }
+  return 0;
+}
+
+/* ------------------------------------------------------------------------------------------------ */
+/* Pinning helpers: RHS (L2Volume functional, swipdg.hh:253-271) and error norms                      */
+/* ------------------------------------------------------------------------------------------------ */
+static double esv2007_u(const double* x) { return cos(0.5 * M_PI * x[0]) * cos(0.5 * M_PI * x[1]); }
+static void esv2007_grad_u(const double* x, double* gu)
+{
+  gu[0] = -0.5 * M_PI * sin(0.5 * M_PI * x[0]) * cos(0.5 * M_PI * x[1]);
+  gu[1] = -0.5 * M_PI * cos(0.5 * M_PI * x[0]) * sin(0.5 * M_PI * x[1]);
+}
+static double esv2007_f(const double* x) { return 0.5 * M_PI * M_PI * esv2007_u(x); }
+
+/* force kinds: 0 = ESV2007 testcase-1 force (integration order 3) */
+int or_rhs_l2(void* gp, int force_kind, int force_order, const int64_t* elem_index, double* b)
+{
+  grid_t* g = (grid_t*)gp;
+  (void)force_kind;
+  const int order = force_order + 1;      /* f.order() + basis order */
+  quad2_t q; volume_rule(g->type, order, &q);
+  memset(b, 0, sizeof(double) * (size_t)(g->ne * g->nb));
+  for (int64_t e = 0; e < g->ne; ++e) {
+    geom_t G; geometry(g, e, &G);
+    const int64_t gid = gid_of(elem_index, e);
+    for (int k = 0; k < q.n; ++k) {
+      double phi[4], gh[4][2], x[2];
+      shape(g->type, q.x[k], phi, gh);
+      global_pt(&G, q.x[k], x);
+      const double fv = esv2007_f(x) * q.w[k] * fabs(G.det);
+      for (int i = 0; i < g->nb; ++i) b[gid * g->nb + i] += fv * phi[i];
+    }
+  }
+  return 0;
+}
+
+/* ||u - u_h||_L2 and |u - u_h|_H1 for the ESV2007 exact solution, element-wise high order quadrature */
+int or_error_norms_esv2007(void* gp, const double* u, const int64_t* elem_index, int order, double* l2,
+                           double* h1)
+{
+  grid_t* g = (grid_t*)gp;
+  quad2_t q; volume_rule(g->type, order, &q);
+  double sl2 = 0.0, sh1 = 0.0;
+  for (int64_t e = 0; e < g->ne; ++e) {
+    geom_t G; geometry(g, e, &G);
+    const double* ue = u + gid_of(elem_index, e) * g->nb;
+    for (int k = 0; k < q.n; ++k) {
+      double phi[4], gh[4][2], gp_[2], x[2];
+      shape(g->type, q.x[k], phi, gh);
+      global_pt(&G, q.x[k], x);
+      double uh = 0.0, guh[2] = {0.0, 0.0};
+      for (int i = 0; i < g->nb; ++i) {
+        map_grad(&G, gh[i], gp_);
+        uh += ue[i] * phi[i]; guh[0] += ue[i] * gp_[0]; guh[1] += ue[i] * gp_[1];
+      }
+      double gu[2]; esv2007_grad_u(x, gu);
+      const double w = q.w[k] * fabs(G.det);
+      const double d = esv2007_u(x) - uh;
+      sl2 += w * d * d;
+      sh1 += w * ((gu[0] - guh[0]) * (gu[0] - guh[0]) + (gu[1] - guh[1]) * (gu[1] - guh[1]));
+    }
+  }
+  *l2 = sqrt(sl2); *h1 = sqrt(sh1);
+  return 0;
+}
