@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 #include <string>
 
 #include "hdd.h"
@@ -87,6 +88,10 @@ extern "C" int hdd_swipdg_assemble(hdd_ctx* ctx, const hdd_mesh* m, const hdd_sc
   a.sigma_inner = p->sigma_inner;
   a.sigma_boundary = p->sigma_boundary;
   a.beta = p->beta;
+  {
+    const char* df = getenv("HDD_DEBUG_FLAGS");   // profiling ablations only
+    a.debug_flags = df ? atoi(df) : 0;
+  }
   // integrand orders of LocalEvaluation::Elliptic / SWIPDG::Inner / BoundaryLHS at p = 1 (piecewise
   // constant tensors): volume ord(kappa); faces ord(kappa) + 2.  One kernel serves components of equal
   // order -- the caller splits mixed-order component sets.

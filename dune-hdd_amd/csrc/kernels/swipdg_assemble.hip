@@ -23,6 +23,8 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 
 #include "hdd.h"
@@ -717,9 +719,11 @@ swipdg_p1_pwc_kernel(const AssembleArgs a)
       const int tw = int(inf & 7u);
       const bool rev = (inf & 8u) != 0u;
       const int ta = E::fv(tw, 0), tb = E::fv(tw, 1), to = 3 - ta - tb;
-      const double Ox = a.coords[(2 * to) * ne + n], Oy = a.coords[(2 * to + 1) * ne + n];
-      const Tensor Ap = tensor_of(a, n);
-      const double kn = kappa_elem(a.kappa[0], n);
+      const int64_t ng = (a.debug_flags & 2) ? e : int64_t(n);   // ablation: no neighbour gathers
+      const double Ox = (a.debug_flags & 2) ? X[fc] + 0.5 * (X[fa] - X[fc]) + nx : a.coords[(2 * to) * ne + ng];
+      const double Oy = (a.debug_flags & 2) ? Y[fc] + 0.5 * (Y[fa] - Y[fc]) + ny : a.coords[(2 * to + 1) * ne + ng];
+      const Tensor Ap = tensor_of(a, ng);
+      const double kn = kappa_elem(a.kappa[0], ng);
       const double dp = agn(Ap, nx, ny, nx, ny);
       const double rs = rcp_nr(dp + dm);
       const double gamma = (dp * dm) * rs;
@@ -743,9 +747,13 @@ swipdg_p1_pwc_kernel(const AssembleArgs a)
         const double vA = cpl * AnA * m1i + sym * Ae[i] * half - pen * (i == fc ? 0.0 : (i == fa ? third : sixth));
         const double vB = cpl * AnB * m1i + sym * Ae[i] * half - pen * (i == fc ? 0.0 : (i == fb ? third : sixth));
         const double vO = cpl * AnO * m1i;
-        row[jA] = vA;
-        row[jB] = vB;
-        row[to] = vO;
+        if (!(a.debug_flags & 4)) {
+          row[jA] = vA;
+          row[jB] = vB;
+          row[to] = vO;
+        } else {
+          S[i][0] += vA + vB + vO;   // ablation: keep the values alive without LDS traffic
+        }
       }
       // entity/entity block
 #pragma unroll
@@ -775,6 +783,10 @@ swipdg_p1_pwc_kernel(const AssembleArgs a)
 
   __syncthreads();
   double* out = a.vals[0];
+  if (a.debug_flags & 1) {   // ablation: no global stores (keep a dependency on the image)
+    if (lds[lane] == 1.2345e-300) out[base] = 0.0;
+    return;
+  }
   const int64_t n2 = (tile_end - base_al) >> 1;
   for (int64_t k = lane; k < n2; k += 64) {
     const int64_t gi = base_al + 2 * k;
@@ -783,6 +795,308 @@ swipdg_p1_pwc_kernel(const AssembleArgs a)
     else out[gi + 1] = v.y;
   }
   if (((tile_end - base_al) & 1) && lane == 0) out[tile_end - 1] = lds[tile_end - 1 - base_al];
+}
+
+// ------------------------------------------------------------------------------------------------
+// Persistent, software-pipelined variant of the P1 kernel.
+//
+// gfx950's vmcnt is in order and counts stores: a wave that waits for a load issued after its stores
+// also waits for those stores.  So each wave walks a sequence of tiles and orders its memory operations
+//   [prefetch own data of tile t+1] [compute tile t -> LDS] [gathers of tile t+1] [stores of tile t]
+// The loads of tile t+1 are in flight while tile t computes, the neighbour gathers are issued before the
+// store burst, and the stores are branch-free buffer stores (fixed count, out-of-range ones dropped by
+// the descriptor's range check), so the next wait can stay counted instead of draining the stores.
+// ------------------------------------------------------------------------------------------------
+struct P1Own {
+  double X[3], Y[3];
+  int32_t nbr[3];
+  uint32_t finfo;
+  Tensor A;
+  double ke;
+};
+
+// offset of this lane's row block inside the tile: sum of 9*nblk over the active lanes below it
+// (the pattern's elem_ptr rule), from two ballots instead of a per-element elem_ptr load
+__device__ __forceinline__ int p1_tile_offset(const P1Own& o, bool active)
+{
+  const int c = int(o.nbr[0] >= 0) + int(o.nbr[1] >= 0) + int(o.nbr[2] >= 0);   // interior faces
+  const uint64_t act = __ballot(active);
+  const uint64_t b0 = __ballot(active && (c & 1));
+  const uint64_t b1 = __ballot(active && (c & 2));
+  auto below = [](uint64_t m) {
+    return int(__builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u)));
+  };
+  return 9 * (below(act) + below(b0) + 2 * below(b1));
+}
+struct P1Gat {
+  double Ox[3], Oy[3];
+  Tensor Ap[3];
+  double kn[3];
+};
+
+template <int TK>
+__device__ __forceinline__ Tensor tensor_k(const AssembleArgs& a, int64_t e)
+{
+  Tensor t;
+  if constexpr (TK == HDD_TENSOR_ISO_PER_ELEM) {
+    const double v = a.tper[e];
+    t.a00 = v; t.a01 = 0.0; t.a11 = v;
+  } else if constexpr (TK == HDD_TENSOR_SYM_PER_ELEM) {
+    t.a00 = a.tper[e]; t.a01 = a.tper[a.n_local + e]; t.a11 = a.tper[2 * a.n_local + e];
+  } else {
+    t.a00 = a.tc0; t.a01 = a.tc1; t.a11 = a.tc2;
+  }
+  return t;
+}
+template <int KK>
+__device__ __forceinline__ double kappa_k(const AssembleArgs& a, int64_t e)
+{
+  if constexpr (KK == HDD_FN_PER_ELEM) return a.kappa[0].per_elem[e];
+  else return a.kappa[0].c;
+}
+
+template <int TK, int KK>
+__device__ __forceinline__ void p1_load_own(const AssembleArgs& a, int64_t e, P1Own& o)
+{
+  const int64_t ne = a.n_local;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    o.X[k] = a.coords[(2 * k) * ne + e];
+    o.Y[k] = a.coords[(2 * k + 1) * ne + e];
+  }
+#pragma unroll
+  for (int f = 0; f < 3; ++f) o.nbr[f] = a.nbrs[f * ne + e];
+  o.finfo = a.finfo[e];
+  o.A = tensor_k<TK>(a, e);
+  o.ke = kappa_k<KK>(a, e);
+}
+
+template <int TK, int KK>
+__device__ __forceinline__ void p1_load_gat(const AssembleArgs& a, int64_t e, const P1Own& o, P1Gat& g)
+{
+  const int64_t ne = a.n_local;
+#pragma unroll
+  for (int f = 0; f < 3; ++f) {
+    const int64_t n = o.nbr[f] >= 0 ? int64_t(o.nbr[f]) : e;   // boundary faces: harmless own reload
+    const uint32_t inf = (o.finfo >> (4 * f)) & 15u;
+    const int tw = int(inf & 7u);
+    const int to = 3 - Simplex::fv(tw, 0) - Simplex::fv(tw, 1);
+    g.Ox[f] = a.coords[(2 * to) * ne + n];
+    g.Oy[f] = a.coords[(2 * to + 1) * ne + n];
+    g.Ap[f] = tensor_k<TK>(a, n);
+    g.kn[f] = kappa_k<KK>(a, n);
+  }
+}
+
+// the per-element math of swipdg_p1_pwc_kernel, on preloaded data; writes the row block into `img`
+__device__ __forceinline__ void p1_compute(const AssembleArgs& a, int64_t e, const P1Own& o, const P1Gat& gt,
+                                           double* img)
+{
+  using E = Simplex;
+  const double j00 = o.X[1] - o.X[0], j01 = o.X[2] - o.X[0], j10 = o.Y[1] - o.Y[0], j11 = o.Y[2] - o.Y[0];
+  const double det = j00 * j11 - j01 * j10;
+  const double id = rcp_nr(det);
+  const double i00 = j11 * id, i01 = -j01 * id, i10 = -j10 * id, i11 = j00 * id;
+  double g[3][2];
+  g[1][0] = i00; g[1][1] = i01;
+  g[2][0] = i10; g[2][1] = i11;
+  g[0][0] = -i00 - i10; g[0][1] = -i01 - i11;
+  double Ag[3][2];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    Ag[k][0] = o.A.a00 * g[k][0] + o.A.a01 * g[k][1];
+    Ag[k][1] = o.A.a01 * g[k][0] + o.A.a11 * g[k][1];
+  }
+  const double adet = fabs(det);
+  const double osgn = det > 0.0 ? 1.0 : -1.0;
+  int nblk = 1, pos_self = 0, pos[3];
+#pragma unroll
+  for (int f = 0; f < 3; ++f) {
+    nblk += o.nbr[f] >= 0;
+    pos_self += (o.nbr[f] >= 0 && o.nbr[f] < e);
+  }
+#pragma unroll
+  for (int f = 0; f < 3; ++f) {
+    int p = (e < o.nbr[f]) ? 1 : 0;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) p += (o.nbr[q] >= 0 && o.nbr[q] < o.nbr[f]);
+    pos[f] = p;
+  }
+  const int rowlen = nblk * 3;
+  const double ke = o.ke;
+  double S[3][3];
+  {
+    const double fac = 0.5 * adet * ke;
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) S[i][j] = fac * (Ag[j][0] * g[i][0] + Ag[j][1] * g[i][1]);
+  }
+#pragma unroll
+  for (int f = 0; f < 3; ++f) {
+    const int32_t n = o.nbr[f];
+    if (n <= HDD_NBR_NEUMANN) continue;
+    const int fa = E::fv(f, 0), fb = E::fv(f, 1), fc = 3 - fa - fb;
+    const double tx = o.X[fb] - o.X[fa], ty = o.Y[fb] - o.Y[fa];
+    const double il = rsq_nr(tx * tx + ty * ty);
+    const double len = (tx * tx + ty * ty) * il;
+    const double nsc = E::face_sign(f) * osgn * il;
+    const double nx = ty * nsc, ny = -tx * nsc;
+    double Ae[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) Ae[k] = Ag[k][0] * nx + Ag[k][1] * ny;
+    const double dm = agn(o.A, nx, ny, nx, ny);
+    const double ihp = a.beta == 1.0 ? il : rcp_nr(pow(len, a.beta));
+    const double half = 0.5 * len, third = len * (1.0 / 3.0), sixth = len * (1.0 / 6.0);
+    if (n >= 0) {
+      const uint32_t inf = (o.finfo >> (4 * f)) & 15u;
+      const int tw = int(inf & 7u);
+      const bool rev = (inf & 8u) != 0u;
+      const int ta = E::fv(tw, 0), tb = E::fv(tw, 1), to = 3 - ta - tb;
+      const double Ox = gt.Ox[f], Oy = gt.Oy[f];
+      const Tensor Ap = gt.Ap[f];
+      const double kn = gt.kn[f];
+      const double dp = agn(Ap, nx, ny, nx, ny);
+      const double rs = rcp_nr(dp + dm);
+      const double gamma = (dp * dm) * rs;
+      const double w_plus = dm * rs, w_minus = dp * rs;
+      const double pen = (ke * kn * a.sigma_inner * gamma) * ihp;
+      const double Ax = o.X[fa], Ay = o.Y[fa], Bx = o.X[fb], By = o.Y[fb];
+      const double iD = rcp_nr((Bx - Ax) * (Oy - Ay) - (By - Ay) * (Ox - Ax));
+      const double mx = Ap.a00 * nx + Ap.a01 * ny, my = Ap.a01 * nx + Ap.a11 * ny;
+      const double AnA = ((By - Oy) * mx + (Ox - Bx) * my) * iD;
+      const double AnB = ((Oy - Ay) * mx + (Ax - Ox) * my) * iD;
+      const double AnO = ((Ay - By) * mx + (Bx - Ax) * my) * iD;
+      const int jA = rev ? tb : ta, jB = rev ? ta : tb;
+      const double cpl = -w_plus * kn;
+      const double sym = w_minus * ke;
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        double* row = img + i * rowlen + pos[f] * 3;
+        const double m1i = i == fc ? 0.0 : half;
+        row[jA] = cpl * AnA * m1i + sym * Ae[i] * half - pen * (i == fc ? 0.0 : (i == fa ? third : sixth));
+        row[jB] = cpl * AnB * m1i + sym * Ae[i] * half - pen * (i == fc ? 0.0 : (i == fb ? third : sixth));
+        row[to] = cpl * AnO * m1i;
+      }
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          const double m1i = i == fc ? 0.0 : half, m1j = j == fc ? 0.0 : half;
+          const double mm = (i == fc || j == fc) ? 0.0 : (i == j ? third : sixth);
+          S[i][j] += -w_minus * ke * (Ae[j] * m1i + Ae[i] * m1j) + pen * mm;
+        }
+    } else {
+      const double pen = (a.sigma_boundary * ke * dm) * ihp;
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          const double m1i = i == fc ? 0.0 : half, m1j = j == fc ? 0.0 : half;
+          const double mm = (i == fc || j == fc) ? 0.0 : (i == j ? third : sixth);
+          S[i][j] += -ke * (Ae[j] * m1i + Ae[i] * m1j) + pen * mm;
+        }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) img[i * rowlen + pos_self * 3 + j] = S[i][j];
+}
+
+typedef int ivec4 __attribute__((ext_vector_type(4)));
+constexpr int P1_RB = 36;                          // values of an interior P1 row block
+constexpr int P1_IMG = 64 * P1_RB;                 // doubles of a full tile image
+constexpr int P1_STORES = (P1_IMG / 2 + 63) / 64;  // 16-byte stores per lane that cover a tile (18)
+
+template <int TK, int KK>
+__global__ void __launch_bounds__(64, 2)
+swipdg_p1_pwc_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
+{
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  const int lane = threadIdx.x;
+  // XCD-aware schedule: the 8 XCDs get contiguous eighths of the tile range; the workgroups of one XCD
+  // sweep their eighth together, so neighbour rows above / below are recent in that XCD's L2.
+  const int64_t G = gridDim.x, b = blockIdx.x;
+  int64_t t, t_end, t_step;
+  if (G >= n_tiles) {
+    t = b; t_end = b + 1; t_step = 1;
+  } else {
+    const int64_t x = b & 7, w = b >> 3, gx = G >> 3;
+    t = (n_tiles * x) / 8 + w;
+    t_end = (n_tiles * (x + 1)) / 8;
+    t_step = gx;
+  }
+  if (t >= t_end) return;
+  double* scratch = lds + P1_IMG + 2;
+
+  auto elem_of = [&](int64_t tile) {
+    const int64_t t0 = a.own_begin + tile * 64;
+    const int64_t e0 = t0 + lane;
+    return e0 < a.own_end ? e0 : t0;
+  };
+  // tile bounds through the scalar cache (lgkmcnt, not the in-order vmcnt the streams share)
+  auto bounds = [&](int64_t tile, int64_t& base, int64_t& tile_end) {
+    const int64_t t0 = __builtin_amdgcn_readfirstlane(a.own_begin + tile * 64);
+    const int64_t tend = t0 + 64 < a.own_end ? t0 + 64 : a.own_end;
+    base = __builtin_amdgcn_readfirstlane(a.elem_ptr[t0 - a.own_begin]);
+    tile_end = __builtin_amdgcn_readfirstlane(a.elem_ptr[tend - a.own_begin]);
+  };
+  int64_t e = elem_of(t);
+  P1Own own;
+  P1Gat gat;
+  p1_load_own<TK, KK>(a, e, own);
+  p1_load_gat<TK, KK>(a, e, own, gat);
+  int64_t base, tile_end;
+  bounds(t, base, tile_end);
+  double* out = a.vals[0];
+  for (;;) {
+    const int64_t tn = t + t_step < t_end ? t + t_step : t;
+    const bool has_next = t + t_step < t_end;
+    const int64_t en = elem_of(tn);
+    P1Own own_n;
+    p1_load_own<TK, KK>(a, en, own_n);                // prefetch, in flight during this tile's compute
+    int64_t base_n, tile_end_n;
+    bounds(tn, base_n, tile_end_n);
+
+    const int64_t t0 = a.own_begin + t * 64;
+    const bool active = t0 + lane < a.own_end;
+    const int64_t base_al = base & ~int64_t(1);
+    const int off = p1_tile_offset(own, active) + int(base - base_al);
+    p1_compute(a, e, own, gat, active ? lds + off : scratch);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+    P1Gat gat_n;
+    p1_load_gat<TK, KK>(a, en, own_n, gat_n);         // issued before this tile's stores
+
+    // stream [base, tile_end): head / tail singles by all lanes (same value), even-aligned body in
+    // fixed-count 16-byte buffer stores, range-checked by the descriptor
+    const int64_t start = (base + 1) & ~int64_t(1);
+    const int64_t stop = tile_end & ~int64_t(1);
+    const double head = lds[base - base_al];
+    const double tail = lds[tile_end - 1 - base_al];
+    out[base] = head;
+    out[tile_end - 1] = tail;
+    const int nbytes = stop > start ? int(stop - start) * 8 : 0;
+    __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(out + start, (short)0, nbytes, 0x00020000);
+    const double* src = lds + (start - base_al);
+#pragma unroll
+    for (int k = 0; k < P1_STORES; ++k) {
+      const int idx = 2 * (lane + 64 * k);
+      const int li = idx < P1_IMG ? idx : 0;
+      const dvec2 v = *reinterpret_cast<const dvec2*>(src + li);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ivec4, v), rsrc, idx * 8, 0, 0);
+    }
+    if (!has_next) break;
+    t = tn;
+    e = en;
+    own = own_n;
+    gat = gat_n;
+    base = base_n;
+    tile_end = tile_end_n;
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -814,6 +1128,36 @@ static hipError_t launch_p1_pwc(const AssembleArgs& a, hipStream_t s)
   if (n_own <= 0) return hipSuccess;
   const int64_t tiles = (n_own + 63) / 64;
   const size_t lds = (size_t(64) * 36 + 2 + 36) * sizeof(double);
+  if (!(a.debug_flags & 64)) {   // persistent pipelined kernel (default); flag 64 = one tile per workgroup
+    int dev = 0, cus = 256;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    int wgcu = 4;   // measured best on MI355X (sweep 1..8: 4 -> 0.301 ms at C2)
+    if (const char* w = getenv("HDD_P1_WGCU")) wgcu = atoi(w);   // profiling sweeps only
+    const int64_t G = std::min<int64_t>(tiles, int64_t(cus) * wgcu);
+    for (int c = 0; c < a.n_comp; ++c) {
+      AssembleArgs ac = a;
+      ac.n_comp = 1;
+      ac.kappa[0] = a.kappa[c];
+      ac.vals[0] = a.vals[c];
+      const int tk = ac.tkind, kk = ac.kappa[0].kind;
+      if (tk == HDD_TENSOR_ISO_PER_ELEM && kk == HDD_FN_CONST)
+        hipLaunchKernelGGL((swipdg_p1_pwc_persistent_kernel<HDD_TENSOR_ISO_PER_ELEM, HDD_FN_CONST>), dim3(unsigned(G)), dim3(64), lds, s, ac, tiles);
+      else if (tk == HDD_TENSOR_ISO_PER_ELEM && kk == HDD_FN_PER_ELEM)
+        hipLaunchKernelGGL((swipdg_p1_pwc_persistent_kernel<HDD_TENSOR_ISO_PER_ELEM, HDD_FN_PER_ELEM>), dim3(unsigned(G)), dim3(64), lds, s, ac, tiles);
+      else if (tk == HDD_TENSOR_CONST && kk == HDD_FN_CONST)
+        hipLaunchKernelGGL((swipdg_p1_pwc_persistent_kernel<HDD_TENSOR_CONST, HDD_FN_CONST>), dim3(unsigned(G)), dim3(64), lds, s, ac, tiles);
+      else if (tk == HDD_TENSOR_CONST && kk == HDD_FN_PER_ELEM)
+        hipLaunchKernelGGL((swipdg_p1_pwc_persistent_kernel<HDD_TENSOR_CONST, HDD_FN_PER_ELEM>), dim3(unsigned(G)), dim3(64), lds, s, ac, tiles);
+      else if (tk == HDD_TENSOR_SYM_PER_ELEM && kk == HDD_FN_CONST)
+        hipLaunchKernelGGL((swipdg_p1_pwc_persistent_kernel<HDD_TENSOR_SYM_PER_ELEM, HDD_FN_CONST>), dim3(unsigned(G)), dim3(64), lds, s, ac, tiles);
+      else
+        hipLaunchKernelGGL((swipdg_p1_pwc_persistent_kernel<HDD_TENSOR_SYM_PER_ELEM, HDD_FN_PER_ELEM>), dim3(unsigned(G)), dim3(64), lds, s, ac, tiles);
+      const hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+  }
   for (int c = 0; c < a.n_comp; ++c) {
     AssembleArgs ac = a;
     ac.n_comp = 1;

@@ -26,6 +26,7 @@ struct AssembleArgs {
   double tc0, tc1, tc2;
   const double* tper;
   double sigma_inner, sigma_boundary, beta;
+  int32_t debug_flags, pad2;   // ablation switches (HDD_DEBUG_FLAGS), 0 in production
   KappaArg kappa[HDD_MAX_COMP];
   double* vals[HDD_MAX_COMP];
 };
