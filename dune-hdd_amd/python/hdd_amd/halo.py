@@ -9,14 +9,14 @@ needed (rows are owned), so there is no all-reduce on the data path.
 """
 import numpy as np
 
-from . import soa_gather, soa_scatter, _torch
+from . import soa_gather, soa_scatter
 
 
 class HaloExchange:
     """arrays: list of (device tensor [rows][n_local] contiguous, rows).  owner: subdomain -> rank map."""
 
     def __init__(self, ctx, local, arrays, owner, rank, host_staging=False):
-        torch = _torch()
+        import torch
         import torch.distributed as dist
         self.dist = dist
         self.ctx = ctx
@@ -35,7 +35,7 @@ class HaloExchange:
             rbuf = torch.empty((self.total_rows, p["recv_count"]), dtype=torch.float64, device=dev)
             hs = hr = None
             if host_staging:
-                hs = torch.empty(sbuf.shape, dtype=torch.float64).pin_memory() if torch.cuda.is_available() else None
+                hs = torch.empty(sbuf.shape, dtype=torch.float64)
                 hr = torch.empty(rbuf.shape, dtype=torch.float64)
             self.peers.append(dict(peer=p["peer"], idx=send_idx, sbuf=sbuf, rbuf=rbuf, off=p["recv_offset"],
                                    n_recv=p["recv_count"], hs=hs, hr=hr))
@@ -44,11 +44,17 @@ class HaloExchange:
     def halo_bytes(self):
         return sum(8 * self.total_rows * (p["idx"].numel() + p["n_recv"]) for p in self.peers)
 
+    def pack(self, p):
+        soa_gather(self.ctx, self.arrays, self.rows, self.ld, p["idx"], p["sbuf"])
+
+    def unpack(self, p):
+        soa_scatter(self.ctx, self.arrays, self.rows, self.ld, p["off"], p["n_recv"], p["rbuf"])
+
     def exchange(self):
         dist = self.dist
         for p in self.peers:
             if p["idx"].numel():
-                soa_gather(self.ctx, self.arrays, self.rows, self.ld, p["idx"], p["sbuf"])
+                self.pack(p)
         if self.host_staging:
             ops = []
             for p in self.peers:
@@ -70,7 +76,7 @@ class HaloExchange:
                     r.wait()
         for p in self.peers:
             if p["n_recv"]:
-                soa_scatter(self.ctx, self.arrays, self.rows, self.ld, p["off"], p["n_recv"], p["rbuf"])
+                self.unpack(p)
 
 
 def strip_owner(n_sub, world):

@@ -1,0 +1,152 @@
+"""Sharded (block-SWIPDG strip) assembly: world_size-2 process groups.
+
+CPU (gloo): the halo plan + exchange protocol of hdd_amd.halo.HaloExchange fills every ghost column with the
+owner's element record (pack / unpack emulated with torch indexing on CPU tensors -- test plumbing only;
+the product packs with the HIP hdd_soa_gather / hdd_soa_scatter kernels).
+
+GPU: two ranks share cuda:0 (gloo with host staging, since RCCL needs one GPU per rank); ghosts are zeroed
+on the device and arrive only through the exchange; each rank assembles its own rows with the HIP kernel;
+the concatenated rows equal the oracle's global block-SWIPDG matrix.
+"""
+import os
+import socket
+import sys
+import tempfile
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _setup_paths():
+    for p in (os.path.join(ROOT, "dune-hdd_amd", "python"), os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+
+
+GRID = dict(nx=24, ny=8, lower=(0.0, 0.0), upper=(4.0, 1.0))
+
+
+def _cpu_worker(rank, world, port, outdir):
+    _setup_paths()
+    import torch
+    import torch.distributed as dist
+
+    import hdd_amd as H
+    from hdd_amd.halo import HaloExchange, strip_owner
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    class HostHalo(HaloExchange):   # test plumbing: CPU pack/unpack
+        def pack(self, p):
+            rows = torch.cat([a.view(-1, self.ld) for a in self.arrays])
+            p["sbuf"].copy_(rows[:, p["idx"].long()])
+
+        def unpack(self, p):
+            r0 = 0
+            for a, nr in zip(self.arrays, self.rows):
+                a.view(nr, self.ld)[:, p["off"]:p["off"] + p["n_recv"]] = p["rbuf"][r0:r0 + nr]
+                r0 += nr
+
+    g = H.Grid.structured(H.SIMPLEX, GRID["nx"], GRID["ny"], GRID["lower"], GRID["upper"], px=world * 2, py=1)
+    owner = strip_owner(g.n_sub, world)
+    s0 = int(np.where(owner == rank)[0][0])
+    s1 = int(np.where(owner == rank)[0][-1]) + 1
+    loc = g.local(s0, s1)
+    truth_c = loc.coords.copy()
+    truth_k = loc.global_id.astype(np.float64) * 0.5 + 1.0
+    coords = torch.from_numpy(truth_c.copy())
+    kk = torch.from_numpy(truth_k.copy())
+    for a in (coords, kk.view(1, -1)):
+        a[:, :loc.own_begin] = 0
+        a[:, loc.own_end:] = 0
+    halo = HostHalo(None, loc, [(coords, coords.shape[0]), (kk.view(1, -1), 1)], owner, rank)
+    halo.exchange()
+    ok = np.array_equal(coords.numpy(), truth_c) and np.array_equal(kk.numpy(), truth_k)
+    np.save(os.path.join(outdir, "ok_%d.npy" % rank), np.array([ok, loc.n_ghost > 0]))
+    dist.destroy_process_group()
+
+
+def test_gloo_halo_exchange_cpu():
+    import torch.multiprocessing as mp
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_cpu_worker, args=(2, _free_port(), d), nprocs=2, join=True)
+        for r in range(2):
+            ok, has_ghosts = np.load(os.path.join(d, "ok_%d.npy" % r))
+            assert ok and has_ghosts
+
+
+def _gpu_worker(rank, world, port, outdir):
+    _setup_paths()
+    import torch
+    import torch.distributed as dist
+
+    import hdd_amd as H
+    import oracle as O
+    from hdd_amd.halo import HaloExchange, strip_owner
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    perm = O.spe10_synthetic_permeability()
+    g = H.Grid.structured(H.SIMPLEX, GRID["nx"], GRID["ny"], GRID["lower"], GRID["upper"], px=world * 2, py=1)
+    owner = strip_owner(g.n_sub, world)
+    s0 = int(np.where(owner == rank)[0][0])
+    s1 = int(np.where(owner == rank)[0][-1]) + 1
+    loc = g.local(s0, s1)
+    kcell = torch.from_numpy(loc.checkerboard(GRID["lower"], GRID["upper"], 100, 20, perm)).cuda()
+    kcell[:loc.own_begin] = 0
+    kcell[loc.own_end:] = 0
+    ctx = H.Context(0)
+    dm = H.DeviceMesh(loc, 0, zero_ghosts=True)
+    dp = H.DevicePattern(loc, 0)
+    halo = HaloExchange(ctx, loc, [(dm.coords, dm.coords.shape[0]), (kcell.view(1, -1), 1)], owner, rank,
+                        host_staging=True)
+    halo.exchange()
+    (val,) = H.assemble(ctx, dm, dp, [H.scalar_fn(H.FN_CONST, 1.0)], H.tensor_fn(H.TENSOR_ISO_PER_ELEM, per_elem=kcell))
+    torch.cuda.synchronize()
+    np.save(os.path.join(outdir, "val_%d.npy" % rank), val.cpu().numpy())
+    np.save(os.path.join(outdir, "rng_%d.npy" % rank), np.array(g.subdomain_range(s0, s1)))
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_two_ranks_one_gpu_match_global_oracle():
+    import torch.multiprocessing as mp
+    _setup_paths()
+    import hdd_amd as H
+    import oracle as O
+    from cases import compare_rows
+
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_gpu_worker, args=(2, _free_port(), d), nprocs=2, join=True)
+        vals = [np.load(os.path.join(d, "val_%d.npy" % r)) for r in range(2)]
+        rngs = [np.load(os.path.join(d, "rng_%d.npy" % r)) for r in range(2)]
+    g = H.Grid.structured(H.SIMPLEX, GRID["nx"], GRID["ny"], GRID["lower"], GRID["upper"], px=4, py=1)
+    pc, pev, psd = g.connectivity()
+    ot, oc, oev = O.kuhn_grid(GRID["nx"], GRID["ny"], GRID["lower"], GRID["upper"])
+    key = {tuple(r): i for i, r in enumerate(oev)}
+    permu = np.array([key[tuple(r)] for r in pev])
+    sub = np.empty(g.ne, np.int32)
+    sub[permu] = psd
+    perm = O.spe10_synthetic_permeability()
+    k = O.checkerboard(O.element_centers(oc, oev), GRID["lower"], GRID["upper"], 100, 20, perm)
+    og = O.Grid(ot, oc, oev)
+    ei, rp, col, oval = O.assemble_block(og, sub, 4, O.scalar(O.FN_CONST, 1.0),
+                                         O.tensor(O.TENSOR_ISO_PER_ELEM, per_elem=k), O.params())
+    assert rngs[0][0] == 0 and rngs[0][1] == rngs[1][0] and rngs[1][1] == g.ne
+    got = np.concatenate(vals)
+    worst, ok = compare_rows(rp, got, oval, 1e-12)
+    assert ok, worst

@@ -1,0 +1,135 @@
+"""Host grids, rank-local views, halo plans and the sparsity pattern (product, C++) against the oracle's
+independent grid walk (faces from element->vertex connectivity) -- CPU only."""
+import numpy as np
+import pytest
+
+import hdd_amd as H
+import oracle as O
+from mesh_tools import nvb_mesh
+
+MK = {H.SIMPLEX: O.kuhn_grid, H.CUBE: O.cube_grid}
+
+
+@pytest.mark.parametrize("et", [H.SIMPLEX, H.CUBE])
+@pytest.mark.parametrize("nx,ny", [(1, 1), (7, 5), (16, 3)])
+def test_structured_matches_oracle(et, nx, ny):
+    g = H.Grid.structured(et, nx, ny, (-1, -2), (3, 1))
+    coords, ev, sd = g.connectivity()
+    ot, oc, oev = MK[et](nx, ny, (-1, -2), (3, 1))
+    assert np.array_equal(coords, oc) and np.array_equal(ev, oev) and not sd.any()
+    og = O.Grid(ot, oc, oev)
+    onb, onf = og.neighbors()
+    loc = g.local()
+    assert loc.n_local == g.ne and loc.own_begin == 0 and loc.n_ghost == 0
+    nb = loc.neighbors.T.astype(np.int64)
+    assert np.array_equal(np.where(onb < 0, H.NBR_DIRICHLET, onb), nb)
+    tw = np.stack([(loc.face_info.astype(np.int64) >> (4 * f)) & 7 for f in range(g.nf)], 1)
+    rev = np.stack([(loc.face_info.astype(np.int64) >> (4 * f + 3)) & 1 for f in range(g.nf)], 1)
+    inner = onb >= 0
+    assert np.array_equal(tw[inner], onf[inner]) and not rev.any()
+    rp, col, ep = loc.pattern()
+    orp, ocol = og.pattern()
+    assert np.array_equal(rp, orp) and np.array_equal(col, ocol)
+    assert np.array_equal(ep, rp[::g.nb])
+
+
+def test_connectivity_grid_bisection_mesh():
+    et, c, ev = nvb_mesh(4, 3)
+    g = H.Grid.from_connectivity(H.SIMPLEX, c, ev)
+    og = O.Grid(et, c, ev)
+    onb, onf = og.neighbors()
+    loc = g.local()
+    nb = loc.neighbors.T.astype(np.int64)
+    assert np.array_equal(np.where(onb < 0, -1, onb), nb)
+    fi = loc.face_info.astype(np.int64)
+    inner = onb >= 0
+    tw = np.stack([(fi >> (4 * f)) & 7 for f in range(3)], 1)
+    assert np.array_equal(tw[inner], onf[inner])
+    # reversal bit: my face vertex 0 is the neighbour's face vertex 1
+    FV = [(0, 1), (0, 2), (1, 2)]
+    for e in range(g.ne):
+        for f in range(3):
+            n = onb[e, f]
+            if n < 0:
+                continue
+            r = (fi[e] >> (4 * f + 3)) & 1
+            mine = ev[e, FV[f][0]]
+            theirs = ev[n, FV[onf[e, f]][0]]
+            assert r == int(mine != theirs)
+    assert (fi & 0x888).any()
+
+
+@pytest.mark.parametrize("et,px,py", [(H.SIMPLEX, 3, 2), (H.CUBE, 4, 4), (H.SIMPLEX, 5, 1)])
+def test_partitioned_numbering_is_block_numbering(et, px, py):
+    nx, ny = 13, 9
+    g = H.Grid.structured(et, nx, ny, (0, 0), (1, 1), px=px, py=py)
+    pc, pev, psd = g.connectivity()
+    ot, oc, oev = MK[et](nx, ny, (0, 0), (1, 1))
+    key = {tuple(r): i for i, r in enumerate(oev)}
+    perm = np.array([key[tuple(r)] for r in pev])
+    assert np.array_equal(np.sort(perm), np.arange(g.ne))
+    assert np.all(np.diff(psd) >= 0)            # subdomain-major
+    sub = np.empty(g.ne, np.int32)
+    sub[perm] = psd
+    og = O.Grid(ot, oc, oev)
+    ei = O.block_numbering(og, sub, px * py)
+    assert np.array_equal(ei[perm], np.arange(g.ne))
+    rp, col, _ = g.local().pattern()
+    orp, ocol = og.pattern(ei)
+    assert np.array_equal(rp, orp) and np.array_equal(col, ocol)
+    # rank-local slices
+    nb = g.nb
+    for s0, s1 in [(0, 1), (1, px * py - 1), (px * py - 1, px * py)]:
+        if s0 >= s1:
+            continue
+        L = g.local(s0, s1)
+        a, b = g.subdomain_range(s0, s1)
+        lrp, lcol, _ = L.pattern()
+        assert np.array_equal(lrp, rp[a * nb:b * nb + 1] - rp[a * nb])
+        assert np.array_equal(lcol, col[rp[a * nb]:rp[b * nb]])
+        # local order == global order
+        assert np.all(np.diff(L.global_id) > 0)
+        assert np.array_equal(L.global_id[L.own_begin:L.own_end], np.arange(a, b))
+
+
+def test_halo_plan_consistency():
+    g = H.Grid.structured(H.SIMPLEX, 24, 6, (0, 0), (4, 1), px=4, py=2)
+    world = 4
+    owner = np.repeat(np.arange(world, dtype=np.int32), 2)        # 2 subdomains (one column) per rank
+    locs = [g.local(2 * r, 2 * r + 2) for r in range(world)]
+    plans = [locs[r].halo_plan(owner, r) for r in range(world)]
+    for r in range(world):
+        peers = [p["peer"] for p in plans[r]]
+        assert peers == sorted(set(peers)) and r not in peers
+        for p in plans[r]:
+            q = p["peer"]
+            back = [x for x in plans[q] if x["peer"] == r][0]
+            sent_gids = locs[r].global_id[p["send"]]
+            recv_gids = locs[q].global_id[back["recv_offset"]:back["recv_offset"] + back["recv_count"]]
+            assert np.array_equal(sent_gids, recv_gids)
+        n_recv = sum(p["recv_count"] for p in plans[r])
+        assert n_recv == locs[r].n_ghost
+
+
+def test_checkerboard_matches_oracle():
+    perm = O.spe10_synthetic_permeability()
+    for et in (H.SIMPLEX, H.CUBE):
+        g = H.Grid.structured(et, 100, 20, (0, 0), (5, 1))
+        k = g.local().checkerboard((0, 0), (5, 1), 100, 20, perm)
+        ot, oc, oev = MK[et](100, 20, (0, 0), (5, 1))
+        assert np.array_equal(k, O.checkerboard(O.element_centers(oc, oev), (0, 0), (5, 1), 100, 20, perm))
+
+
+def test_bench_size_counts():
+    """C2 sizes quoted in SURVEY.md 8(a): 3200x640 Kuhn -> 4,096,000 triangles, 147,386,880 nnz."""
+    g = H.Grid.structured(H.SIMPLEX, 3200, 640, (0, 0), (5, 1))
+    assert g.ne == 4096000
+    L = g.local()
+    import ctypes as C
+    nnz = C.c_int64()
+    nb = np.ascontiguousarray(L.neighbors)
+    H._check(H.lib().hdd_pattern_count(H.SIMPLEX, L.n_local, L.own_begin, L.own_end, nb.ctypes.data, C.byref(nnz)))
+    assert nnz.value == 147386880
+    g1 = H.Grid.structured(H.CUBE, 16, 16, (-1, -1), (1, 1))
+    rp, col, _ = g1.local().pattern()
+    assert col.shape[0] == 19456                                  # C1
