@@ -40,6 +40,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU work of the baseline sample")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo = rehearsal of the N-rank path on one GPU (host-staged halo)")
     return ap.parse_args()
 
 
@@ -88,9 +90,14 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit("--gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
-    torch.cuda.set_device(local_rank)
+    gpu = local_rank if args.backend == "nccl" else 0
+    torch.cuda.set_device(gpu)
+    local_rank = gpu
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group("gloo")
 
     nx, ny = args.nx * world, args.ny
     lower, upper = (0.0, 0.0), (5.0 * world, 1.0)
@@ -112,7 +119,7 @@ def main():
     halo = None
     if world > 1:
         halo = HaloExchange(ctx, local, [(dmesh.coords, dmesh.coords.shape[0]), (tens.view(1, -1), 1)],
-                            strip_owner(grid.n_sub, world), rank)
+                            strip_owner(grid.n_sub, world), rank, host_staging=args.backend == "gloo")
 
     n_own = local.n_own
     dofs_rank = 3 * n_own
@@ -148,7 +155,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
-    t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device="cuda")
+    t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device="cuda" if args.backend == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, kernel_ms_max = float(t[0]), float(t[1])

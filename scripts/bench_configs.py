@@ -1,0 +1,99 @@
+#!/usr/bin/env python3
+"""Measured runs of the other BASELINE configurations (the driver's bench line is C2 in bench.py):
+
+  c3  OS2014 parametric, [-1,1]^2, 1024^2 Kuhn triangles (2.10 M elements, 6.29 M DoFs, 75.5 M nnz per
+      component): (i) assembly of the affine part + the mu-component (smooth kappa, integration order 3,
+      problems/OS2014.hh:63-76) and (ii) 128 theta-lincombs A(mu_s) = A_aff + mu_s A_1, mu ~ U(0.1, 1)
+      (seed 14), materialised in HBM.
+  c4  SPE10-like 3520 x 1200 Q1 quads on [0,5]x[0,1], 8x8 subdomains (block numbering), synthetic
+      permeability, single GPU (the 8-GPU sharded form is bench.py --gpus 8 on the strip workload).
+Prints one JSON line per config."""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "dune-hdd_amd", "python"))
+
+
+def timed(fn, steps, warmup):
+    import torch
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(steps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / steps * 1e-3
+
+
+def c3(args):
+    import torch
+    import hdd_amd as H
+    n = args.n or 1024
+    grid = H.Grid.structured(H.SIMPLEX, n, n, (-1, -1), (1, 1))
+    loc = grid.local()
+    ctx = H.Context(0)
+    dm, dp = H.DeviceMesh(loc), H.DevicePattern(loc)
+    kx, ky = 4 * math.pi, 2 * math.pi
+    fns = [H.scalar_fn(H.FN_SINUSOID, 1.0, 0.75, kx, ky, order=3), H.scalar_fn(H.FN_SINUSOID, 0.0, -0.75, kx, ky, order=3)]
+    vals = [torch.empty(dp.nnz, dtype=torch.float64, device="cuda") for _ in range(2)]
+    t_asm = timed(lambda: H.assemble(ctx, dm, dp, fns, H.tensor_fn(), vals=vals), args.steps, args.warmup)
+    mus = np.random.default_rng(14).uniform(0.1, 1.0, args.samples)
+    theta = np.stack([np.ones_like(mus), mus], 1)          # A(mu) = A_aff + mu A_1 (ParameterFunctional "mu")
+    out = torch.empty((args.samples, dp.nnz), dtype=torch.float64, device="cuda")
+    t_lc = timed(lambda: H.affine_lincomb(ctx, vals, theta, out=out), max(1, args.steps // 4), 1)
+    dofs = 3 * loc.n_own
+    nif = int((loc.neighbors[:, :] >= 0).sum()) // 2
+    alg = 8 * dp.nnz * 2 + loc.n_own * (84 + 16) + 12 * nif
+    lc_bytes = args.samples * 8 * dp.nnz + 2 * 8 * dp.nnz * math.ceil(args.samples / 16)
+    return dict(config="c3_os2014_multiquery_kuhn%dx%d" % (n, n), dofs=dofs, nnz_per_component=dp.nnz,
+                components=2, assembly_ms=t_asm * 1e3, assembled_dofs_per_s=dofs / t_asm,
+                assembly_alg_GBps=alg / t_asm / 1e9, samples=args.samples, lincomb_ms=t_lc * 1e3,
+                lincomb_matrices_per_s=args.samples / t_lc, lincomb_GBps=lc_bytes / t_lc / 1e9)
+
+
+def c4(args):
+    import torch
+    import hdd_amd as H
+    nx, ny = (args.n or 3520), (args.n and args.n * 1200 // 3520) or 1200
+    grid = H.Grid.structured(H.CUBE, nx, ny, (0, 0), (5, 1), px=8, py=8)
+    loc = grid.local()
+    rng = np.random.default_rng(10)
+    k = torch.from_numpy(loc.checkerboard((0, 0), (5, 1), 100, 20, 10.0 ** rng.uniform(-3, 3, 2000))).cuda()
+    ctx = H.Context(0)
+    dm, dp = H.DeviceMesh(loc), H.DevicePattern(loc)
+    vals = [torch.empty(dp.nnz, dtype=torch.float64, device="cuda")]
+    fn = lambda: H.assemble(ctx, dm, dp, [H.scalar_fn(H.FN_CONST, 1.0)], H.tensor_fn(H.TENSOR_ISO_PER_ELEM, per_elem=k), vals=vals)
+    t = timed(fn, args.steps, args.warmup)
+    nif = int((loc.neighbors >= 0).sum()) // 2
+    alg = 8 * dp.nnz + loc.n_own * (104 + 8) + 12 * nif
+    dofs = 4 * loc.n_own
+    return dict(config="c4_spe10_q1_%dx%d_block8x8" % (nx, ny), dofs=dofs, nnz=dp.nnz, assembly_ms=t * 1e3,
+                assembled_dofs_per_s=dofs / t, alg_GBps=alg / t / 1e9, roofline_frac=alg / t / 8e12)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("configs", nargs="*", default=["c3", "c4"])
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--samples", type=int, default=128)
+    ap.add_argument("--n", type=int, default=0)
+    args = ap.parse_args()
+    import torch
+    torch.cuda.set_device(0)
+    for c in args.configs:
+        print(json.dumps(dict(c3=c3, c4=c4)[c](args)), flush=True)
+
+
+if __name__ == "__main__":
+    main()
