@@ -636,3 +636,35 @@ extern "C" int hdd_pattern_fill(int32_t elem_type, int64_t n_local, int64_t own_
   if (elem_ptr) elem_ptr[own_end - own_begin] = off;
   return HDD_OK;
 }
+
+// ------------------------------------------------------------------------------------------------
+// block operator maps (local / coupling operators of BlockSWIPDG)
+// ------------------------------------------------------------------------------------------------
+extern "C" int hdd_block_operator_map(const hdd_grid* g, int32_t ss, int32_t nn, const int64_t* row_ptr,
+                                      const int32_t* col, int64_t* out_row_ptr, int32_t* out_col, int64_t* out_src,
+                                      int64_t* nnz)
+{
+  if (!g || !row_ptr || !col || !nnz) return set_error(HDD_ERR_INVALID, "hdd_block_operator_map: null argument");
+  const Grid& G = *g->impl;
+  if (ss < 0 || nn < 0 || ss >= G.n_sub || nn >= G.n_sub)
+    return set_error(HDD_ERR_RANGE, "hdd_block_operator_map: 0 <= ss, nn < num_subdomains violated");
+  const int nb = G.nb;
+  const int64_t r0 = G.sub_first[ss] * nb, r1 = G.sub_first[ss + 1] * nb;
+  const int64_t c0 = G.sub_first[nn] * nb, c1 = G.sub_first[nn + 1] * nb;
+  int64_t k = 0;
+  if (out_row_ptr) out_row_ptr[0] = 0;
+  for (int64_t r = r0; r < r1; ++r) {
+    for (int64_t q = row_ptr[r]; q < row_ptr[r + 1]; ++q) {
+      const int64_t c = col[q];
+      if (c < c0 || c >= c1) continue;
+      if (out_col) {
+        out_col[k] = int32_t(c - c0);
+        if (out_src) out_src[k] = q;
+      }
+      ++k;
+    }
+    if (out_row_ptr) out_row_ptr[r - r0 + 1] = k;
+  }
+  *nnz = k;
+  return HDD_OK;
+}

@@ -297,3 +297,28 @@ extern "C" int hdd_soa_scatter(hdd_ctx* ctx, double* const* arrays, const int32_
   e = hipGetLastError();
   return e == hipSuccess ? HDD_OK : hip_fail(e, "hdd_soa_scatter: launch");
 }
+
+// ------------------------------------------------------------------------------------------------
+// value gather (block operator extraction)
+// ------------------------------------------------------------------------------------------------
+namespace {
+__global__ void __launch_bounds__(256) gather_values_kernel(const double* v, const int64_t* src, int64_t n, double* out)
+{
+  for (int64_t k = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; k < n; k += int64_t(gridDim.x) * blockDim.x)
+    out[k] = v[src[k]];
+}
+}  // namespace
+
+extern "C" int hdd_gather_values(hdd_ctx* ctx, const double* d_vals, const int64_t* d_src, int64_t n, double* d_out,
+                                 void* stream)
+{
+  if (!ctx || !d_vals || !d_src || !d_out || n < 0) return set_error(HDD_ERR_INVALID, "hdd_gather_values: invalid argument");
+  if (n == 0) return HDD_OK;
+  hipError_t e = hipSetDevice(ctx->device);
+  if (e != hipSuccess) return hip_fail(e, "hdd_gather_values: hipSetDevice");
+  const unsigned grid = unsigned(std::min<int64_t>((n + 255) / 256, 256 * 16));
+  hipLaunchKernelGGL(gather_values_kernel, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream), d_vals, d_src, n,
+                     d_out);
+  e = hipGetLastError();
+  return e == hipSuccess ? HDD_OK : hip_fail(e, "hdd_gather_values: launch");
+}

@@ -615,188 +615,6 @@ __device__ __forceinline__ double rsq_nr(double x)
   return y;
 }
 
-__global__ void __launch_bounds__(64)
-swipdg_p1_pwc_kernel(const AssembleArgs a)
-{
-  using E = Simplex;
-  constexpr int RB = 3 * 4 * 3;                 // max values of one element row block
-  extern __shared__ __attribute__((aligned(16))) double lds[];
-  const int lane = threadIdx.x;
-
-  const int64_t nwg = gridDim.x;
-  const int64_t b = blockIdx.x;
-  const int64_t q8 = nwg >> 3, r8 = nwg & 7, xcd = b & 7;
-  const int64_t tile = xcd * q8 + (xcd < r8 ? xcd : r8) + (b >> 3);
-
-  const int64_t t0 = a.own_begin + tile * 64;
-  const int64_t tend = t0 + 64 < a.own_end ? t0 + 64 : a.own_end;
-  const int64_t e0 = t0 + lane;
-  const bool active = e0 < tend;
-  const int64_t e = active ? e0 : t0;
-  const int64_t ne = a.n_local;
-  const int64_t* eptr = a.elem_ptr - a.own_begin;
-  const int64_t base = eptr[t0];
-  const int64_t base_al = base & ~int64_t(1);
-  const int64_t tile_end = eptr[tend];
-
-  double X[3], Y[3];
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    X[k] = a.coords[(2 * k) * ne + e];
-    Y[k] = a.coords[(2 * k + 1) * ne + e];
-  }
-  int32_t nbr[3];
-#pragma unroll
-  for (int f = 0; f < 3; ++f) nbr[f] = a.nbrs[f * ne + e];
-  const uint32_t finfo = a.finfo[e];
-  const Tensor Am = tensor_of(a, e);
-  const double ke = kappa_elem(a.kappa[0], e);
-  const int64_t my_off = eptr[e];
-
-  // own geometry and gradients  (J = [v1-v0, v2-v0], grad phi = J^{-T} grad phi_hat)
-  const double j00 = X[1] - X[0], j01 = X[2] - X[0], j10 = Y[1] - Y[0], j11 = Y[2] - Y[0];
-  const double det = j00 * j11 - j01 * j10;
-  const double id = rcp_nr(det);
-  const double i00 = j11 * id, i01 = -j01 * id, i10 = -j10 * id, i11 = j00 * id;
-  double g[3][2];
-  g[1][0] = i00; g[1][1] = i01;
-  g[2][0] = i10; g[2][1] = i11;
-  g[0][0] = -i00 - i10; g[0][1] = -i01 - i11;
-  double Ag[3][2];
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    Ag[k][0] = Am.a00 * g[k][0] + Am.a01 * g[k][1];
-    Ag[k][1] = Am.a01 * g[k][0] + Am.a11 * g[k][1];
-  }
-  const double adet = fabs(det);
-  const double osgn = det > 0.0 ? 1.0 : -1.0;
-
-  int nblk = 1, pos_self = 0, pos[3];
-#pragma unroll
-  for (int f = 0; f < 3; ++f) {
-    nblk += nbr[f] >= 0;
-    pos_self += (nbr[f] >= 0 && nbr[f] < e);
-  }
-#pragma unroll
-  for (int f = 0; f < 3; ++f) {
-    int p = (e < nbr[f]) ? 1 : 0;
-#pragma unroll
-    for (int q = 0; q < 3; ++q) p += (nbr[q] >= 0 && nbr[q] < nbr[f]);
-    pos[f] = p;
-  }
-  const int rowlen = nblk * 3;
-  double* img = active ? lds + (my_off - base_al) : lds + 64 * RB + 2;
-
-  // ---- volume (1-point rule, weight 1/2 |det J|) ----
-  double S[3][3];
-  {
-    const double fac = 0.5 * adet * ke;
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-#pragma unroll
-      for (int j = 0; j < 3; ++j) S[i][j] = fac * (Ag[j][0] * g[i][0] + Ag[j][1] * g[i][1]);
-  }
-
-  // ---- faces ----
-#pragma unroll
-  for (int f = 0; f < 3; ++f) {
-    const int32_t n = nbr[f];
-    if (n <= HDD_NBR_NEUMANN) continue;
-    const int fa = E::fv(f, 0), fb = E::fv(f, 1), fc = 3 - fa - fb;
-    const double tx = X[fb] - X[fa], ty = Y[fb] - Y[fa];
-    const double il = rsq_nr(tx * tx + ty * ty);
-    const double len = (tx * tx + ty * ty) * il;
-    const double nsc = E::face_sign(f) * osgn * il;
-    const double nx = ty * nsc, ny = -tx * nsc;
-    double Ae[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) Ae[k] = Ag[k][0] * nx + Ag[k][1] * ny;
-    const double dm = agn(Am, nx, ny, nx, ny);
-    const double ihp = a.beta == 1.0 ? il : rcp_nr(pow(len, a.beta));
-    const double half = 0.5 * len, third = len * (1.0 / 3.0), sixth = len * (1.0 / 6.0);
-    if (n >= 0) {
-      const uint32_t inf = (finfo >> (4 * f)) & 15u;
-      const int tw = int(inf & 7u);
-      const bool rev = (inf & 8u) != 0u;
-      const int ta = E::fv(tw, 0), tb = E::fv(tw, 1), to = 3 - ta - tb;
-      const int64_t ng = (a.debug_flags & 2) ? e : int64_t(n);   // ablation: no neighbour gathers
-      const double Ox = (a.debug_flags & 2) ? X[fc] + 0.5 * (X[fa] - X[fc]) + nx : a.coords[(2 * to) * ne + ng];
-      const double Oy = (a.debug_flags & 2) ? Y[fc] + 0.5 * (Y[fa] - Y[fc]) + ny : a.coords[(2 * to + 1) * ne + ng];
-      const Tensor Ap = tensor_of(a, ng);
-      const double kn = kappa_elem(a.kappa[0], ng);
-      const double dp = agn(Ap, nx, ny, nx, ny);
-      const double rs = rcp_nr(dp + dm);
-      const double gamma = (dp * dm) * rs;
-      const double w_plus = dm * rs, w_minus = dp * rs;
-      const double pen = (ke * kn * a.sigma_inner * gamma) * ihp;
-      // neighbour barycentric gradients of the roles A (= my a), B (= my b), O, dotted with A+ n
-      const double Ax = X[fa], Ay = Y[fa], Bx = X[fb], By = Y[fb];
-      const double iD = rcp_nr((Bx - Ax) * (Oy - Ay) - (By - Ay) * (Ox - Ax));
-      const double mx = Ap.a00 * nx + Ap.a01 * ny, my = Ap.a01 * nx + Ap.a11 * ny;
-      const double AnA = ((By - Oy) * mx + (Ox - Bx) * my) * iD;
-      const double AnB = ((Oy - Ay) * mx + (Ax - Ox) * my) * iD;
-      const double AnO = ((Ay - By) * mx + (Bx - Ax) * my) * iD;
-      // entity/neighbour block, column slots of the roles in the neighbour's local numbering
-      const int jA = rev ? tb : ta, jB = rev ? ta : tb;
-      const double cpl = -w_plus * kn;          // consistency term of the neighbour side
-      const double sym = w_minus * ke;          // symmetry term of the entity side
-#pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        double* row = img + i * rowlen + pos[f] * 3;
-        const double m1i = i == fc ? 0.0 : half;
-        const double vA = cpl * AnA * m1i + sym * Ae[i] * half - pen * (i == fc ? 0.0 : (i == fa ? third : sixth));
-        const double vB = cpl * AnB * m1i + sym * Ae[i] * half - pen * (i == fc ? 0.0 : (i == fb ? third : sixth));
-        const double vO = cpl * AnO * m1i;
-        if (!(a.debug_flags & 4)) {
-          row[jA] = vA;
-          row[jB] = vB;
-          row[to] = vO;
-        } else {
-          S[i][0] += vA + vB + vO;   // ablation: keep the values alive without LDS traffic
-        }
-      }
-      // entity/entity block
-#pragma unroll
-      for (int i = 0; i < 3; ++i)
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          const double m1i = i == fc ? 0.0 : half, m1j = j == fc ? 0.0 : half;
-          const double mm = (i == fc || j == fc) ? 0.0 : (i == j ? third : sixth);
-          S[i][j] += -w_minus * ke * (Ae[j] * m1i + Ae[i] * m1j) + pen * mm;
-        }
-    } else {   // Dirichlet: SWIPDG::BoundaryLHS
-      const double pen = (a.sigma_boundary * ke * dm) * ihp;
-#pragma unroll
-      for (int i = 0; i < 3; ++i)
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          const double m1i = i == fc ? 0.0 : half, m1j = j == fc ? 0.0 : half;
-          const double mm = (i == fc || j == fc) ? 0.0 : (i == j ? third : sixth);
-          S[i][j] += -ke * (Ae[j] * m1i + Ae[i] * m1j) + pen * mm;
-        }
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < 3; ++i)
-#pragma unroll
-    for (int j = 0; j < 3; ++j) img[i * rowlen + pos_self * 3 + j] = S[i][j];
-
-  __syncthreads();
-  double* out = a.vals[0];
-  if (a.debug_flags & 1) {   // ablation: no global stores (keep a dependency on the image)
-    if (lds[lane] == 1.2345e-300) out[base] = 0.0;
-    return;
-  }
-  const int64_t n2 = (tile_end - base_al) >> 1;
-  for (int64_t k = lane; k < n2; k += 64) {
-    const int64_t gi = base_al + 2 * k;
-    const dvec2 v = *reinterpret_cast<const dvec2*>(lds + 2 * k);
-    if (gi >= base) __builtin_nontemporal_store(v, reinterpret_cast<dvec2*>(out + gi));
-    else out[gi + 1] = v.y;
-  }
-  if (((tile_end - base_al) & 1) && lane == 0) out[tile_end - 1] = lds[tile_end - 1 - base_al];
-}
-
 // ------------------------------------------------------------------------------------------------
 // Persistent, software-pipelined variant of the P1 kernel.
 //
@@ -814,20 +632,6 @@ struct P1Own {
   Tensor A;
   double ke;
 };
-
-// offset of this lane's row block inside the tile: sum of 9*nblk over the active lanes below it
-// (the pattern's elem_ptr rule), from two ballots instead of a per-element elem_ptr load
-__device__ __forceinline__ int p1_tile_offset(const P1Own& o, bool active)
-{
-  const int c = int(o.nbr[0] >= 0) + int(o.nbr[1] >= 0) + int(o.nbr[2] >= 0);   // interior faces
-  const uint64_t act = __ballot(active);
-  const uint64_t b0 = __ballot(active && (c & 1));
-  const uint64_t b1 = __ballot(active && (c & 2));
-  auto below = [](uint64_t m) {
-    return int(__builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u)));
-  };
-  return 9 * (below(act) + below(b0) + 2 * below(b1));
-}
 struct P1Gat {
   double Ox[3], Oy[3];
   Tensor Ap[3];
@@ -888,7 +692,7 @@ __device__ __forceinline__ void p1_load_gat(const AssembleArgs& a, int64_t e, co
   }
 }
 
-// the per-element math of swipdg_p1_pwc_kernel, on preloaded data; writes the row block into `img`
+// P1 closed-form per-element math on preloaded data (role form, see above); writes the row block into `img`
 __device__ __forceinline__ void p1_compute(const AssembleArgs& a, int64_t e, const P1Own& o, const P1Gat& gt,
                                            double* img)
 {
@@ -1005,74 +809,330 @@ __device__ __forceinline__ void p1_compute(const AssembleArgs& a, int64_t e, con
 }
 
 typedef int ivec4 __attribute__((ext_vector_type(4)));
-constexpr int P1_RB = 36;                          // values of an interior P1 row block
-constexpr int P1_IMG = 64 * P1_RB;                 // doubles of a full tile image
-constexpr int P1_STORES = (P1_IMG / 2 + 63) / 64;  // 16-byte stores per lane that cover a tile (18)
 
-template <int TK, int KK>
-__global__ void __launch_bounds__(64, 2)
-swipdg_p1_pwc_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
+// ------------------------------------------------------------------------------------------------
+// Generic thread-per-element policy (Q1 parallelograms, smooth coefficients): quadrature at compile-time
+// points on my side, "role" coordinates on the neighbour side.  Roles are named by physical position
+// (A = my fv(f,0), B = my fv(f,1), third role = the neighbour vertex next to A off the face, fourth
+// (cubes) = next to B) and numbered like the reference element, so the neighbour's basis in role
+// coordinates is E::shape at the compile-time point (s, 0) and only the LDS column slots depend on the
+// twin face / reversal.  Gathers per face: one neighbour vertex (2 doubles), its tensor, its kappa.
+// ------------------------------------------------------------------------------------------------
+template <class E>
+struct GOwn {
+  double X[E::NV], Y[E::NV];
+  int32_t nbr[E::NF];
+  uint32_t finfo;
+  Tensor A;
+  double ke;
+};
+template <class E>
+struct GGat {
+  double Cx[E::NF], Cy[E::NF];
+  Tensor Ap[E::NF];
+  double kn[E::NF];
+};
+
+template <class E>
+__device__ __forceinline__ int role_slot(uint32_t finfo, int f, int r)
 {
+  const uint32_t inf = (finfo >> (4 * f)) & 15u;
+  const int tw = int(inf & 7u);
+  const bool rev = (inf & 8u) != 0u;
+  const int ka = rev ? 1 : 0;
+  if (r == 0) return E::fv(tw, ka);
+  if (r == 1) return E::fv(tw, 1 - ka);
+  if constexpr (E::NV == 3) return 3 - E::fv(tw, 0) - E::fv(tw, 1);
+  else return r == 2 ? E::fv(tw ^ 1, ka) : E::fv(tw ^ 1, 1 - ka);
+}
+
+template <class E, int NQV, int NQF, int TK, int KK>
+struct GenericPolicy {
+  static constexpr int NB = E::NB, NF = E::NF, NV = E::NV;
+  static constexpr int RB = (NF + 1) * NB * NB;
+  using Own = GOwn<E>;
+  using Gat = GGat<E>;
+
+  __device__ static void load_own(const AssembleArgs& a, int64_t e, Own& o)
+  {
+    const int64_t ne = a.n_local;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      o.X[k] = a.coords[(2 * k) * ne + e];
+      o.Y[k] = a.coords[(2 * k + 1) * ne + e];
+    }
+#pragma unroll
+    for (int f = 0; f < NF; ++f) o.nbr[f] = a.nbrs[f * ne + e];
+    o.finfo = a.finfo[e];
+    o.A = tensor_k<TK>(a, e);
+    o.ke = KK == HDD_FN_SINUSOID ? 0.0 : kappa_k<KK == HDD_FN_PER_ELEM ? HDD_FN_PER_ELEM : HDD_FN_CONST>(a, e);
+  }
+
+  __device__ static void load_gat(const AssembleArgs& a, int64_t e, const Own& o, Gat& g)
+  {
+    const int64_t ne = a.n_local;
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+      const int64_t n = o.nbr[f] >= 0 ? int64_t(o.nbr[f]) : e;
+      const int c = role_slot<E>(o.finfo, f, 2);
+      g.Cx[f] = a.coords[(2 * c) * ne + n];
+      g.Cy[f] = a.coords[(2 * c + 1) * ne + n];
+      g.Ap[f] = tensor_k<TK>(a, n);
+      g.kn[f] = KK == HDD_FN_SINUSOID ? 0.0 : kappa_k<KK == HDD_FN_PER_ELEM ? HDD_FN_PER_ELEM : HDD_FN_CONST>(a, n);
+    }
+  }
+
+  __device__ static double kap(const AssembleArgs& a, double x, double y)
+  {
+    const KappaArg& K = a.kappa[0];
+    return K.c + K.b * sin(K.kx * x + K.ky * y);
+  }
+
+  __device__ static int n_interior(const Own& o)
+  {
+    int c = 0;
+#pragma unroll
+    for (int f = 0; f < NF; ++f) c += o.nbr[f] >= 0;
+    return c;
+  }
+
+  __device__ static void compute(const AssembleArgs& a, int64_t e, const Own& o, const Gat& gt, double* img)
+  {
+    Geom G;
+    G.init(o.X[0], o.Y[0], o.X[1], o.Y[1], o.X[2], o.Y[2]);
+    const double adet = fabs(G.det);
+    const double osgn = G.det > 0.0 ? 1.0 : -1.0;
+    int pos_self = 0, pos[NF];
+#pragma unroll
+    for (int f = 0; f < NF; ++f) pos_self += (o.nbr[f] >= 0 && o.nbr[f] < e);
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+      int p = (e < o.nbr[f]) ? 1 : 0;
+#pragma unroll
+      for (int q = 0; q < NF; ++q) p += (o.nbr[q] >= 0 && o.nbr[q] < o.nbr[f]);
+      pos[f] = p;
+    }
+    const int rowlen = (n_interior(o) + 1) * NB;
+    double S[NB][NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+#pragma unroll
+      for (int j = 0; j < NB; ++j) S[i][j] = 0.0;
+    // ---- LocalEvaluation::Elliptic ----
+#pragma unroll
+    for (int q = 0; q < NQV; ++q) {
+      double phi[NB], ghx[NB], ghy[NB], gx[NB], gy[NB];
+      E::shape(VolRule<E, NQV>::x(q), VolRule<E, NQV>::y(q), phi, ghx, ghy);
+#pragma unroll
+      for (int k = 0; k < NB; ++k) G.grad(ghx[k], ghy[k], gx[k], gy[k]);
+      double kq = o.ke;
+      if constexpr (KK == HDD_FN_SINUSOID) {
+        double px, py;
+        G.global(VolRule<E, NQV>::x(q), VolRule<E, NQV>::y(q), px, py);
+        kq = kap(a, px, py);
+      }
+      const double fac = VolRule<E, NQV>::w(q) * adet * kq;
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        const double Agx = o.A.a00 * gx[j] + o.A.a01 * gy[j];
+        const double Agy = o.A.a01 * gx[j] + o.A.a11 * gy[j];
+#pragma unroll
+        for (int i = 0; i < NB; ++i) S[i][j] += fac * (Agx * gx[i] + Agy * gy[i]);
+      }
+    }
+    // ---- faces ----
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+      const int32_t n = o.nbr[f];
+      if (n <= HDD_NBR_NEUMANN) continue;
+      const int fa = E::fv(f, 0), fb = E::fv(f, 1);
+      const double Ax = o.X[fa], Ay = o.Y[fa], Bx = o.X[fb], By = o.Y[fb];
+      const double tx = Bx - Ax, ty = By - Ay;
+      const double il = rsq_nr(tx * tx + ty * ty);
+      const double len = (tx * tx + ty * ty) * il;
+      const double nsc = E::face_sign(f) * osgn * il;
+      const double nx = ty * nsc, ny = -tx * nsc;
+      const double dm = agn(o.A, nx, ny, nx, ny);
+      const double ihp = a.beta == 1.0 ? il : rcp_nr(pow(len, a.beta));
+      const double rax = E::rv(fa, 0), ray = E::rv(fa, 1), rbx = E::rv(fb, 0), rby = E::rv(fb, 1);
+      if (n >= 0) {
+        Geom Hn;   // neighbour in role coordinates: A = (0,0), B = (1,0), third role = (0,1)
+        Hn.init(Ax, Ay, Bx, By, gt.Cx[f], gt.Cy[f]);
+        const Tensor Ap = gt.Ap[f];
+        const double dp = agn(Ap, nx, ny, nx, ny);
+        const double rs = rcp_nr(dp + dm);
+        const double gamma = (dp * dm) * rs;
+        const double w_plus = dm * rs, w_minus = dp * rs;
+        double EN[NB][NB];
+#pragma unroll
+        for (int i = 0; i < NB; ++i)
+#pragma unroll
+          for (int j = 0; j < NB; ++j) EN[i][j] = 0.0;
+#pragma unroll
+        for (int q = 0; q < NQF; ++q) {
+          const double s = Gauss01<NQF>::s(q);
+          double pe[NB], ghx[NB], ghy[NB], gex[NB], gey[NB];
+          E::shape(rax + s * (rbx - rax), ray + s * (rby - ray), pe, ghx, ghy);
+#pragma unroll
+          for (int k = 0; k < NB; ++k) G.grad(ghx[k], ghy[k], gex[k], gey[k]);
+          double pn[NB], hhx[NB], hhy[NB];
+          E::shape(s, 0.0, pn, hhx, hhy);
+          double kme = o.ke, knb = gt.kn[f];
+          if constexpr (KK == HDD_FN_SINUSOID) {
+            kme = kap(a, Ax + s * tx, Ay + s * ty);
+            knb = kme;
+          }
+          const double pen = (kme * knb * a.sigma_inner * gamma) * ihp;
+          const double fac = Gauss01<NQF>::w(q) * len;
+          double Ae[NB], An[NB];
+#pragma unroll
+          for (int k = 0; k < NB; ++k) {
+            double hx, hy;
+            Hn.grad(hhx[k], hhy[k], hx, hy);
+            Ae[k] = agn(o.A, gex[k], gey[k], nx, ny);
+            An[k] = agn(Ap, hx, hy, nx, ny);
+          }
+#pragma unroll
+          for (int i = 0; i < NB; ++i)
+#pragma unroll
+            for (int j = 0; j < NB; ++j) {
+              S[i][j] += fac * (-w_minus * kme * Ae[j] * pe[i] - w_minus * kme * pe[j] * Ae[i] + pen * pe[j] * pe[i]);
+              EN[i][j] += fac * (-w_plus * knb * An[j] * pe[i] + w_minus * kme * pn[j] * Ae[i] - pen * pn[j] * pe[i]);
+            }
+        }
+        int slot[NB];
+#pragma unroll
+        for (int r = 0; r < NB; ++r) slot[r] = role_slot<E>(o.finfo, f, r);
+#pragma unroll
+        for (int i = 0; i < NB; ++i) {
+          double* row = img + i * rowlen + pos[f] * NB;
+#pragma unroll
+          for (int r = 0; r < NB; ++r) row[slot[r]] = EN[i][r];
+        }
+      } else {   // Dirichlet: SWIPDG::BoundaryLHS
+#pragma unroll
+        for (int q = 0; q < NQF; ++q) {
+          const double s = Gauss01<NQF>::s(q);
+          double pe[NB], ghx[NB], ghy[NB], gex[NB], gey[NB];
+          E::shape(rax + s * (rbx - rax), ray + s * (rby - ray), pe, ghx, ghy);
+#pragma unroll
+          for (int k = 0; k < NB; ++k) G.grad(ghx[k], ghy[k], gex[k], gey[k]);
+          double kme = o.ke;
+          if constexpr (KK == HDD_FN_SINUSOID) kme = kap(a, Ax + s * tx, Ay + s * ty);
+          const double pen = (a.sigma_boundary * kme * dm) * ihp;
+          const double fac = Gauss01<NQF>::w(q) * len;
+          double Ae[NB];
+#pragma unroll
+          for (int k = 0; k < NB; ++k) Ae[k] = agn(o.A, gex[k], gey[k], nx, ny);
+#pragma unroll
+          for (int i = 0; i < NB; ++i)
+#pragma unroll
+            for (int j = 0; j < NB; ++j)
+              S[i][j] += fac * (-kme * Ae[j] * pe[i] - kme * pe[j] * Ae[i] + pen * pe[j] * pe[i]);
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+#pragma unroll
+      for (int j = 0; j < NB; ++j) img[i * rowlen + pos_self * NB + j] = S[i][j];
+  }
+};
+
+// P1 simplex, piecewise-constant coefficients: the closed-form policy (p1_compute above)
+template <int TK, int KK>
+struct P1PwcPolicy {
+  static constexpr int NB = 3, NF = 3;
+  static constexpr int RB = 36;
+  using Own = P1Own;
+  using Gat = P1Gat;
+  __device__ static void load_own(const AssembleArgs& a, int64_t e, Own& o) { p1_load_own<TK, KK>(a, e, o); }
+  __device__ static void load_gat(const AssembleArgs& a, int64_t e, const Own& o, Gat& g) { p1_load_gat<TK, KK>(a, e, o, g); }
+  __device__ static int n_interior(const Own& o) { return int(o.nbr[0] >= 0) + int(o.nbr[1] >= 0) + int(o.nbr[2] >= 0); }
+  __device__ static void compute(const AssembleArgs& a, int64_t e, const Own& o, const Gat& g, double* img)
+  {
+    p1_compute(a, e, o, g, img);
+  }
+};
+
+// offset of this lane's row block inside the tile: NB^2 * sum over the active lanes below of (1 + interior
+// faces) -- the pattern's elem_ptr rule -- from ballots + mbcnt instead of a per-element elem_ptr load
+template <int NB>
+__device__ __forceinline__ int tile_offset(int c, bool active)
+{
+  auto below = [](uint64_t m) {
+    return int(__builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u)));
+  };
+  int sum = below(__ballot(active));
+  sum += below(__ballot(active && (c & 1)));
+  sum += 2 * below(__ballot(active && (c & 2)));
+  sum += 4 * below(__ballot(active && (c & 4)));
+  return NB * NB * sum;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Persistent, software-pipelined driver (see the P1 comment above): per wave a sequence of 64-element
+// tiles, memory order [prefetch own data t+1][compute t -> LDS][gathers t+1][stores t].
+// ------------------------------------------------------------------------------------------------
+template <class P>
+__global__ void __launch_bounds__(64, 1)
+swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
+{
+  constexpr int IMG = 64 * P::RB;
+  constexpr int STORES = (IMG / 2 + 63) / 64;
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const int lane = threadIdx.x;
-  // XCD-aware schedule: the 8 XCDs get contiguous eighths of the tile range; the workgroups of one XCD
-  // sweep their eighth together, so neighbour rows above / below are recent in that XCD's L2.
   const int64_t G = gridDim.x, b = blockIdx.x;
   int64_t t, t_end, t_step;
   if (G >= n_tiles) {
     t = b; t_end = b + 1; t_step = 1;
-  } else {
+  } else {   // XCD-aware: the 8 XCDs sweep contiguous eighths of the tile range
     const int64_t x = b & 7, w = b >> 3, gx = G >> 3;
     t = (n_tiles * x) / 8 + w;
     t_end = (n_tiles * (x + 1)) / 8;
     t_step = gx;
   }
   if (t >= t_end) return;
-  double* scratch = lds + P1_IMG + 2;
-
+  double* scratch = lds + IMG + 2;
   auto elem_of = [&](int64_t tile) {
     const int64_t t0 = a.own_begin + tile * 64;
     const int64_t e0 = t0 + lane;
     return e0 < a.own_end ? e0 : t0;
   };
-  // tile bounds through the scalar cache (lgkmcnt, not the in-order vmcnt the streams share)
-  auto bounds = [&](int64_t tile, int64_t& base, int64_t& tile_end) {
+  auto bounds = [&](int64_t tile, int64_t& base, int64_t& tile_end) {   // scalar loads (lgkmcnt)
     const int64_t t0 = __builtin_amdgcn_readfirstlane(a.own_begin + tile * 64);
     const int64_t tend = t0 + 64 < a.own_end ? t0 + 64 : a.own_end;
     base = __builtin_amdgcn_readfirstlane(a.elem_ptr[t0 - a.own_begin]);
     tile_end = __builtin_amdgcn_readfirstlane(a.elem_ptr[tend - a.own_begin]);
   };
   int64_t e = elem_of(t);
-  P1Own own;
-  P1Gat gat;
-  p1_load_own<TK, KK>(a, e, own);
-  p1_load_gat<TK, KK>(a, e, own, gat);
+  typename P::Own own;
+  typename P::Gat gat;
+  P::load_own(a, e, own);
+  P::load_gat(a, e, own, gat);
   int64_t base, tile_end;
   bounds(t, base, tile_end);
   double* out = a.vals[0];
   for (;;) {
-    const int64_t tn = t + t_step < t_end ? t + t_step : t;
     const bool has_next = t + t_step < t_end;
+    const int64_t tn = has_next ? t + t_step : t;
     const int64_t en = elem_of(tn);
-    P1Own own_n;
-    p1_load_own<TK, KK>(a, en, own_n);                // prefetch, in flight during this tile's compute
+    typename P::Own own_n;
+    P::load_own(a, en, own_n);
     int64_t base_n, tile_end_n;
     bounds(tn, base_n, tile_end_n);
 
-    const int64_t t0 = a.own_begin + t * 64;
-    const bool active = t0 + lane < a.own_end;
+    const bool active = a.own_begin + t * 64 + lane < a.own_end;
     const int64_t base_al = base & ~int64_t(1);
-    const int off = p1_tile_offset(own, active) + int(base - base_al);
-    p1_compute(a, e, own, gat, active ? lds + off : scratch);
+    const int off = tile_offset<P::NB>(P::n_interior(own), active) + int(base - base_al);
+    P::compute(a, e, own, gat, active ? lds + off : scratch);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
-    P1Gat gat_n;
-    p1_load_gat<TK, KK>(a, en, own_n, gat_n);         // issued before this tile's stores
+    typename P::Gat gat_n;
+    P::load_gat(a, en, own_n, gat_n);
 
-    // stream [base, tile_end): head / tail singles by all lanes (same value), even-aligned body in
-    // fixed-count 16-byte buffer stores, range-checked by the descriptor
     const int64_t start = (base + 1) & ~int64_t(1);
     const int64_t stop = tile_end & ~int64_t(1);
     const double head = lds[base - base_al];
@@ -1083,9 +1143,9 @@ swipdg_p1_pwc_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
     __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(out + start, (short)0, nbytes, 0x00020000);
     const double* src = lds + (start - base_al);
 #pragma unroll
-    for (int k = 0; k < P1_STORES; ++k) {
+    for (int k = 0; k < STORES; ++k) {
       const int idx = 2 * (lane + 64 * k);
-      const int li = idx < P1_IMG ? idx : 0;
+      const int li = idx < IMG ? idx : 0;
       const dvec2 v = *reinterpret_cast<const dvec2*>(src + li);
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ivec4, v), rsrc, idx * 8, 0, 0);
     }
@@ -1122,49 +1182,74 @@ static hipError_t launch_t(const AssembleArgs& a, hipStream_t s)
   return hipSuccess;
 }
 
-static hipError_t launch_p1_pwc(const AssembleArgs& a, hipStream_t s)
+template <class P>
+static hipError_t launch_persistent(const AssembleArgs& a, hipStream_t s)
 {
   const int64_t n_own = a.own_end - a.own_begin;
   if (n_own <= 0) return hipSuccess;
   const int64_t tiles = (n_own + 63) / 64;
-  const size_t lds = (size_t(64) * 36 + 2 + 36) * sizeof(double);
-  if (!(a.debug_flags & 64)) {   // persistent pipelined kernel (default); flag 64 = one tile per workgroup
-    int dev = 0, cus = 256;
-    hipGetDevice(&dev);
-    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    int wgcu = 4;   // measured best on MI355X (sweep 1..8: 4 -> 0.301 ms at C2)
-    if (const char* w = getenv("HDD_P1_WGCU")) wgcu = atoi(w);   // profiling sweeps only
-    const int64_t G = std::min<int64_t>(tiles, int64_t(cus) * wgcu);
-    for (int c = 0; c < a.n_comp; ++c) {
-      AssembleArgs ac = a;
-      ac.n_comp = 1;
-      ac.kappa[0] = a.kappa[c];
-      ac.vals[0] = a.vals[c];
-      const int tk = ac.tkind, kk = ac.kappa[0].kind;
-      if (tk == HDD_TENSOR_ISO_PER_ELEM && kk == HDD_FN_CONST)
-        hipLaunchKernelGGL((swipdg_p1_pwc_persistent_kernel<HDD_TENSOR_ISO_PER_ELEM, HDD_FN_CONST>), dim3(unsigned(G)), dim3(64), lds, s, ac, tiles);
-      else if (tk == HDD_TENSOR_ISO_PER_ELEM && kk == HDD_FN_PER_ELEM)
-        hipLaunchKernelGGL((swipdg_p1_pwc_persistent_kernel<HDD_TENSOR_ISO_PER_ELEM, HDD_FN_PER_ELEM>), dim3(unsigned(G)), dim3(64), lds, s, ac, tiles);
-      else if (tk == HDD_TENSOR_CONST && kk == HDD_FN_CONST)
-        hipLaunchKernelGGL((swipdg_p1_pwc_persistent_kernel<HDD_TENSOR_CONST, HDD_FN_CONST>), dim3(unsigned(G)), dim3(64), lds, s, ac, tiles);
-      else if (tk == HDD_TENSOR_CONST && kk == HDD_FN_PER_ELEM)
-        hipLaunchKernelGGL((swipdg_p1_pwc_persistent_kernel<HDD_TENSOR_CONST, HDD_FN_PER_ELEM>), dim3(unsigned(G)), dim3(64), lds, s, ac, tiles);
-      else if (tk == HDD_TENSOR_SYM_PER_ELEM && kk == HDD_FN_CONST)
-        hipLaunchKernelGGL((swipdg_p1_pwc_persistent_kernel<HDD_TENSOR_SYM_PER_ELEM, HDD_FN_CONST>), dim3(unsigned(G)), dim3(64), lds, s, ac, tiles);
-      else
-        hipLaunchKernelGGL((swipdg_p1_pwc_persistent_kernel<HDD_TENSOR_SYM_PER_ELEM, HDD_FN_PER_ELEM>), dim3(unsigned(G)), dim3(64), lds, s, ac, tiles);
-      const hipError_t e = hipGetLastError();
-      if (e != hipSuccess) return e;
-    }
-    return hipSuccess;
-  }
+  const size_t lds = (size_t(64) * P::RB + 2 + P::RB) * sizeof(double);
+  int dev = 0, cus = 256;
+  hipGetDevice(&dev);
+  hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  int wgcu = 4;   // measured best on MI355X for P1 (sweep 1..8: profiles/r01/sweep_wg_per_cu.log)
+  if (const char* w = getenv("HDD_P1_WGCU")) wgcu = atoi(w);   // profiling sweeps only
+  wgcu = std::max(1, std::min<int>(wgcu, int((160 * 1024) / lds)));   // resident by LDS (Q1 tiles: 3 per CU)
+  const int64_t G = std::min<int64_t>(tiles, int64_t(cus) * wgcu);
   for (int c = 0; c < a.n_comp; ++c) {
     AssembleArgs ac = a;
     ac.n_comp = 1;
     ac.kappa[0] = a.kappa[c];
     ac.vals[0] = a.vals[c];
-    hipLaunchKernelGGL(swipdg_p1_pwc_kernel, dim3(unsigned(tiles)), dim3(64), lds, s, ac);
+    hipLaunchKernelGGL(swipdg_persistent_kernel<P>, dim3(unsigned(G)), dim3(64), lds, s, ac, tiles);
     const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+// instantiate a policy for the runtime (tensor kind, kappa kind) pair
+template <template <int, int> class PT>
+static hipError_t dispatch_kinds(const AssembleArgs& a, hipStream_t s, bool smooth)
+{
+  const int tk = a.tkind, kk = a.kappa[0].kind;
+  if (smooth) {
+    if (tk == HDD_TENSOR_CONST) return launch_persistent<PT<HDD_TENSOR_CONST, HDD_FN_SINUSOID>>(a, s);
+    if (tk == HDD_TENSOR_ISO_PER_ELEM) return launch_persistent<PT<HDD_TENSOR_ISO_PER_ELEM, HDD_FN_SINUSOID>>(a, s);
+    return launch_persistent<PT<HDD_TENSOR_SYM_PER_ELEM, HDD_FN_SINUSOID>>(a, s);
+  }
+  const bool pe = kk == HDD_FN_PER_ELEM;
+  if (tk == HDD_TENSOR_CONST)
+    return pe ? launch_persistent<PT<HDD_TENSOR_CONST, HDD_FN_PER_ELEM>>(a, s) : launch_persistent<PT<HDD_TENSOR_CONST, HDD_FN_CONST>>(a, s);
+  if (tk == HDD_TENSOR_ISO_PER_ELEM)
+    return pe ? launch_persistent<PT<HDD_TENSOR_ISO_PER_ELEM, HDD_FN_PER_ELEM>>(a, s) : launch_persistent<PT<HDD_TENSOR_ISO_PER_ELEM, HDD_FN_CONST>>(a, s);
+  return pe ? launch_persistent<PT<HDD_TENSOR_SYM_PER_ELEM, HDD_FN_PER_ELEM>>(a, s) : launch_persistent<PT<HDD_TENSOR_SYM_PER_ELEM, HDD_FN_CONST>>(a, s);
+}
+
+template <int TK, int KK> using P1Pwc = P1PwcPolicy<TK, KK>;
+template <int TK, int KK> using Q1Pwc = GenericPolicy<Cube, 1, 2, TK, KK>;
+template <int TK, int KK> using Q1Smooth3 = GenericPolicy<Cube, 4, 3, TK, KK>;
+template <int TK, int KK> using P1Smooth3 = GenericPolicy<Simplex, 6, 3, TK, KK>;
+
+// one launch per component: components of one call may differ in kind (affine part const, component
+// per-element, ...) -- the kinds are compile-time inside the kernels
+static hipError_t launch_components(const AssembleArgs& a, int nqv, int nqf, hipStream_t s, bool* supported)
+{
+  for (int c = 0; c < a.n_comp; ++c) {
+    AssembleArgs ac = a;
+    ac.n_comp = 1;
+    ac.kappa[0] = a.kappa[c];
+    ac.vals[0] = a.vals[c];
+    const bool smooth = ac.kappa[0].kind == HDD_FN_SINUSOID;
+    hipError_t e = hipSuccess;
+    if (ac.elem_type == HDD_SIMPLEX && nqv == 1 && nqf == 2 && !smooth) e = dispatch_kinds<P1Pwc>(ac, s, false);
+    else if (ac.elem_type == HDD_SIMPLEX && nqv == 6 && nqf == 3 && smooth) e = dispatch_kinds<P1Smooth3>(ac, s, true);
+    else if (ac.elem_type == HDD_CUBE && nqv == 1 && nqf == 2 && !smooth) e = dispatch_kinds<Q1Pwc>(ac, s, false);
+    else if (ac.elem_type == HDD_CUBE && nqv == 4 && nqf == 3 && smooth) e = dispatch_kinds<Q1Smooth3>(ac, s, true);
+    else {
+      *supported = false;
+      return hipSuccess;
+    }
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
@@ -1185,10 +1270,15 @@ int face_points(int order)
 hipError_t launch_assemble(const AssembleArgs& a, int nqv, int nqf, hipStream_t s, bool* supported)
 {
   *supported = true;
+  if (!(a.debug_flags & 64)) {
+    const hipError_t e = launch_components(a, nqv, nqf, s, supported);
+    if (*supported) return e;
+    *supported = true;   // fall through to the wave-per-row kernels for the remaining rules
+  }
   bool pwc = true;
   for (int c = 0; c < a.n_comp; ++c) pwc &= a.kappa[c].kind != HDD_FN_SINUSOID;
   if (a.elem_type == HDD_SIMPLEX) {
-    if (nqv == 1 && nqf == 2) return pwc ? launch_p1_pwc(a, s) : launch_t<Simplex, 1, 2, false>(a, s);
+    if (nqv == 1 && nqf == 2) return pwc ? launch_t<Simplex, 1, 2, true>(a, s) : launch_t<Simplex, 1, 2, false>(a, s);
     if (nqv == 6 && nqf == 3) return launch_t<Simplex, 6, 3, false>(a, s);
     if (nqv == 3 && nqf == 2) return launch_t<Simplex, 3, 2, false>(a, s);
   } else {

@@ -212,6 +212,19 @@ int hdd_soa_gather(hdd_ctx* ctx, const double* const* arrays, const int32_t* row
 int hdd_soa_scatter(hdd_ctx* ctx, double* const* arrays, const int32_t* rows, int32_t n_arrays, int64_t ld,
                     int64_t dst_offset, int64_t n, const double* d_buf, void* stream);
 
+/* ---------------------------------------------------------------------------------------------- */
+/* block operators -- replaces BlockSWIPDG::get_local_operator(ss) / get_coupling_operator(ss, nn)   */
+/* (block-swipdg.hh:625-676): in the subdomain-major numbering they are the diagonal / off-diagonal   */
+/* blocks of the global matrix, extracted through a value map built once from the pattern.            */
+/* ---------------------------------------------------------------------------------------------- */
+/* rows of subdomain ss, columns of subdomain nn (ss == nn: local operator), local numbering on both
+ * sides.  Call with out_col == NULL to get *nnz; out_row_ptr [rows+1], out_col / out_src [nnz]
+ * (out_src = index of each extracted value in the global value array).  Host arrays. */
+int hdd_block_operator_map(const hdd_grid* g, int32_t ss, int32_t nn, const int64_t* row_ptr, const int32_t* col,
+                           int64_t* out_row_ptr, int32_t* out_col, int64_t* out_src, int64_t* nnz);
+/* d_out[k] = d_vals[d_src[k]] for k < n (device arrays) */
+int hdd_gather_values(hdd_ctx* ctx, const double* d_vals, const int64_t* d_src, int64_t n, double* d_out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
