@@ -42,6 +42,9 @@ def parse():
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo = rehearsal of the N-rank path on one GPU (host-staged halo)")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="N>1: exchange the halo before the whole assembly instead of overlapping it "
+                         "with the interior tiles")
     return ap.parse_args()
 
 
@@ -131,8 +134,24 @@ def main():
     alg_bytes = 8 * dpat.nnz * qp1 + n_own * (84 + 8 * qp1) + 12 * nif     # SURVEY.md 8(d) formula
 
     stream = torch.cuda.current_stream()
+    overlap = halo is not None and not args.no_overlap
+    if overlap:
+        t_in, t_bd = H.halo_tiles(local)
+        tiles_in = torch.from_numpy(t_in).cuda()
+        tiles_bd = torch.from_numpy(t_bd).cuda()
 
     def step(ev=None):
+        if overlap:
+            # interior tiles (no ghost face neighbour) run while the face halo is in flight
+            halo.start()
+            if ev is not None:
+                ev[0].record(stream)
+            H.assemble_tiles(ctx, dmesh, dpat, kappa, tensor, tiles_in, vals)
+            halo.finish()
+            H.assemble_tiles(ctx, dmesh, dpat, kappa, tensor, tiles_bd, vals)
+            if ev is not None:
+                ev[1].record(stream)
+            return
         if halo is not None:
             halo.exchange()
         if ev is not None:
@@ -191,7 +210,8 @@ def main():
             "config": {"workload": "spe10_swipdg_p1_kuhn_%dx%d_per_gpu" % (args.nx, args.ny),
                        "elements_per_gpu": n_own, "dofs_per_gpu": dofs_rank, "nnz_per_gpu": dpat.nnz,
                        "total_dofs": total_dofs, "components": qp1,
-                       "parallelism": "block-swipdg strips x%d, owner-computes, RCCL face halo" % world
+                       "parallelism": "block-swipdg strips x%d, owner-computes, RCCL face halo%s"
+                       % (world, " overlapped with interior tiles" if overlap else "")
                        if world > 1 else "single GPU"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

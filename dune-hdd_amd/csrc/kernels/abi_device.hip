@@ -43,9 +43,9 @@ extern "C" void hdd_ctx_destroy(hdd_ctx* ctx) { delete ctx; }
 
 static int fn_order(const hdd_scalar_fn& f) { return f.kind == HDD_FN_SINUSOID ? f.order : 0; }
 
-extern "C" int hdd_swipdg_assemble(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_fn* kappa, int32_t n_comp,
-                                   const hdd_tensor_fn* tensor, const hdd_swipdg_params* p, const hdd_csr* pattern,
-                                   double* const* d_vals, void* stream)
+static int assemble_impl(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_fn* kappa, int32_t n_comp,
+                         const hdd_tensor_fn* tensor, const hdd_swipdg_params* p, const hdd_csr* pattern,
+                         double* const* d_vals, const int32_t* d_tiles, int64_t n_tiles, void* stream)
 {
   using namespace hdd::dev;
   if (!ctx || !m || !kappa || !tensor || !p || !pattern || !d_vals)
@@ -88,6 +88,8 @@ extern "C" int hdd_swipdg_assemble(hdd_ctx* ctx, const hdd_mesh* m, const hdd_sc
   a.sigma_inner = p->sigma_inner;
   a.sigma_boundary = p->sigma_boundary;
   a.beta = p->beta;
+  a.tile_list = d_tiles;
+  a.n_tile_list = n_tiles;
   {
     const char* df = getenv("HDD_DEBUG_FLAGS");   // profiling ablations only
     a.debug_flags = df ? atoi(df) : 0;
@@ -121,6 +123,23 @@ extern "C" int hdd_swipdg_assemble(hdd_ctx* ctx, const hdd_mesh* m, const hdd_sc
                                               " / face order " + std::to_string(face_order));
   if (e != hipSuccess) return hip_fail(e, "hdd_swipdg_assemble: launch");
   return HDD_OK;
+}
+
+extern "C" int hdd_swipdg_assemble(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_fn* kappa, int32_t n_comp,
+                                   const hdd_tensor_fn* tensor, const hdd_swipdg_params* p, const hdd_csr* pattern,
+                                   double* const* d_vals, void* stream)
+{
+  return assemble_impl(ctx, m, kappa, n_comp, tensor, p, pattern, d_vals, nullptr, 0, stream);
+}
+
+extern "C" int hdd_swipdg_assemble_tiles(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_fn* kappa, int32_t n_comp,
+                                         const hdd_tensor_fn* tensor, const hdd_swipdg_params* p,
+                                         const hdd_csr* pattern, double* const* d_vals, const int32_t* d_tiles,
+                                         int64_t n_tiles, void* stream)
+{
+  if (!d_tiles && n_tiles) return set_error(HDD_ERR_INVALID, "hdd_swipdg_assemble_tiles: null tile list");
+  if (n_tiles == 0) return HDD_OK;
+  return assemble_impl(ctx, m, kappa, n_comp, tensor, p, pattern, d_vals, d_tiles, n_tiles, stream);
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -1094,13 +1094,17 @@ swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
   }
   if (t >= t_end) return;
   double* scratch = lds + IMG + 2;
-  auto elem_of = [&](int64_t tile) {
-    const int64_t t0 = a.own_begin + tile * 64;
+  // optional tile list (interior / halo-boundary split of a sharded assembly): position -> tile
+  auto tile_at = [&](int64_t pos) -> int64_t {
+    return a.tile_list ? int64_t(__builtin_amdgcn_readfirstlane(a.tile_list[pos])) : pos;
+  };
+  auto elem_of = [&](int64_t pos) {
+    const int64_t t0 = a.own_begin + tile_at(pos) * 64;
     const int64_t e0 = t0 + lane;
     return e0 < a.own_end ? e0 : t0;
   };
-  auto bounds = [&](int64_t tile, int64_t& base, int64_t& tile_end) {   // scalar loads (lgkmcnt)
-    const int64_t t0 = __builtin_amdgcn_readfirstlane(a.own_begin + tile * 64);
+  auto bounds = [&](int64_t pos, int64_t& base, int64_t& tile_end) {   // scalar loads (lgkmcnt)
+    const int64_t t0 = __builtin_amdgcn_readfirstlane(a.own_begin + tile_at(pos) * 64);
     const int64_t tend = t0 + 64 < a.own_end ? t0 + 64 : a.own_end;
     base = __builtin_amdgcn_readfirstlane(a.elem_ptr[t0 - a.own_begin]);
     tile_end = __builtin_amdgcn_readfirstlane(a.elem_ptr[tend - a.own_begin]);
@@ -1122,7 +1126,7 @@ swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
     int64_t base_n, tile_end_n;
     bounds(tn, base_n, tile_end_n);
 
-    const bool active = a.own_begin + t * 64 + lane < a.own_end;
+    const bool active = a.own_begin + tile_at(t) * 64 + lane < a.own_end;
     const int64_t base_al = base & ~int64_t(1);
     const int off = tile_offset<P::NB>(P::n_interior(own), active) + int(base - base_al);
     P::compute(a, e, own, gat, active ? lds + off : scratch);
@@ -1187,7 +1191,8 @@ static hipError_t launch_persistent(const AssembleArgs& a, hipStream_t s)
 {
   const int64_t n_own = a.own_end - a.own_begin;
   if (n_own <= 0) return hipSuccess;
-  const int64_t tiles = (n_own + 63) / 64;
+  const int64_t tiles = a.tile_list ? a.n_tile_list : (n_own + 63) / 64;
+  if (tiles <= 0) return hipSuccess;
   const size_t lds = (size_t(64) * P::RB + 2 + P::RB) * sizeof(double);
   int dev = 0, cus = 256;
   hipGetDevice(&dev);
@@ -1272,8 +1277,12 @@ hipError_t launch_assemble(const AssembleArgs& a, int nqv, int nqf, hipStream_t 
   *supported = true;
   if (!(a.debug_flags & 64)) {
     const hipError_t e = launch_components(a, nqv, nqf, s, supported);
-    if (*supported) return e;
+    if (*supported || a.tile_list) return e;
     *supported = true;   // fall through to the wave-per-row kernels for the remaining rules
+  }
+  if (a.tile_list) {
+    *supported = false;
+    return hipSuccess;
   }
   bool pwc = true;
   for (int c = 0; c < a.n_comp; ++c) pwc &= a.kappa[c].kind != HDD_FN_SINUSOID;

@@ -27,6 +27,8 @@ struct AssembleArgs {
   const double* tper;
   double sigma_inner, sigma_boundary, beta;
   int32_t debug_flags, pad2;   // ablation switches (HDD_DEBUG_FLAGS), 0 in production
+  const int32_t* tile_list;    // optional: 64-element tiles to assemble (relative to own_begin)
+  int64_t n_tile_list;         // entries of tile_list (tile_list == nullptr: all tiles)
   KappaArg kappa[HDD_MAX_COMP];
   double* vals[HDD_MAX_COMP];
 };

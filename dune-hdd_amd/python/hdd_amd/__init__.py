@@ -113,7 +113,11 @@ def lib():
         "hdd_pattern_fill": (_I32, [_I32, _I64, _I64, _I64, _VP, _VP, _VP, _VP, _VP]),
         "hdd_swipdg_assemble": (_I32, [_VP, C.POINTER(MeshT), C.POINTER(ScalarFn), _I32, C.POINTER(TensorFn),
                                        C.POINTER(Params), C.POINTER(CsrT), _VP, _VP]),
+        "hdd_swipdg_assemble_tiles": (_I32, [_VP, C.POINTER(MeshT), C.POINTER(ScalarFn), _I32, C.POINTER(TensorFn),
+                                             C.POINTER(Params), C.POINTER(CsrT), _VP, _VP, _I64, _VP]),
         "hdd_affine_lincomb": (_I32, [_VP, _I64, _VP, _I32, _VP, _I32, _VP, _I64, _VP]),
+        "hdd_block_operator_map": (_I32, [_VP, _I32, _I32, _VP, _VP, _VP, _VP, _VP, C.POINTER(_I64)]),
+        "hdd_gather_values": (_I32, [_VP, _VP, _VP, _I64, _VP, _VP]),
         "hdd_soa_gather": (_I32, [_VP, _VP, _VP, _I32, _I64, _VP, _I64, _VP, _VP]),
         "hdd_soa_scatter": (_I32, [_VP, _VP, _VP, _I32, _I64, _I64, _I64, _VP, _VP]),
     }
@@ -368,6 +372,33 @@ def assemble(ctx, dmesh, dpattern, kappas, tensor, prm=None, vals=None, stream=N
     _check(lib().hdd_swipdg_assemble(ctx.h, C.byref(dmesh.t), arr, n, C.byref(tensor), C.byref(prm),
                                      C.byref(dpattern.t), ptrs, C.c_void_p(s)), "hdd_swipdg_assemble")
     return vals
+
+
+def assemble_tiles(ctx, dmesh, dpattern, kappas, tensor, tiles, vals, prm=None, stream=None):
+    """hdd_swipdg_assemble_tiles: assemble only the 64-element tiles listed in `tiles` (device int32)."""
+    torch = _torch()
+    kappas = list(kappas)
+    n = len(kappas)
+    arr = (ScalarFn * n)(*kappas)
+    ptrs = (C.c_void_p * n)(*[v.data_ptr() for v in vals])
+    prm = prm or params()
+    s = stream if stream is not None else torch.cuda.current_stream(dmesh.coords.device).cuda_stream
+    _check(lib().hdd_swipdg_assemble_tiles(ctx.h, C.byref(dmesh.t), arr, n, C.byref(tensor), C.byref(prm),
+                                           C.byref(dpattern.t), ptrs, tiles.data_ptr(), tiles.numel(),
+                                           C.c_void_p(s)), "hdd_swipdg_assemble_tiles")
+    return vals
+
+
+def halo_tiles(local):
+    """(interior, boundary) 64-element tile indices of a rank-local mesh: boundary tiles hold an element
+    with a face neighbour in the ghost region (they need the halo)."""
+    nb = local.neighbors[:, local.own_begin:local.own_end]
+    ghost = ((nb >= 0) & ((nb < local.own_begin) | (nb >= local.own_end))).any(axis=0)
+    n_tiles = (local.n_own + 63) // 64
+    padded = np.zeros(n_tiles * 64, bool)
+    padded[:local.n_own] = ghost
+    bt = padded.reshape(n_tiles, 64).any(axis=1)
+    return np.nonzero(~bt)[0].astype(np.int32), np.nonzero(bt)[0].astype(np.int32)
 
 
 def affine_lincomb(ctx, comps, theta, out=None, stream=None):

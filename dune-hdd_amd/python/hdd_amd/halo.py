@@ -50,13 +50,15 @@ class HaloExchange:
     def unpack(self, p):
         soa_scatter(self.ctx, self.arrays, self.rows, self.ld, p["off"], p["n_recv"], p["rbuf"])
 
-    def exchange(self):
+    def start(self):
+        """Pack the send lists and post the RCCL send/recv.  Device work queued on the current stream after
+        this call (the interior tiles) overlaps the transfer; finish() orders the stream after it."""
         dist = self.dist
         for p in self.peers:
             if p["idx"].numel():
                 self.pack(p)
-        if self.host_staging:
-            ops = []
+        ops = []
+        if self.host_staging:      # gloo rehearsal: host-staged and synchronous, nothing to overlap
             for p in self.peers:
                 p["hs"].copy_(p["sbuf"])
             for p in self.peers:
@@ -66,17 +68,25 @@ class HaloExchange:
                 r.wait()
             for p in self.peers:
                 p["rbuf"].copy_(p["hr"])
-        else:
-            ops = []
-            for p in self.peers:
-                ops.append(dist.P2POp(dist.isend, p["sbuf"], p["peer"]))
-                ops.append(dist.P2POp(dist.irecv, p["rbuf"], p["peer"]))
-            if ops:
-                for r in dist.batch_isend_irecv(ops):
-                    r.wait()
+            self.pending = []
+            return
+        for p in self.peers:
+            ops.append(dist.P2POp(dist.isend, p["sbuf"], p["peer"]))
+            ops.append(dist.P2POp(dist.irecv, p["rbuf"], p["peer"]))
+        self.pending = dist.batch_isend_irecv(ops) if ops else []
+
+    def finish(self):
+        """Make the current stream wait for the transfer (no host block for RCCL) and unpack the ghosts."""
+        for r in self.pending:
+            r.wait()
+        self.pending = []
         for p in self.peers:
             if p["n_recv"]:
                 self.unpack(p)
+
+    def exchange(self):
+        self.start()
+        self.finish()
 
 
 def strip_owner(n_sub, world):

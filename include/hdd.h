@@ -195,6 +195,14 @@ int hdd_swipdg_assemble(hdd_ctx* ctx, const hdd_mesh* mesh, const hdd_scalar_fn*
                         const hdd_tensor_fn* tensor, const hdd_swipdg_params* params, const hdd_csr* pattern,
                         double* const* d_vals, void* stream);
 
+/* Same, restricted to the 64-element tiles d_tiles[0..n_tiles) (tile t = owned elements
+ * [own_begin + 64t, own_begin + 64t + 64)): lets a sharded assembly run its interior tiles while the face
+ * halo is in flight and the halo-dependent tiles afterwards.  Only the thread-per-element kernels
+ * (P1 / Q1 with the reference integrand orders) take tile lists; others return HDD_ERR_UNSUPPORTED. */
+int hdd_swipdg_assemble_tiles(hdd_ctx* ctx, const hdd_mesh* mesh, const hdd_scalar_fn* kappa, int32_t n_comp,
+                              const hdd_tensor_fn* tensor, const hdd_swipdg_params* params, const hdd_csr* pattern,
+                              double* const* d_vals, const int32_t* d_tiles, int64_t n_tiles, void* stream);
+
 /* theta-lincomb of affine components on a shared pattern -- replaces
  * AffinelyDecomposedContainer::freeze_parameter(mu) as used by ContainerBasedDefault::uncached_solve
  * (base.hh:338-341, 357-361):  out[s][k] = sum_q theta[s*n_comp+q] * d_vals[q][k]  (theta on host) */

@@ -171,6 +171,34 @@ def test_rank_local_rows_equal_global_slice(ctx):
         assert np.allclose(val, gval[lo:hi], rtol=0, atol=1e-13 * np.max(np.abs(gval)))
 
 
+@pytest.mark.parametrize("et,smooth", [(H.SIMPLEX, False), (H.SIMPLEX, True), (H.CUBE, False), (H.CUBE, True)])
+def test_tile_split_overlap(ctx, et, smooth):
+    """hdd_swipdg_assemble_tiles: interior tiles assembled while the ghost records are garbage (NaN), then
+    the halo-boundary tiles after the ghosts are restored, reproduce the one-shot assembly bit for bit."""
+    torch = _torch()
+    grid = H.Grid.structured(et, 1024, 4, (0, 0), (4, 1), px=4, py=1)
+    local = grid.local(1, 3)
+    dm = H.DeviceMesh(local)
+    dp = H.DevicePattern(local)
+    kcell = torch.from_numpy(local.checkerboard((0, 0), (4, 1), 100, 20, O.spe10_synthetic_permeability())).cuda()
+    kap = [H.scalar_fn(H.FN_SINUSOID if smooth else H.FN_CONST, 1.0, b=0.5, kx=3.0, ky=2.0, order=3)
+           if smooth else H.scalar_fn(H.FN_CONST, 1.0)]
+    ten = H.tensor_fn(H.TENSOR_ISO_PER_ELEM, per_elem=kcell)
+    (ref,) = H.assemble(ctx, dm, dp, kap, ten)
+    t_in, t_bd = H.halo_tiles(local)
+    assert len(t_in) and len(t_bd)
+    val = torch.full_like(ref, float("nan"))
+    saved = dm.coords.clone()
+    ghosts = torch.ones(local.n_local, dtype=torch.bool, device="cuda")
+    ghosts[local.own_begin:local.own_end] = False
+    dm.coords[:, ghosts] = float("nan")
+    H.assemble_tiles(ctx, dm, dp, kap, ten, torch.from_numpy(t_in).cuda(), [val])
+    dm.coords.copy_(saved)
+    H.assemble_tiles(ctx, dm, dp, kap, ten, torch.from_numpy(t_bd).cuda(), [val])
+    torch.cuda.synchronize()
+    assert torch.equal(val, ref)
+
+
 def test_golden_fixtures(ctx):
     """Committed golden CSR fixtures (generated by tests/golden/make_golden.py with the pinned oracle)."""
     import glob

@@ -57,9 +57,8 @@ def test_cpp_surface_against_oracle():
     L.sort_indices()
     assert np.array_equal(lrp, L.indptr) and np.array_equal(lcol, L.indices)
     assert np.max(np.abs(lval - L.data)) <= 1e-12 * np.max(np.abs(L.data))
-    Cm = A[a0 * 3:b0 * 3, an * 3:bn * 3].tocsr()
-    Cm.eliminate_zeros()
-    Cm.sort_indices()
+    Cm = A[a0 * 3:b0 * 3, an * 3:bn * 3].tocsr()    # keeps the pattern's explicit zeros: the coupling
+    Cm.sort_indices()                                # pattern is the full element-block face coupling
     assert np.array_equal(crp, Cm.indptr) and np.array_equal(ccol, Cm.indices)
     assert np.max(np.abs(cval - Cm.data)) <= 1e-12 * np.max(np.abs(val))
     assert sorted(nbs.tolist()) == [1, 2]      # 2x2 partition: subdomain 0's face neighbours
