@@ -40,12 +40,12 @@ static inline double linspace_node(double a, double b, int64_t n, int64_t i)
 
 struct Grid {
   virtual ~Grid() = default;
-  int elem_type = HDD_SIMPLEX, nvpe = 3, nf = 3, nb = 3;
+  int elem_type = HDD_SIMPLEX, nvpe = 3, nf = 3, nb = 3, dim = 2;
   int64_t ne = 0, nv = 0;
   int32_t n_sub = 1;
   std::vector<int64_t> sub_first;   // [n_sub+1] element ranges of the subdomains
   virtual void vertices(int64_t g, int64_t* v) const = 0;
-  virtual void vertex_coord(int64_t v, double* xy) const = 0;
+  virtual void vertex_coord(int64_t v, double* xy) const = 0;   // dim values
   virtual int64_t neighbor(int64_t g, int f) const = 0;      // >= 0 element, else HDD_NBR_*
   virtual uint32_t face_info(int64_t g) const = 0;
   int32_t subdomain(int64_t g) const
@@ -172,6 +172,104 @@ struct StructuredGrid final : Grid {
 };
 
 // ------------------------------------------------------------------------------------------------
+// structured nx x ny x nz axis-aligned hexahedra (3d), px x py x pz subdomains, implicit formulas
+// ------------------------------------------------------------------------------------------------
+struct StructuredGrid3 final : Grid {
+  hdd_structured3_desc d{};
+  int64_t n[3] = {1, 1, 1}, p[3] = {1, 1, 1};
+  std::vector<int64_t> cut[3];         // first layer of each subdomain slab per axis [p+1]
+  std::vector<int64_t> blk_first;      // first element of each subdomain [n_sub+1]
+  int32_t bcode = HDD_NBR_DIRICHLET;
+
+  explicit StructuredGrid3(const hdd_structured3_desc& desc) : d(desc)
+  {
+    elem_type = HDD_HEX;
+    dim = 3;
+    nvpe = 8;
+    nf = 6;
+    nb = (d.degree + 1) * (d.degree + 1) * (d.degree + 1);
+    n[0] = d.nx; n[1] = d.ny; n[2] = d.nz;
+    p[0] = d.px; p[1] = d.py; p[2] = d.pz;
+    nv = (n[0] + 1) * (n[1] + 1) * (n[2] + 1);
+    ne = n[0] * n[1] * n[2];
+    bcode = d.boundary == HDD_BOUNDARY_ALL_NEUMANN ? HDD_NBR_NEUMANN : HDD_NBR_DIRICHLET;
+    for (int a = 0; a < 3; ++a) {
+      cut[a].resize(p[a] + 1);
+      for (int64_t s = 0; s <= p[a]; ++s) cut[a][s] = (s * n[a] + p[a] - 1) / p[a];
+    }
+    n_sub = int32_t(p[0] * p[1] * p[2]);
+    blk_first.assign(n_sub + 1, 0);
+    for (int64_t sx = 0; sx < p[0]; ++sx)
+      for (int64_t sy = 0; sy < p[1]; ++sy)
+        for (int64_t sz = 0; sz < p[2]; ++sz) {
+          const int64_t s = (sx * p[1] + sy) * p[2] + sz;
+          blk_first[s + 1] = (cut[0][sx + 1] - cut[0][sx]) * (cut[1][sy + 1] - cut[1][sy]) * (cut[2][sz + 1] - cut[2][sz]);
+        }
+    for (int s = 0; s < n_sub; ++s) blk_first[s + 1] += blk_first[s];
+    sub_first = blk_first;
+  }
+
+  int64_t elem_id(const int64_t* c) const
+  {
+    int64_t sc[3], w[3];
+    for (int a = 0; a < 3; ++a) {
+      sc[a] = (c[a] * p[a]) / n[a];
+      w[a] = cut[a][sc[a] + 1] - cut[a][sc[a]];
+    }
+    const int64_t s = (sc[0] * p[1] + sc[1]) * p[2] + sc[2];
+    const int64_t l0 = c[0] - cut[0][sc[0]], l1 = c[1] - cut[1][sc[1]], l2 = c[2] - cut[2][sc[2]];
+    return blk_first[s] + l0 + w[0] * (l1 + w[1] * l2);
+  }
+
+  void cell_of(int64_t g, int64_t* c) const
+  {
+    const int64_t s = int64_t(std::upper_bound(blk_first.begin(), blk_first.end(), g) - blk_first.begin()) - 1;
+    const int64_t sz = s % p[2], sy = (s / p[2]) % p[1], sx = s / (p[1] * p[2]);
+    const int64_t sc[3] = {sx, sy, sz};
+    int64_t w[3];
+    for (int a = 0; a < 3; ++a) w[a] = cut[a][sc[a] + 1] - cut[a][sc[a]];
+    int64_t loc = g - blk_first[s];
+    for (int a = 0; a < 3; ++a) {
+      c[a] = cut[a][sc[a]] + loc % w[a];
+      loc /= w[a];
+    }
+  }
+
+  void vertices(int64_t g, int64_t* v) const override
+  {
+    int64_t c[3];
+    cell_of(g, c);
+    for (int k = 0; k < 8; ++k)   // Dune cube vertex k = (k&1, (k>>1)&1, k>>2)
+      v[k] = (c[0] + (k & 1)) + (n[0] + 1) * ((c[1] + ((k >> 1) & 1)) + (n[1] + 1) * (c[2] + (k >> 2)));
+  }
+
+  void vertex_coord(int64_t v, double* xyz) const override
+  {
+    const int64_t i = v % (n[0] + 1), j = (v / (n[0] + 1)) % (n[1] + 1), k = v / ((n[0] + 1) * (n[1] + 1));
+    xyz[0] = linspace_node(d.lower[0], d.upper[0], n[0], i);
+    xyz[1] = linspace_node(d.lower[1], d.upper[1], n[1], j);
+    xyz[2] = linspace_node(d.lower[2], d.upper[2], n[2], k);
+  }
+
+  int64_t neighbor(int64_t g, int f) const override
+  {
+    int64_t c[3];
+    cell_of(g, c);
+    const int a = f / 2;
+    c[a] += (f & 1) ? 1 : -1;
+    if (c[a] < 0 || c[a] >= n[a]) return bcode;
+    return elem_id(c);
+  }
+
+  uint32_t face_info(int64_t) const override
+  {
+    uint32_t fi = 0;   // twin of face f is f^1, never reversed (aligned structured faces)
+    for (uint32_t f = 0; f < 6; ++f) fi |= (f ^ 1u) << (4 * f);
+    return fi;
+  }
+};
+
+// ------------------------------------------------------------------------------------------------
 // general conforming mesh from connectivity
 // ------------------------------------------------------------------------------------------------
 struct ExplicitGrid final : Grid {
@@ -247,6 +345,27 @@ extern "C" int hdd_grid_create_structured(const hdd_structured_desc* desc, hdd_g
     return set_error(HDD_ERR_RANGE, "hdd_grid_create_structured: too many elements for int32 DoF columns");
   auto* g = new hdd_grid;
   g->impl.reset(new StructuredGrid(*desc));
+  *out = g;
+  return HDD_OK;
+}
+
+extern "C" int hdd_grid_create_structured_3d(const hdd_structured3_desc* desc, hdd_grid** out)
+{
+  if (!desc || !out) return set_error(HDD_ERR_INVALID, "hdd_grid_create_structured_3d: null argument");
+  if (desc->nx < 1 || desc->ny < 1 || desc->nz < 1 || desc->px < 1 || desc->py < 1 || desc->pz < 1 ||
+      desc->px > desc->nx || desc->py > desc->ny || desc->pz > desc->nz)
+    return set_error(HDD_ERR_INVALID, "hdd_grid_create_structured_3d: need 1 <= p_a <= n_a");
+  if (desc->degree < 1 || desc->degree > 3)
+    return set_error(HDD_ERR_UNSUPPORTED, "hdd_grid_create_structured_3d: degree must be 1, 2 or 3");
+  for (int a = 0; a < 3; ++a)
+    if (!(desc->upper[a] > desc->lower[a]))
+      return set_error(HDD_ERR_INVALID, "hdd_grid_create_structured_3d: empty domain");
+  const int64_t nb = int64_t(desc->degree + 1) * (desc->degree + 1) * (desc->degree + 1);
+  const int64_t ne = int64_t(desc->nx) * desc->ny * desc->nz;
+  if (ne * nb > int64_t(INT32_MAX))
+    return set_error(HDD_ERR_RANGE, "hdd_grid_create_structured_3d: too many DoFs for int32 columns");
+  auto* g = new hdd_grid;
+  g->impl.reset(new StructuredGrid3(*desc));
   *out = g;
   return HDD_OK;
 }
@@ -342,7 +461,7 @@ extern "C" int hdd_grid_get_info(const hdd_grid* g, hdd_grid_info* out)
   out->n_elements = G.ne;
   out->n_vertices = G.nv;
   out->n_subdomains = G.n_sub;
-  out->pad = 0;
+  out->dim = G.dim;
   return HDD_OK;
 }
 
@@ -363,8 +482,8 @@ extern "C" int hdd_grid_connectivity(const hdd_grid* g, double* vertex_coords, i
   if (!g) return set_error(HDD_ERR_INVALID, "hdd_grid_connectivity: null grid");
   const Grid& G = *g->impl;
   if (vertex_coords)
-    for (int64_t v = 0; v < G.nv; ++v) G.vertex_coord(v, vertex_coords + 2 * v);
-  int64_t vv[4];
+    for (int64_t v = 0; v < G.nv; ++v) G.vertex_coord(v, vertex_coords + G.dim * v);
+  int64_t vv[8];
   for (int64_t e = 0; e < G.ne; ++e) {
     if (elem_vert) {
       G.vertices(e, vv);
@@ -424,8 +543,9 @@ extern "C" int hdd_local_fill(const hdd_local* l, double* coords, int32_t* neigh
   const Local& L = l->impl;
   const Grid& G = *L.g;
   const int64_t nl = L.n_local();
-  int64_t vv[4];
-  double xy[2];
+  const int dim = G.dim;
+  int64_t vv[8];
+  double xy[3];
   for (int64_t e = 0; e < nl; ++e) {
     const int64_t gid = L.global_of(e);
     const bool owned = e >= L.own_begin() && e < L.own_end();
@@ -433,8 +553,7 @@ extern "C" int hdd_local_fill(const hdd_local* l, double* coords, int32_t* neigh
       G.vertices(gid, vv);
       for (int k = 0; k < G.nvpe; ++k) {
         G.vertex_coord(vv[k], xy);
-        coords[(2 * k) * nl + e] = xy[0];
-        coords[(2 * k + 1) * nl + e] = xy[1];
+        for (int c = 0; c < dim; ++c) coords[(dim * k + c) * nl + e] = xy[c];
       }
     }
     if (neighbors)
@@ -460,18 +579,16 @@ extern "C" int hdd_local_centers(const hdd_local* l, double* centers)
   const Local& L = l->impl;
   const Grid& G = *L.g;
   const int64_t nl = L.n_local();
-  int64_t vv[4];
-  double xy[2];
+  int64_t vv[8];
+  double xy[3];
   for (int64_t e = 0; e < nl; ++e) {
     G.vertices(L.global_of(e), vv);
-    double sx = 0.0, sy = 0.0;
+    double sum[3] = {0.0, 0.0, 0.0};
     for (int k = 0; k < G.nvpe; ++k) {
       G.vertex_coord(vv[k], xy);
-      sx += xy[0];
-      sy += xy[1];
+      for (int c = 0; c < G.dim; ++c) sum[c] += xy[c];
     }
-    centers[e] = sx / G.nvpe;
-    centers[nl + e] = sy / G.nvpe;
+    for (int c = 0; c < G.dim; ++c) centers[c * nl + e] = sum[c] / G.nvpe;
   }
   return HDD_OK;
 }
@@ -584,14 +701,12 @@ extern "C" int hdd_checkerboard(int64_t n, const double* centers, const double l
 // ------------------------------------------------------------------------------------------------
 static int nb_of(int32_t et) { return et == HDD_SIMPLEX ? 3 : (et == HDD_CUBE ? 4 : 0); }
 
-extern "C" int hdd_pattern_count(int32_t elem_type, int64_t n_local, int64_t own_begin, int64_t own_end,
-                                 const int32_t* neighbors, int64_t* nnz)
+extern "C" int hdd_dg_pattern_count(int32_t nf, int32_t nb, int64_t n_local, int64_t own_begin, int64_t own_end,
+                                    const int32_t* neighbors, int64_t* nnz)
 {
-  const int nb = nb_of(elem_type);
-  if (!nb) return set_error(HDD_ERR_UNSUPPORTED, "hdd_pattern_count: unknown element type");
+  if (nf < 1 || nf > 6 || nb < 1) return set_error(HDD_ERR_INVALID, "hdd_dg_pattern_count: need 1 <= n_faces <= 6, nb >= 1");
   if (!neighbors || !nnz || own_begin < 0 || own_end > n_local || own_begin > own_end)
-    return set_error(HDD_ERR_INVALID, "hdd_pattern_count: invalid argument");
-  const int nf = nb;
+    return set_error(HDD_ERR_INVALID, "hdd_dg_pattern_count: invalid argument");
   int64_t total = 0;
   for (int64_t e = own_begin; e < own_end; ++e) {
     int blocks = 1;
@@ -602,26 +717,24 @@ extern "C" int hdd_pattern_count(int32_t elem_type, int64_t n_local, int64_t own
   return HDD_OK;
 }
 
-extern "C" int hdd_pattern_fill(int32_t elem_type, int64_t n_local, int64_t own_begin, int64_t own_end,
-                                const int32_t* neighbors, const int64_t* global_id, int64_t* row_ptr, int32_t* col,
-                                int64_t* elem_ptr)
+extern "C" int hdd_dg_pattern_fill(int32_t nf, int32_t nb, int64_t n_local, int64_t own_begin, int64_t own_end,
+                                   const int32_t* neighbors, const int64_t* global_id, int64_t* row_ptr,
+                                   int32_t* col, int64_t* elem_ptr)
 {
-  const int nb = nb_of(elem_type);
-  if (!nb) return set_error(HDD_ERR_UNSUPPORTED, "hdd_pattern_fill: unknown element type");
+  if (nf < 1 || nf > 6 || nb < 1) return set_error(HDD_ERR_INVALID, "hdd_dg_pattern_fill: need 1 <= n_faces <= 6, nb >= 1");
   if (!neighbors || !row_ptr || !col || own_begin < 0 || own_end > n_local || own_begin > own_end)
-    return set_error(HDD_ERR_INVALID, "hdd_pattern_fill: invalid argument");
-  const int nf = nb;
+    return set_error(HDD_ERR_INVALID, "hdd_dg_pattern_fill: invalid argument");
   int64_t off = 0;
   row_ptr[0] = 0;
   for (int64_t e = own_begin; e < own_end; ++e) {
     const int64_t k = e - own_begin;
-    int64_t blk[5];
+    int64_t blk[7];
     int nblk = 0;
     blk[nblk++] = global_id ? global_id[e] : e;
     for (int f = 0; f < nf; ++f) {
       const int32_t n = neighbors[f * n_local + e];
       if (n >= 0) {
-        if (n >= n_local) return set_error(HDD_ERR_RANGE, "hdd_pattern_fill: neighbour out of range");
+        if (n >= n_local) return set_error(HDD_ERR_RANGE, "hdd_dg_pattern_fill: neighbour out of range");
         blk[nblk++] = global_id ? global_id[n] : n;
       }
     }
@@ -635,6 +748,23 @@ extern "C" int hdd_pattern_fill(int32_t elem_type, int64_t n_local, int64_t own_
   }
   if (elem_ptr) elem_ptr[own_end - own_begin] = off;
   return HDD_OK;
+}
+
+extern "C" int hdd_pattern_count(int32_t elem_type, int64_t n_local, int64_t own_begin, int64_t own_end,
+                                 const int32_t* neighbors, int64_t* nnz)
+{
+  const int nb = nb_of(elem_type);
+  if (!nb) return set_error(HDD_ERR_UNSUPPORTED, "hdd_pattern_count: 2d element type expected (use hdd_dg_pattern_count)");
+  return hdd_dg_pattern_count(nb, nb, n_local, own_begin, own_end, neighbors, nnz);
+}
+
+extern "C" int hdd_pattern_fill(int32_t elem_type, int64_t n_local, int64_t own_begin, int64_t own_end,
+                                const int32_t* neighbors, const int64_t* global_id, int64_t* row_ptr, int32_t* col,
+                                int64_t* elem_ptr)
+{
+  const int nb = nb_of(elem_type);
+  if (!nb) return set_error(HDD_ERR_UNSUPPORTED, "hdd_pattern_fill: 2d element type expected (use hdd_dg_pattern_fill)");
+  return hdd_dg_pattern_fill(nb, nb, n_local, own_begin, own_end, neighbors, global_id, row_ptr, col, elem_ptr);
 }
 
 // ------------------------------------------------------------------------------------------------

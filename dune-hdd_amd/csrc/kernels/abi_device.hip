@@ -5,6 +5,10 @@
 // around the RCCL face-halo exchange of a sharded BlockSWIPDG.
 #include <hip/hip_runtime.h>
 
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cmath>
 #include <cstdint>
 #include <cstdlib>
 #include <string>
@@ -43,6 +47,124 @@ extern "C" void hdd_ctx_destroy(hdd_ctx* ctx) { delete ctx; }
 
 static int fn_order(const hdd_scalar_fn& f) { return f.kind == HDD_FN_SINUSOID ? f.order : 0; }
 
+// ---------------------------------------------------------------------------------------------------
+// HDD_HEX: Q_p on affine hexahedra (hex_qp.hip)
+// ---------------------------------------------------------------------------------------------------
+static void gauss_legendre01(int n, double* x, double* w)   // Newton on P_n, mapped to [0,1]
+{
+  for (int i = 0; i < n; ++i) {
+    double z = std::cos(M_PI * (i + 0.75) / (n + 0.5)), dp = 1.0;
+    for (int it = 0; it < 100; ++it) {
+      double p0 = 1.0, p1 = z;
+      for (int k = 2; k <= n; ++k) {
+        const double p2 = ((2.0 * k - 1.0) * z * p1 - (k - 1.0) * p0) / k;
+        p0 = p1;
+        p1 = p2;
+      }
+      if (n == 1) { p0 = 1.0; p1 = z; }
+      dp = n * (z * p1 - p0) / (z * z - 1.0);
+      const double dz = p1 / dp;
+      z -= dz;
+      if (std::fabs(dz) < 1e-16) {
+        double q0 = 1.0, q1 = z;
+        for (int k = 2; k <= n; ++k) {
+          const double q2 = ((2.0 * k - 1.0) * z * q1 - (k - 1.0) * q0) / k;
+          q0 = q1;
+          q1 = q2;
+        }
+        if (n == 1) { q0 = 1.0; q1 = z; }
+        dp = n * (z * q1 - q0) / (z * z - 1.0);
+        break;
+      }
+    }
+    x[n - 1 - i] = 0.5 * (z + 1.0);
+    w[n - 1 - i] = 1.0 / ((1.0 - z * z) * dp * dp);
+  }
+}
+
+// equidistant Lagrange polynomial k of degree p and its derivative at x
+static void lagrange_1d(int p, int k, double x, double* v, double* d)
+{
+  double val = 1.0, der = 0.0;
+  for (int m = 0; m <= p; ++m) {
+    if (m == k) continue;
+    const double den = double(k - m) / p, f = (x - double(m) / p) / den;
+    der = der * f + val / den;
+    val *= f;
+  }
+  *v = val;
+  *d = der;
+}
+
+static int assemble_hex(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_fn* kappa, int32_t n_comp,
+                        const hdd_tensor_fn* tensor, const hdd_swipdg_params* p, const hdd_csr* pattern,
+                        double* const* d_vals, void* stream)
+{
+  using namespace hdd::dev;
+  const int deg = m->degree < 1 ? 1 : m->degree;
+  if (deg > 3) return set_error(HDD_ERR_UNSUPPORTED, "hdd_swipdg_assemble: HDD_HEX supports p = 1..3");
+  const int nb = (deg + 1) * (deg + 1) * (deg + 1);
+  if (pattern->n_rows != int64_t(nb) * (m->own_end - m->own_begin))
+    return set_error(HDD_ERR_INVALID, "hdd_swipdg_assemble: pattern rows != nb * owned elements");
+  if (tensor->kind != HDD_TENSOR_CONST && tensor->kind != HDD_TENSOR_ISO_PER_ELEM &&
+      tensor->kind != HDD_TENSOR_SYM_PER_ELEM)
+    return set_error(HDD_ERR_UNSUPPORTED, "hdd_swipdg_assemble: unknown tensor kind");
+  if (tensor->kind != HDD_TENSOR_CONST && !tensor->per_elem)
+    return set_error(HDD_ERR_INVALID, "hdd_swipdg_assemble: tensor per_elem missing");
+  hipError_t e = hipSetDevice(ctx->device);
+  if (e != hipSuccess) return hip_fail(e, "hdd_swipdg_assemble: hipSetDevice");
+  for (int c = 0; c < n_comp; ++c) {
+    const hdd_scalar_fn& k = kappa[c];
+    if (k.kind != HDD_FN_CONST && k.kind != HDD_FN_PER_ELEM && k.kind != HDD_FN_SINUSOID)
+      return set_error(HDD_ERR_UNSUPPORTED, "hdd_swipdg_assemble: unknown diffusion factor kind");
+    if (k.kind == HDD_FN_PER_ELEM && !k.per_elem)
+      return set_error(HDD_ERR_INVALID, "hdd_swipdg_assemble: diffusion factor per_elem missing");
+    if (!d_vals[c]) return set_error(HDD_ERR_INVALID, "hdd_swipdg_assemble: null value array");
+    // integrand orders (dune-gdt): volume ord(kappa) + ord(A) + 2 (p-1), faces ord(kappa) + ord(A) + 2p
+    const int ko = fn_order(k);
+    const int vol_order = p->vol_order >= 0 ? p->vol_order : ko + 2 * (deg - 1);
+    const int face_order = p->face_order >= 0 ? p->face_order : ko + 2 * deg;
+    const int nq1v = std::max(1, (vol_order + 2) / 2), nq1f = std::max(1, (face_order + 2) / 2);
+    if (nq1v > 8 || nq1f > 8)
+      return set_error(HDD_ERR_UNSUPPORTED, "hdd_swipdg_assemble: quadrature order too high for HDD_HEX");
+    HexArgs a{};
+    a.n_local = m->n_local;
+    a.own_begin = m->own_begin;
+    a.own_end = m->own_end;
+    a.coords = m->coords;
+    a.nbrs = m->neighbors;
+    a.elem_ptr = pattern->elem_ptr;
+    a.tkind = tensor->kind;
+    for (int r = 0; r < 6; ++r) a.tc[r] = tensor->c[r];
+    a.tper = tensor->per_elem;
+    a.kkind = k.kind;
+    a.kc = k.c;
+    a.kb = k.b;
+    a.kx = k.kx;
+    a.ky = k.ky;
+    a.kper = k.per_elem;
+    a.vals = d_vals[c];
+    a.sigma_inner = p->sigma_inner;
+    a.sigma_boundary = p->sigma_boundary;
+    a.beta = p->beta;
+    gauss_legendre01(nq1v, a.tab.sv, a.tab.wv);
+    gauss_legendre01(nq1f, a.tab.sf, a.tab.wf);
+    for (int r = 0; r <= deg; ++r) {
+      for (int q = 0; q < nq1v; ++q) lagrange_1d(deg, r, a.tab.sv[q], &a.tab.Lv[r][q], &a.tab.Dv[r][q]);
+      for (int q = 0; q < nq1f; ++q) lagrange_1d(deg, r, a.tab.sf[q], &a.tab.Lf[r][q], &a.tab.Df[r][q]);
+      for (int q = 0; q < 2; ++q) lagrange_1d(deg, r, double(q), &a.tab.Le[r][q], &a.tab.De[r][q]);
+    }
+    bool supported = false;
+    e = launch_hex(a, deg, nq1v, nq1f, static_cast<hipStream_t>(stream), &supported);
+    if (!supported)
+      return set_error(HDD_ERR_UNSUPPORTED, "hdd_swipdg_assemble: no HDD_HEX kernel for p=" + std::to_string(deg) +
+                                                ", volume order " + std::to_string(vol_order) + ", face order " +
+                                                std::to_string(face_order));
+    if (e != hipSuccess) return hip_fail(e, "hdd_swipdg_assemble: launch");
+  }
+  return HDD_OK;
+}
+
 static int assemble_impl(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_fn* kappa, int32_t n_comp,
                          const hdd_tensor_fn* tensor, const hdd_swipdg_params* p, const hdd_csr* pattern,
                          double* const* d_vals, const int32_t* d_tiles, int64_t n_tiles, void* stream)
@@ -52,7 +174,7 @@ static int assemble_impl(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_fn* k
     return set_error(HDD_ERR_INVALID, "hdd_swipdg_assemble: null argument");
   if (n_comp < 1 || n_comp > HDD_MAX_COMP)
     return set_error(HDD_ERR_INVALID, "hdd_swipdg_assemble: need 1 <= n_comp <= HDD_MAX_COMP");
-  if (m->elem_type != HDD_SIMPLEX && m->elem_type != HDD_CUBE)
+  if (m->elem_type != HDD_SIMPLEX && m->elem_type != HDD_CUBE && m->elem_type != HDD_HEX)
     return set_error(HDD_ERR_UNSUPPORTED, "hdd_swipdg_assemble: unknown element type");
   if (!m->coords || !m->neighbors || !m->face_info || !pattern->elem_ptr)
     return set_error(HDD_ERR_INVALID, "hdd_swipdg_assemble: mesh / pattern arrays missing");
@@ -60,6 +182,12 @@ static int assemble_impl(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_fn* k
     return set_error(HDD_ERR_RANGE, "hdd_swipdg_assemble: 0 <= own_begin <= own_end <= n_local violated");
   if (m->n_local >= int64_t(INT32_MAX))
     return set_error(HDD_ERR_RANGE, "hdd_swipdg_assemble: n_local must fit int32 neighbour ids");
+  if (m->elem_type == HDD_HEX) {
+    if (d_tiles) return set_error(HDD_ERR_UNSUPPORTED, "hdd_swipdg_assemble_tiles: no tile lists for HDD_HEX");
+    return assemble_hex(ctx, m, kappa, n_comp, tensor, p, pattern, d_vals, stream);
+  }
+  if (m->degree > 1)
+    return set_error(HDD_ERR_UNSUPPORTED, "hdd_swipdg_assemble: 2d meshes carry P1 / Q1 only (degree <= 1)");
   const int nb = m->elem_type == HDD_SIMPLEX ? 3 : 4;
   if (pattern->n_rows != int64_t(nb) * (m->own_end - m->own_begin))
     return set_error(HDD_ERR_INVALID, "hdd_swipdg_assemble: pattern rows != nb * owned elements");
@@ -340,4 +468,64 @@ extern "C" int hdd_gather_values(hdd_ctx* ctx, const double* d_vals, const int64
                      d_out);
   e = hipGetLastError();
   return e == hipSuccess ? HDD_OK : hip_fail(e, "hdd_gather_values: launch");
+}
+
+// ------------------------------------------------------------------------------------------------
+// device pattern build (EllipticSWIPDG::pattern, swipdg.hh:169)
+// ------------------------------------------------------------------------------------------------
+static int mesh_faces(const hdd_mesh* m)
+{
+  return m->elem_type == HDD_SIMPLEX ? 3 : (m->elem_type == HDD_CUBE ? 4 : (m->elem_type == HDD_HEX ? 6 : 0));
+}
+
+extern "C" int hdd_pattern_elem_ptr_device(hdd_ctx* ctx, const hdd_mesh* m, int32_t nb, int64_t* d_elem_ptr,
+                                           int64_t* nnz, void* stream)
+{
+  if (!ctx || !m || !d_elem_ptr || !nnz || nb < 1 || !m->neighbors)
+    return set_error(HDD_ERR_INVALID, "hdd_pattern_elem_ptr_device: invalid argument");
+  const int nf = mesh_faces(m);
+  if (!nf) return set_error(HDD_ERR_UNSUPPORTED, "hdd_pattern_elem_ptr_device: unknown element type");
+  if (m->own_begin < 0 || m->own_end > m->n_local || m->own_begin > m->own_end)
+    return set_error(HDD_ERR_RANGE, "hdd_pattern_elem_ptr_device: 0 <= own_begin <= own_end <= n_local violated");
+  hipError_t e = hipSetDevice(ctx->device);
+  if (e != hipSuccess) return hip_fail(e, "hdd_pattern_elem_ptr_device: hipSetDevice");
+  const hipStream_t s = static_cast<hipStream_t>(stream);
+  const int64_t n_own = m->own_end - m->own_begin;
+  e = hipMemsetAsync(d_elem_ptr, 0, sizeof(int64_t), s);
+  if (e != hipSuccess) return hip_fail(e, "hdd_pattern_elem_ptr_device: memset");
+  if (n_own > 0) {
+    e = hdd::dev::launch_pattern_counts(m->neighbors, nf, m->n_local, m->own_begin, m->own_end, int64_t(nb) * nb,
+                                        d_elem_ptr + 1, s);
+    if (e != hipSuccess) return hip_fail(e, "hdd_pattern_elem_ptr_device: counts");
+    size_t tmp_bytes = 0;
+    e = hipcub::DeviceScan::InclusiveSum(nullptr, tmp_bytes, d_elem_ptr + 1, d_elem_ptr + 1, n_own, s);
+    if (e != hipSuccess) return hip_fail(e, "hdd_pattern_elem_ptr_device: scan size");
+    void* tmp = nullptr;
+    e = hipMalloc(&tmp, tmp_bytes);
+    if (e != hipSuccess) return hip_fail(e, "hdd_pattern_elem_ptr_device: scan scratch");
+    e = hipcub::DeviceScan::InclusiveSum(tmp, tmp_bytes, d_elem_ptr + 1, d_elem_ptr + 1, n_own, s);
+    const hipError_t e2 = hipStreamSynchronize(s);
+    (void)hipFree(tmp);
+    if (e != hipSuccess) return hip_fail(e, "hdd_pattern_elem_ptr_device: scan");
+    if (e2 != hipSuccess) return hip_fail(e2, "hdd_pattern_elem_ptr_device: synchronize");
+  }
+  e = hipMemcpy(nnz, d_elem_ptr + n_own, sizeof(int64_t), hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return hip_fail(e, "hdd_pattern_elem_ptr_device: read nnz");
+  return HDD_OK;
+}
+
+extern "C" int hdd_pattern_fill_device(hdd_ctx* ctx, const hdd_mesh* m, int32_t nb, const int64_t* d_global_id,
+                                       const int64_t* d_elem_ptr, int64_t* d_row_ptr, int32_t* d_col, void* stream)
+{
+  if (!ctx || !m || !d_elem_ptr || !d_row_ptr || !d_col || nb < 1 || !m->neighbors)
+    return set_error(HDD_ERR_INVALID, "hdd_pattern_fill_device: invalid argument");
+  const int nf = mesh_faces(m);
+  if (!nf) return set_error(HDD_ERR_UNSUPPORTED, "hdd_pattern_fill_device: unknown element type");
+  if (m->own_begin < 0 || m->own_end > m->n_local || m->own_begin > m->own_end)
+    return set_error(HDD_ERR_RANGE, "hdd_pattern_fill_device: 0 <= own_begin <= own_end <= n_local violated");
+  hipError_t e = hipSetDevice(ctx->device);
+  if (e != hipSuccess) return hip_fail(e, "hdd_pattern_fill_device: hipSetDevice");
+  e = hdd::dev::launch_pattern_fill(m->neighbors, nf, nb, m->n_local, m->own_begin, m->own_end, d_global_id,
+                                    d_elem_ptr, d_row_ptr, d_col, static_cast<hipStream_t>(stream));
+  return e == hipSuccess ? HDD_OK : hip_fail(e, "hdd_pattern_fill_device: launch");
 }

@@ -1195,8 +1195,8 @@ static hipError_t launch_persistent(const AssembleArgs& a, hipStream_t s)
   if (tiles <= 0) return hipSuccess;
   const size_t lds = (size_t(64) * P::RB + 2 + P::RB) * sizeof(double);
   int dev = 0, cus = 256;
-  hipGetDevice(&dev);
-  hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   int wgcu = 4;   // measured best on MI355X for P1 (sweep 1..8: profiles/r01/sweep_wg_per_cu.log)
   if (const char* w = getenv("HDD_P1_WGCU")) wgcu = atoi(w);   // profiling sweeps only
   wgcu = std::max(1, std::min<int>(wgcu, int((160 * 1024) / lds)));   // resident by LDS (Q1 tiles: 3 per CU)

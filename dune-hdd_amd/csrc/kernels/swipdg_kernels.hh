@@ -33,6 +33,43 @@ struct AssembleArgs {
   double* vals[HDD_MAX_COMP];
 };
 
+// ---------------------------------------------------------------------------------------------
+// Q_p on affine hexahedra (HDD_HEX): 1D reference tables of the tensor-product basis / quadrature
+// (host-computed, passed by value), one launch per affine component.
+// ---------------------------------------------------------------------------------------------
+struct HexTables {
+  double sv[8], wv[8];          // volume Gauss-Legendre points / weights on [0,1]
+  double sf[8], wf[8];          // face rule
+  double Lv[4][8], Dv[4][8];    // L_k(sv_q), L_k'(sv_q): equidistant Lagrange polynomials of degree p
+  double Lf[4][8], Df[4][8];    // at the face points
+  double Le[4][2], De[4][2];    // at 0 and 1 (face planes)
+};
+
+struct HexArgs {
+  int64_t n_local, own_begin, own_end;
+  const double* coords;         // [24][n_local]
+  const int32_t* nbrs;          // [6][n_local]
+  const int64_t* elem_ptr;      // [n_own+1]
+  int32_t tkind, kkind;
+  double tc[6];
+  const double* tper;           // ISO [n_local] / SYM [6][n_local]
+  double kc, kb, kx, ky;
+  const double* kper;
+  double* vals;
+  double sigma_inner, sigma_boundary, beta;
+  HexTables tab;
+};
+
+// degree p in 1..3; (nq1v, nq1f) Gauss points per direction; *supported = false if no kernel matches
+hipError_t launch_hex(const HexArgs& a, int degree, int nq1v, int nq1f, hipStream_t s, bool* supported);
+
+// device pattern (any element type): blocks per element = 1 + interior faces
+hipError_t launch_pattern_counts(const int32_t* nbrs, int32_t nf, int64_t n_local, int64_t own_begin, int64_t own_end,
+                                 int64_t nb2, int64_t* d_counts, hipStream_t s);
+hipError_t launch_pattern_fill(const int32_t* nbrs, int32_t nf, int32_t nb, int64_t n_local, int64_t own_begin,
+                               int64_t own_end, const int64_t* gid, const int64_t* elem_ptr, int64_t* row_ptr,
+                               int32_t* col, hipStream_t s);
+
 int volume_points(int elem_type, int order);
 int face_points(int order);
 hipError_t launch_assemble(const AssembleArgs& a, int nqv, int nqf, hipStream_t s, bool* supported);

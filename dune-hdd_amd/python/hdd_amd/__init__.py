@@ -15,7 +15,7 @@ ROOT = os.path.abspath(os.path.join(_PKG, "..", ".."))          # dune-hdd_amd/
 LIB_PATH = os.path.join(ROOT, "lib", "libhdd_amd.so")
 HEADER = os.path.abspath(os.path.join(ROOT, "..", "include", "hdd.h"))
 
-SIMPLEX, CUBE = 0, 1
+SIMPLEX, CUBE, HEX = 0, 1, 2
 NBR_DIRICHLET, NBR_NEUMANN = -1, -2
 FN_CONST, FN_PER_ELEM, FN_SINUSOID = 0, 1, 2
 TENSOR_CONST, TENSOR_ISO_PER_ELEM, TENSOR_SYM_PER_ELEM = 0, 1, 2
@@ -25,6 +25,17 @@ MAX_COMP = 8
 # dune-gdt LocalEvaluation::SWIPDG::internal defaults at p = 1 (pinned by the ESV2007 expectation tables)
 SIGMA_INNER_P1 = 8.0
 SIGMA_BOUNDARY_P1 = 14.0
+# inner_sigma(p) / boundary_sigma(p) for higher p (restated dune-gdt tables)
+_SIGMA_INNER = {0: 8.0, 1: 8.0, 2: 20.0, 3: 38.0}
+_SIGMA_BOUNDARY = {0: 14.0, 1: 14.0, 2: 38.0, 3: 74.0}
+
+
+def sigma_inner(p):
+    return _SIGMA_INNER.get(p, 50.0)
+
+
+def sigma_boundary(p):
+    return _SIGMA_BOUNDARY.get(p, 99.0)
 
 
 class HddError(RuntimeError):
@@ -37,10 +48,16 @@ class StructuredDesc(C.Structure):
                 ("lower", C.c_double * 2), ("upper", C.c_double * 2)]
 
 
+class Structured3Desc(C.Structure):
+    _fields_ = [("nx", C.c_int32), ("ny", C.c_int32), ("nz", C.c_int32), ("px", C.c_int32), ("py", C.c_int32),
+                ("pz", C.c_int32), ("boundary", C.c_int32), ("degree", C.c_int32),
+                ("lower", C.c_double * 3), ("upper", C.c_double * 3)]
+
+
 class GridInfo(C.Structure):
     _fields_ = [("elem_type", C.c_int32), ("nb", C.c_int32), ("nfaces", C.c_int32), ("nvpe", C.c_int32),
                 ("n_elements", C.c_int64), ("n_vertices", C.c_int64), ("n_subdomains", C.c_int32),
-                ("pad", C.c_int32)]
+                ("dim", C.c_int32)]
 
 
 class LocalInfo(C.Structure):
@@ -49,7 +66,7 @@ class LocalInfo(C.Structure):
 
 
 class MeshT(C.Structure):
-    _fields_ = [("elem_type", C.c_int32), ("pad", C.c_int32), ("n_local", C.c_int64), ("own_begin", C.c_int64),
+    _fields_ = [("elem_type", C.c_int32), ("degree", C.c_int32), ("n_local", C.c_int64), ("own_begin", C.c_int64),
                 ("own_end", C.c_int64), ("coords", C.c_void_p), ("neighbors", C.c_void_p),
                 ("face_info", C.c_void_p)]
 
@@ -60,7 +77,7 @@ class ScalarFn(C.Structure):
 
 
 class TensorFn(C.Structure):
-    _fields_ = [("kind", C.c_int32), ("pad", C.c_int32), ("c", C.c_double * 3), ("per_elem", C.c_void_p)]
+    _fields_ = [("kind", C.c_int32), ("pad", C.c_int32), ("c", C.c_double * 6), ("per_elem", C.c_void_p)]
 
 
 class Params(C.Structure):
@@ -96,6 +113,7 @@ def lib():
         "hdd_ctx_destroy": (None, [_VP]),
         "hdd_last_error": (C.c_char_p, [_VP]),
         "hdd_grid_create_structured": (_I32, [C.POINTER(StructuredDesc), _VP]),
+        "hdd_grid_create_structured_3d": (_I32, [C.POINTER(Structured3Desc), _VP]),
         "hdd_grid_create_from_connectivity": (_I32, [_I32, _I64, _VP, _I64, _VP, _VP, _I32, _I32, _VP]),
         "hdd_grid_destroy": (None, [_VP]),
         "hdd_grid_get_info": (_I32, [_VP, C.POINTER(GridInfo)]),
@@ -111,6 +129,10 @@ def lib():
         "hdd_checkerboard": (_I32, [_I64, _VP, _VP, _VP, _I32, _I32, _VP, _VP]),
         "hdd_pattern_count": (_I32, [_I32, _I64, _I64, _I64, _VP, C.POINTER(_I64)]),
         "hdd_pattern_fill": (_I32, [_I32, _I64, _I64, _I64, _VP, _VP, _VP, _VP, _VP]),
+        "hdd_dg_pattern_count": (_I32, [_I32, _I32, _I64, _I64, _I64, _VP, C.POINTER(_I64)]),
+        "hdd_dg_pattern_fill": (_I32, [_I32, _I32, _I64, _I64, _I64, _VP, _VP, _VP, _VP, _VP]),
+        "hdd_pattern_elem_ptr_device": (_I32, [_VP, C.POINTER(MeshT), _I32, _VP, C.POINTER(_I64), _VP]),
+        "hdd_pattern_fill_device": (_I32, [_VP, C.POINTER(MeshT), _I32, _VP, _VP, _VP, _VP, _VP]),
         "hdd_swipdg_assemble": (_I32, [_VP, C.POINTER(MeshT), C.POINTER(ScalarFn), _I32, C.POINTER(TensorFn),
                                        C.POINTER(Params), C.POINTER(CsrT), _VP, _VP]),
         "hdd_swipdg_assemble_tiles": (_I32, [_VP, C.POINTER(MeshT), C.POINTER(ScalarFn), _I32, C.POINTER(TensorFn),
@@ -164,6 +186,8 @@ class Grid:
         self.ne = info.n_elements
         self.nv = info.n_vertices
         self.n_sub = info.n_subdomains
+        self.dim = info.dim
+        self.degree = 1
 
     @classmethod
     def structured(cls, elem_type, nx, ny, lower=(0.0, 0.0), upper=(1.0, 1.0), px=1, py=1,
@@ -173,6 +197,19 @@ class Grid:
         h = C.c_void_p()
         _check(lib().hdd_grid_create_structured(C.byref(d), C.byref(h)), "hdd_grid_create_structured")
         return cls(h)
+
+    @classmethod
+    def structured3d(cls, n, lower=(0.0, 0.0, 0.0), upper=(1.0, 1.0, 1.0), p=(1, 1, 1), degree=1,
+                     boundary=BOUNDARY_ALL_DIRICHLET):
+        """3d grid of n[0] x n[1] x n[2] axis-aligned hexahedra carrying DG Q_degree, p[0] x p[1] x p[2]
+        subdomains (x-slabs contiguous)."""
+        d = Structured3Desc(n[0], n[1], n[2], p[0], p[1], p[2], boundary, degree, (C.c_double * 3)(*lower),
+                            (C.c_double * 3)(*upper))
+        h = C.c_void_p()
+        _check(lib().hdd_grid_create_structured_3d(C.byref(d), C.byref(h)), "hdd_grid_create_structured_3d")
+        g = cls(h)
+        g.degree = degree
+        return g
 
     @classmethod
     def from_connectivity(cls, elem_type, coords, elem_vert, subdomain=None, n_sub=1,
@@ -188,11 +225,14 @@ class Grid:
 
     def __del__(self):
         if getattr(self, "h", None):
-            lib().hdd_grid_destroy(self.h)
+            try:
+                lib().hdd_grid_destroy(self.h)
+            except Exception:   # interpreter shutdown: module globals may already be gone
+                pass
             self.h = None
 
     def connectivity(self):
-        coords = np.empty((self.nv, 2))
+        coords = np.empty((self.nv, self.dim))
         ev = np.empty((self.ne, self.nvpe), np.int32)
         sd = np.empty(self.ne, np.int32)
         _check(lib().hdd_grid_connectivity(self.h, _p(coords), _p(ev), _p(sd)), "hdd_grid_connectivity")
@@ -221,8 +261,9 @@ class LocalMesh:
         self.n_local, self.own_begin, self.own_end = info.n_local, info.own_begin, info.own_end
         self.n_ghost, self.global_first = info.n_ghost, info.global_first
         self.elem_type, self.nb, self.nf, self.nvpe = grid.elem_type, grid.nb, grid.nf, grid.nvpe
+        self.dim, self.degree = grid.dim, grid.degree
         n = self.n_local
-        self.coords = np.empty((2 * self.nvpe, n))
+        self.coords = np.empty((self.dim * self.nvpe, n))
         self.neighbors = np.empty((self.nf, n), np.int32)
         self.face_info = np.empty(n, np.uint32)
         self.global_id = np.empty(n, np.int64)
@@ -232,7 +273,10 @@ class LocalMesh:
 
     def __del__(self):
         if getattr(self, "h", None):
-            lib().hdd_local_destroy(self.h)
+            try:
+                lib().hdd_local_destroy(self.h)
+            except Exception:   # interpreter shutdown: module globals may already be gone
+                pass
             self.h = None
 
     @property
@@ -240,7 +284,7 @@ class LocalMesh:
         return self.own_end - self.own_begin
 
     def centers(self):
-        c = np.empty((2, self.n_local))
+        c = np.empty((self.dim, self.n_local))
         _check(lib().hdd_local_centers(self.h, _p(c)), "hdd_local_centers")
         return c
 
@@ -275,13 +319,14 @@ class LocalMesh:
         """Host CSR pattern of the owned rows (global columns): row_ptr, col, elem_ptr."""
         nnz = C.c_int64()
         nbrs = np.ascontiguousarray(self.neighbors)
-        _check(lib().hdd_pattern_count(self.elem_type, self.n_local, self.own_begin, self.own_end, _p(nbrs),
-                                       C.byref(nnz)), "hdd_pattern_count")
+        _check(lib().hdd_dg_pattern_count(self.nf, self.nb, self.n_local, self.own_begin, self.own_end, _p(nbrs),
+                                          C.byref(nnz)), "hdd_dg_pattern_count")
         row_ptr = np.empty(self.nb * self.n_own + 1, np.int64)
         col = np.empty(nnz.value, np.int32)
         elem_ptr = np.empty(self.n_own + 1, np.int64)
-        _check(lib().hdd_pattern_fill(self.elem_type, self.n_local, self.own_begin, self.own_end, _p(nbrs),
-                                      _p(self.global_id), _p(row_ptr), _p(col), _p(elem_ptr)), "hdd_pattern_fill")
+        _check(lib().hdd_dg_pattern_fill(self.nf, self.nb, self.n_local, self.own_begin, self.own_end, _p(nbrs),
+                                         _p(self.global_id), _p(row_ptr), _p(col), _p(elem_ptr)),
+               "hdd_dg_pattern_fill")
         return row_ptr, col, elem_ptr
 
 
@@ -304,7 +349,10 @@ class Context:
 
     def __del__(self):
         if getattr(self, "h", None):
-            lib().hdd_ctx_destroy(self.h)
+            try:
+                lib().hdd_ctx_destroy(self.h)
+            except Exception:   # interpreter shutdown: module globals may already be gone
+                pass
             self.h = None
 
 
@@ -315,14 +363,23 @@ def scalar_fn(kind=FN_CONST, c=1.0, b=0.0, kx=0.0, ky=0.0, per_elem=None, order=
     return f
 
 
-def tensor_fn(kind=TENSOR_CONST, c=(1.0, 0.0, 1.0), per_elem=None):
-    t = TensorFn(kind, 0, (C.c_double * 3)(*c), None if per_elem is None else per_elem.data_ptr())
+def tensor_fn(kind=TENSOR_CONST, c=(1.0, 0.0, 1.0), per_elem=None, dim=2):
+    """Diffusion tensor; CONST c = (a11, a12, a22) in 2d, (a11, a12, a13, a22, a23, a33) in 3d."""
+    if dim == 3 and tuple(c) == (1.0, 0.0, 1.0):
+        c = (1.0, 0.0, 0.0, 1.0, 0.0, 1.0)
+    cc = list(c) + [0.0] * (6 - len(c))
+    t = TensorFn(kind, 0, (C.c_double * 6)(*cc), None if per_elem is None else per_elem.data_ptr())
     t._keep = per_elem
     return t
 
 
 def params(sigma_inner=SIGMA_INNER_P1, sigma_boundary=SIGMA_BOUNDARY_P1, beta=1.0, vol_order=-1, face_order=-1):
     return Params(sigma_inner, sigma_boundary, beta, vol_order, face_order)
+
+
+def params_for(degree, dim, vol_order=-1, face_order=-1):
+    """dune-gdt defaults for DG degree p in d dimensions: sigma(p), beta = 1/(d-1)."""
+    return Params(sigma_inner(degree), sigma_boundary(degree), 1.0 / (dim - 1), vol_order, face_order)
 
 
 class DeviceMesh:
@@ -339,14 +396,38 @@ class DeviceMesh:
         self.neighbors = torch.from_numpy(local.neighbors).to(dev).contiguous()
         self.face_info = torch.from_numpy(local.face_info.view(np.int32)).to(dev).contiguous()
         self.local = local
-        self.t = MeshT(local.elem_type, 0, local.n_local, local.own_begin, local.own_end, self.coords.data_ptr(),
+        self.t = MeshT(local.elem_type, local.degree, local.n_local, local.own_begin, local.own_end, self.coords.data_ptr(),
                        self.neighbors.data_ptr(), self.face_info.data_ptr())
 
 
 class DevicePattern:
-    def __init__(self, local, device=0, host=None):
+    """CSR pattern of the owned rows in HBM.  on_device=True builds it with the HIP pattern kernels
+    (hdd_pattern_elem_ptr_device / hdd_pattern_fill_device) instead of on the host."""
+
+    def __init__(self, local, device=0, host=None, ctx=None, dmesh=None, on_device=False):
         torch = _torch()
         dev = torch.device("cuda", device)
+        if on_device:
+            ctx = ctx or Context(device)
+            dmesh = dmesh or DeviceMesh(local, device)
+            s = torch.cuda.current_stream(dev).cuda_stream
+            self.elem_ptr = torch.empty(local.n_own + 1, dtype=torch.int64, device=dev)
+            nnz = C.c_int64()
+            _check(lib().hdd_pattern_elem_ptr_device(ctx.h, C.byref(dmesh.t), local.nb, self.elem_ptr.data_ptr(),
+                                                     C.byref(nnz), C.c_void_p(s)), "hdd_pattern_elem_ptr_device")
+            self.nnz = nnz.value
+            self.row_ptr = torch.empty(local.nb * local.n_own + 1, dtype=torch.int64, device=dev)
+            self.col = torch.empty(self.nnz, dtype=torch.int32, device=dev)
+            gid = torch.from_numpy(local.global_id).to(dev)
+            _check(lib().hdd_pattern_fill_device(ctx.h, C.byref(dmesh.t), local.nb, gid.data_ptr(),
+                                                 self.elem_ptr.data_ptr(), self.row_ptr.data_ptr(),
+                                                 self.col.data_ptr(), C.c_void_p(s)), "hdd_pattern_fill_device")
+            torch.cuda.current_stream(dev).synchronize()
+            self.host = None
+            n_cols = int(local.grid.ne) * local.nb
+            self.t = CsrT(local.nb * local.n_own, n_cols, self.nnz, self.row_ptr.data_ptr(), self.col.data_ptr(),
+                          self.elem_ptr.data_ptr())
+            return
         row_ptr, col, elem_ptr = host if host is not None else local.pattern()
         self.host = (row_ptr, col, elem_ptr)
         self.row_ptr = torch.from_numpy(row_ptr).to(dev)

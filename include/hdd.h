@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define HDD_ABI_VERSION 1
+#define HDD_ABI_VERSION 2
 #define HDD_MAX_COMP 8
 
 typedef enum {
@@ -41,7 +41,8 @@ typedef enum {
   HDD_ERR_RANGE = 5         /* index_out_of_range */
 } hdd_status;
 
-enum { HDD_SIMPLEX = 0, HDD_CUBE = 1 };                      /* P1 triangles / Q1 parallelograms (2d) */
+enum { HDD_SIMPLEX = 0, HDD_CUBE = 1,                       /* P1 triangles / Q1 parallelograms (2d) */
+       HDD_HEX = 2 };                                        /* Q_p (p = 1..3) on affine hexahedra (3d) */
 enum { HDD_NBR_DIRICHLET = -1, HDD_NBR_NEUMANN = -2 };       /* neighbour codes of domain-boundary faces */
 enum { HDD_FN_CONST = 0, HDD_FN_PER_ELEM = 1, HDD_FN_SINUSOID = 2 };
 enum { HDD_TENSOR_CONST = 0, HDD_TENSOR_ISO_PER_ELEM = 1, HDD_TENSOR_SYM_PER_ELEM = 2 };
@@ -75,13 +76,26 @@ typedef struct {
   double lower[2], upper[2];
 } hdd_structured_desc;
 
+/* 3d structured grid of nx x ny x nz axis-aligned hexahedra (SGrid / YaspGrid cube provider in 3d),
+ * px x py x pz subdomains (subdomain id (sx*py + sy)*pz + sz: x-slabs are contiguous element ranges);
+ * inside a subdomain elements are lexicographic (x fastest).  Faces: 2a (x_a = 0 side), 2a+1. */
 typedef struct {
-  int32_t elem_type, nb, nfaces, nvpe;
+  int32_t nx, ny, nz;
+  int32_t px, py, pz;
+  int32_t boundary;           /* HDD_BOUNDARY_* */
+  int32_t degree;             /* polynomial degree p of the DG Q_p space carried by the grid (1..3) */
+  double lower[3], upper[3];
+} hdd_structured3_desc;
+
+typedef struct {
+  int32_t elem_type, nb, nfaces, nvpe;   /* nb = basis functions per element of the carried DG space */
   int64_t n_elements, n_vertices;
-  int32_t n_subdomains, pad;
+  int32_t n_subdomains, dim;
 } hdd_grid_info;
 
 int hdd_grid_create_structured(const hdd_structured_desc* desc, hdd_grid** out);
+/* 3d (C5: ESV2007 3d structured, SWIPDG p=3) */
+int hdd_grid_create_structured_3d(const hdd_structured3_desc* desc, hdd_grid** out);
 /* general conforming 2d mesh from connectivity (vertex order = Dune reference element order);
  * `subdomain` (nullable) assigns elements to subdomains, elements are then renumbered subdomain-major */
 int hdd_grid_create_from_connectivity(int32_t elem_type, int64_t n_vertices, const double* vertex_coords,
@@ -106,7 +120,7 @@ int hdd_local_create(const hdd_grid* g, int32_t s_begin, int32_t s_end, hdd_loca
 void hdd_local_destroy(hdd_local* l);
 int hdd_local_get_info(const hdd_local* l, hdd_local_info* out);
 /* host SoA arrays, n_local columns each:
- *   coords    [2*nvpe][n_local] : x of vertex k at (2k)*n_local+e, y at (2k+1)*n_local+e (ghost rows too)
+ *   coords    [dim*nvpe][n_local]: coordinate c of vertex k at (dim*k + c)*n_local + e (ghosts too)
  *   neighbors [nfaces][n_local] : local neighbour id or HDD_NBR_* (ghost columns: -3)
  *   face_info [n_local]         : 4 bits per face: twin local face (bits 0-2), reversed (bit 3)
  *   global_id [n_local]         : global element id
@@ -114,7 +128,7 @@ int hdd_local_get_info(const hdd_local* l, hdd_local_info* out);
  * any pointer may be NULL */
 int hdd_local_fill(const hdd_local* l, double* coords, int32_t* neighbors, uint32_t* face_info,
                    int64_t* global_id, int32_t* subdomain);
-/* element barycentres [2][n_local] (coefficient lookup, e.g. the Spe10 checkerboard) */
+/* element barycentres [dim][n_local] (coefficient lookup, e.g. the Spe10 checkerboard) */
 int hdd_local_centers(const hdd_local* l, double* centers);
 /* halo plan with the subdomain -> rank map `owner` [n_subdomains]:
  *   peers[n_peers] ranks this rank exchanges with (ascending); for peer p: send_count[p] owned elements
@@ -142,6 +156,13 @@ int hdd_pattern_count(int32_t elem_type, int64_t n_local, int64_t own_begin, int
 int hdd_pattern_fill(int32_t elem_type, int64_t n_local, int64_t own_begin, int64_t own_end,
                      const int32_t* neighbors, const int64_t* global_id, int64_t* row_ptr, int32_t* col,
                      int64_t* elem_ptr);
+/* the same for any DG space: n_faces faces and nb basis functions per element (Q_p: nb = (p+1)^dim) */
+int hdd_dg_pattern_count(int32_t n_faces, int32_t nb, int64_t n_local, int64_t own_begin, int64_t own_end,
+                         const int32_t* neighbors, int64_t* nnz);
+int hdd_dg_pattern_fill(int32_t n_faces, int32_t nb, int64_t n_local, int64_t own_begin, int64_t own_end,
+                        const int32_t* neighbors, const int64_t* global_id, int64_t* row_ptr, int32_t* col,
+                        int64_t* elem_ptr);
+
 
 /* ---------------------------------------------------------------------------------------------- */
 /* device assembly -- replaces the LHS part of SWIPDG::init() (swipdg.hh:222-249 + walk() at 485):   */
@@ -149,9 +170,9 @@ int hdd_pattern_fill(int32_t elem_type, int64_t n_local, int64_t own_begin, int6
 /* SWIPDG::Inner + SWIPDG::BoundaryLHS, scattered into Q+1 CSR value arrays on one pattern; and the  */
 /* BlockSWIPDG boundary / coupling assemblers (block-swipdg.hh:1136-1179, 1270-1326).                */
 /* ---------------------------------------------------------------------------------------------- */
-typedef struct {
-  int32_t elem_type;          /* HDD_SIMPLEX | HDD_CUBE */
-  int32_t pad;
+typedef struct hdd_mesh_s {
+  int32_t elem_type;          /* HDD_SIMPLEX | HDD_CUBE | HDD_HEX */
+  int32_t degree;             /* polynomial degree p of the DG space (0 or 1: P1 / Q1; HDD_HEX: 1..3) */
   int64_t n_local;            /* columns of the SoA arrays (owned + ghosts) */
   int64_t own_begin, own_end; /* elements whose rows are assembled */
   const double* coords;       /* device, layout of hdd_local_fill */
@@ -170,15 +191,15 @@ typedef struct {              /* one diffusion-factor component kappa_q (a Stuff
 typedef struct {              /* the (non-parametric) diffusion tensor A */
   int32_t kind;               /* HDD_TENSOR_* */
   int32_t pad;
-  double c[3];                /* CONST: a11, a12, a22 */
-  const double* per_elem;     /* ISO: device [n_local]; SYM: device [3][n_local] */
+  double c[6];                /* CONST: 2d a11 a12 a22; 3d a11 a12 a13 a22 a23 a33 */
+  const double* per_elem;     /* ISO: device [n_local]; SYM: device [3 | 6][n_local] */
 } hdd_tensor_fn;
 
 typedef struct {
   double sigma_inner;         /* LocalEvaluation::SWIPDG::internal::inner_sigma(p)    (8 at p=1) */
   double sigma_boundary;      /* LocalEvaluation::SWIPDG::internal::boundary_sigma(p) (14 at p=1) */
   double beta;                /* LocalEvaluation::SWIPDG::internal::default_beta(d) = 1/(d-1) (swipdg.hh:168) */
-  int32_t vol_order;          /* -1: the reference's integrand order (ord kappa + ord A + 2(p-1)) */
+  int32_t vol_order;          /* -1: the reference's integrand order (ord kappa + ord A + 2 max(p-1, 0)) */
   int32_t face_order;         /* -1: ord kappa + ord A + 2p */
 } hdd_swipdg_params;
 
@@ -188,6 +209,15 @@ typedef struct {
   const int32_t* col;         /* device [nnz] */
   const int64_t* elem_ptr;    /* device [n_owned+1]: first value of each owned element's row block */
 } hdd_csr;
+
+/* Device pattern build (the pattern of a p=3 3d mesh is ~4 bytes x 28672 per
+ * element, too large to build on the host).  Step 1 writes d_elem_ptr [n_own+1] and returns the total
+ * nnz in *nnz (host; synchronises `stream`).  Step 2 writes d_row_ptr [nb*n_own+1] and d_col [nnz];
+ * d_global_id [n_local] maps local to global element ids (NULL: local == global). */
+int hdd_pattern_elem_ptr_device(hdd_ctx* ctx, const hdd_mesh* mesh, int32_t nb, int64_t* d_elem_ptr,
+                                int64_t* nnz, void* stream);
+int hdd_pattern_fill_device(hdd_ctx* ctx, const hdd_mesh* mesh, int32_t nb, const int64_t* d_global_id,
+                            const int64_t* d_elem_ptr, int64_t* d_row_ptr, int32_t* d_col, void* stream);
 
 /* Writes d_vals[q][0..nnz) for q < n_comp (each value exactly once, no atomics, no zero-fill needed).
  * Face terms are evaluated by the row owner on both sides of each face (owner-computes). */

@@ -248,3 +248,110 @@ def esv2007_eoc(grid, prm, elem_index=None):
     b = rhs_esv2007(grid, elem_index)
     u = spla.spsolve(A.tocsc(), b)
     return error_norms_esv2007(grid, u, elem_index)
+
+
+# ------------------------------------------------------------------------------------------------------
+# DG Q_p on structured 2D/3D cube grids (swipdg_oracle_qp.c): the C5 configuration (p = 3, 3D)
+# ------------------------------------------------------------------------------------------------------
+# dune-gdt LocalEvaluation::SWIPDG::internal::{inner,boundary}_sigma(p) (restated)
+SIGMA_INNER = {0: 8.0, 1: 8.0, 2: 20.0, 3: 38.0}
+SIGMA_BOUNDARY = {0: 14.0, 1: 14.0, 2: 38.0, 3: 74.0}
+
+
+def sigma_inner(p):
+    return SIGMA_INNER.get(p, 50.0)
+
+
+def sigma_boundary(p):
+    return SIGMA_BOUNDARY.get(p, 99.0)
+
+
+class QpGridT(C.Structure):
+    _fields_ = [("dim", C.c_int32), ("degree", C.c_int32), ("n", C.c_int64 * 3),
+                ("lower", C.c_double * 3), ("upper", C.c_double * 3)]
+
+
+class QpTensorT(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("pad", C.c_int32), ("c", C.c_double * 6), ("per_elem", C.c_void_p)]
+
+
+def _qp_lib():
+    L = lib()
+    if not getattr(L, "_qp_ready", False):
+        L.or_qp_num_elements.restype = C.c_int64
+        L.or_qp_pattern_nnz.restype = C.c_int64
+        for nm in ("or_qp_pattern", "or_qp_assemble", "or_qp_rhs_esv2007", "or_qp_error_esv2007"):
+            getattr(L, nm).restype = C.c_int
+        VP = C.c_void_p
+        L.or_qp_num_elements.argtypes = [VP]
+        L.or_qp_pattern_nnz.argtypes = [VP]
+        L.or_qp_pattern.argtypes = [VP, VP, VP, VP]
+        L.or_qp_assemble.argtypes = [VP, VP, VP, VP, VP, VP, VP, VP]
+        L.or_qp_rhs_esv2007.argtypes = [VP, C.c_int, VP, VP]
+        L.or_qp_error_esv2007.argtypes = [VP, VP, VP, C.c_int, VP, VP]
+        L._qp_ready = True
+    return L
+
+
+class QpGrid:
+    """Structured grid of n[0] x n[1] (x n[2]) axis-aligned cubes on [lower, upper] carrying DG Q_p;
+    element id = i + n0 (j + n1 k) (lexicographic, x fastest)."""
+
+    def __init__(self, dim, p, n, lower, upper):
+        self.dim, self.p = int(dim), int(p)
+        n = list(n) + [1] * (3 - len(n))
+        lo = list(lower) + [0.0] * (3 - len(lower))
+        up = list(upper) + [1.0] * (3 - len(upper))
+        self.t = QpGridT(self.dim, self.p, (C.c_int64 * 3)(*n), (C.c_double * 3)(*lo), (C.c_double * 3)(*up))
+        self.nb = (self.p + 1) ** self.dim
+        self.ne = int(_qp_lib().or_qp_num_elements(C.byref(self.t)))
+        if self.ne < 0:
+            raise ValueError("invalid Q_p grid")
+
+    def pattern(self, elem_index=None):
+        L = _qp_lib()
+        nnz = L.or_qp_pattern_nnz(C.byref(self.t))
+        rp = np.empty(self.ne * self.nb + 1, np.int64)
+        col = np.empty(nnz, np.int32)
+        ei = None if elem_index is None else np.ascontiguousarray(elem_index, np.int64)
+        L.or_qp_pattern(C.byref(self.t), _ptr(ei), _ptr(rp), _ptr(col))
+        return rp, col
+
+
+def qp_tensor(kind=TENSOR_CONST, c=None, per_elem=None, dim=3):
+    if c is None:
+        c = (1.0, 0.0, 1.0) if dim == 2 else (1.0, 0.0, 0.0, 1.0, 0.0, 1.0)
+    cc = list(c) + [0.0] * (6 - len(c))
+    t = QpTensorT(kind, 0, (C.c_double * 6)(*cc), _ptr(per_elem))
+    t._keep = per_elem
+    return t
+
+
+def qp_params(grid, boundary=BOUNDARY_DIRICHLET, vol_order=-1, face_order=-1):
+    return ParamsT(sigma_inner(grid.p), sigma_boundary(grid.p), 1.0 / (grid.dim - 1), boundary, vol_order,
+                   face_order, 0)
+
+
+def qp_assemble(grid, kappa, A, prm, elem_index=None, pattern=None):
+    ei = None if elem_index is None else np.ascontiguousarray(elem_index, np.int64)
+    rp, col = pattern if pattern is not None else grid.pattern(ei)
+    val = np.empty(col.shape[0], np.float64)
+    rc = _qp_lib().or_qp_assemble(C.byref(grid.t), C.byref(kappa), C.byref(A), C.byref(prm), _ptr(ei), _ptr(rp),
+                                  _ptr(col), _ptr(val))
+    if rc:
+        raise ValueError("or_qp_assemble failed")
+    return rp, col, val
+
+
+def qp_esv2007_errors(grid, elem_index=None):
+    """Assemble + solve the d-dimensional ESV2007 problem (u = prod cos(pi x_a/2)) on the Q_p grid;
+    returns (L2, H1-semi) errors."""
+    import scipy.sparse.linalg as spla
+    rp, col, val = qp_assemble(grid, scalar(FN_CONST, 1.0), qp_tensor(dim=grid.dim), qp_params(grid), elem_index)
+    b = np.empty(grid.ne * grid.nb)
+    ei = None if elem_index is None else np.ascontiguousarray(elem_index, np.int64)
+    _qp_lib().or_qp_rhs_esv2007(C.byref(grid.t), 3 if grid.dim == 2 else 3, _ptr(ei), _ptr(b))
+    u = spla.spsolve(to_scipy(rp, col, val).tocsc(), b)
+    l2, h1 = C.c_double(), C.c_double()
+    _qp_lib().or_qp_error_esv2007(C.byref(grid.t), _ptr(u), _ptr(ei), 2 * grid.p + 6, C.byref(l2), C.byref(h1))
+    return l2.value, h1.value

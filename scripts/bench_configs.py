@@ -7,6 +7,10 @@
       (seed 14), materialised in HBM.
   c4  SPE10-like 3520 x 1200 Q1 quads on [0,5]x[0,1], 8x8 subdomains (block numbering), synthetic
       permeability, single GPU (the 8-GPU sharded form is bench.py --gpus 8 on the strip workload).
+  c5  ESV2007 3d structured, n^3 axis-aligned hexahedra on [-1,1]^3 (default n = 64: 262,144 elements,
+      16.8 M DoFs, 7.4 G nnz, 59 GB of values resident in HBM), DG Q3 (64 basis functions), kappa = 1, A = I,
+      AllDirichlet; f64 MFMA kernel (hex_qp.hip).  The device pattern build is timed separately (the
+      reference builds its pattern outside init(), swipdg.hh:169).
 Prints one JSON line per config."""
 import argparse
 import json
@@ -81,6 +85,43 @@ def c4(args):
                 assembled_dofs_per_s=dofs / t, alg_GBps=alg / t / 1e9, roofline_frac=alg / t / 8e12)
 
 
+def c5(args):
+    import torch
+    import hdd_amd as H
+    n, deg = (args.n or 64), args.degree
+    grid = H.Grid.structured3d((n, n, n), (-1, -1, -1), (1, 1, 1), degree=deg)
+    loc = grid.local()
+    ctx = H.Context(0)
+    dm = H.DeviceMesh(loc)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    dp = H.DevicePattern(loc, ctx=ctx, dmesh=dm, on_device=True)
+    torch.cuda.synchronize()
+    t_pat = time.perf_counter() - t0
+    vals = [torch.empty(dp.nnz, dtype=torch.float64, device="cuda")]
+    prm = H.params_for(deg, 3)
+    fn = lambda: H.assemble(ctx, dm, dp, [H.scalar_fn(H.FN_CONST, 1.0)], H.tensor_fn(dim=3), prm, vals=vals)
+    t = timed(fn, args.steps, args.warmup)
+    nb = grid.nb
+    nbr = loc.neighbors
+    n_inner = int((nbr >= 0).sum())                 # interior (element, face) pairs = 2 nif
+    nif, nbf = n_inner // 2, int((nbr == H.NBR_DIRICHLET).sum())
+    nq1v, nq1f = deg, deg + 1                        # reference integrand orders 2(p-1) / 2p
+    nq, nqf = nq1v ** 3, nq1f ** 2
+    # F = ne 2 nb^2 nq d + nif 24 nb^2 nqf + nbf 6 nb^2 nqf (reference quadrature)
+    alg_flops = loc.n_own * 2 * nb * nb * nq * 3 + nif * 24 * nb * nb * nqf + nbf * 6 * nb * nb * nqf
+    nbp = (nb + 15) // 16 * 16
+    kv, kf = (3 * nq + 3) // 4 * 4, (2 * nqf + 3) // 4 * 4
+    mfma_flops = 2 * nbp * nbp * (loc.n_own * (kv + 6 * kf) + n_inner * kf)   # executed (padded) MFMA work
+    alg_bytes = 8 * dp.nnz + loc.n_own * (24 * 8 + 8 + 6 * 4)
+    dofs = nb * loc.n_own
+    return dict(config="c5_esv2007_3d_q%d_%d^3" % (deg, n), dofs=dofs, nnz=dp.nnz, values_GB=8 * dp.nnz / 1e9,
+                pattern_build_s=t_pat, assembly_ms=t * 1e3, assembled_dofs_per_s=dofs / t,
+                alg_GBps=alg_bytes / t / 1e9, hbm_frac=alg_bytes / t / 8e12,
+                alg_TFLOPs=alg_flops / t / 1e12, mfma_exec_TFLOPs=mfma_flops / t / 1e12,
+                fp64_peak_TF=78.6, mfma_frac=mfma_flops / t / 78.6e12)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("configs", nargs="*", default=["c3", "c4"])
@@ -88,11 +129,12 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--samples", type=int, default=128)
     ap.add_argument("--n", type=int, default=0)
+    ap.add_argument("--degree", type=int, default=3)
     args = ap.parse_args()
     import torch
     torch.cuda.set_device(0)
     for c in args.configs:
-        print(json.dumps(dict(c3=c3, c4=c4)[c](args)), flush=True)
+        print(json.dumps(dict(c3=c3, c4=c4, c5=c5)[c](args)), flush=True)
 
 
 if __name__ == "__main__":
