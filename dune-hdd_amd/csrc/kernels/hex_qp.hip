@@ -26,6 +26,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 
 #include "swipdg_kernels.hh"
 
@@ -378,6 +379,287 @@ __global__ __launch_bounds__((HexCfg<P, SM>::THREADS)) void hex_qp_kernel(HexArg
   }
 }
 
+// ---------------------------------------------------------------------------------------------------
+// p = 3, reference integrand orders, piecewise-constant kappa (the C5 configuration): register-only
+// fragment generation.  With lane l = 16 g + r, r = i0 + 4 i1 and row tile I = i2, every MFMA operand value
+// is (per-lane factor) x (wave-uniform factor): the lane group g carries one quadrature coordinate
+// (q0 in the volume, qs on faces) and the k-step the others (compile-time after unrolling).  No LDS
+// tables, no barriers in the element loop; each wave (column tile w) is independent.
+//   volume K: k-step s = (a, q1, q2) (27 steps, g = q0 with q0 = 3 a zero-weight pad), faces K: 8 steps,
+//   s < 4: [V] with qt = s, s >= 4: [N] with qt = s - 4 (qs = g).
+// ---------------------------------------------------------------------------------------------------
+struct Q3Tab {
+  double Lv[4][3], Dv[4][3], wv[3];   // volume (3 Gauss points per direction)
+  double Lf[4][4], Df[4][4], wf[4];   // faces (4 points)
+  double Le[4][2], De[4][2];          // on the face planes x = 0 / 1
+};
+
+// value and (c . reference gradient) of the basis function with lane indices (i0, i1) and third index
+// T (factors lT*, uniform) at the face point (qs = g, qt) of a face with axis AF, side value table column
+template <int AF>
+__device__ __forceinline__ void q3_face_eval(double Le0, double De0, double Le1, double De1,   // [i0][sd], [i1][sd]
+                                             double Lfg0, double Dfg0, double Lfg1, double Dfg1, // [i0][g], [i1][g]
+                                             double Lf1q, double Df1q,                         // [i1][qt]
+                                             double lTf, double dTf, double lTe, double dTe,   // [T][qt], [T][sd]
+                                             double c0, double c1, double c2, double& V, double& N)
+{
+  if (AF == 0) {          // x face: x <-> i0 (side), y <-> i1 (qs), z <-> T (qt)
+    const double b = Le0 * Lfg1;
+    V = b * lTf;
+    N = (c0 * De0 * Lfg1 + c1 * Le0 * Dfg1) * lTf + c2 * b * dTf;
+  } else if (AF == 1) {   // y face: x <-> i0 (qs), y <-> i1 (side), z <-> T (qt)
+    const double b = Lfg0 * Le1;
+    V = b * lTf;
+    N = (c0 * Dfg0 * Le1 + c1 * Lfg0 * De1) * lTf + c2 * b * dTf;
+  } else {                // z face: x <-> i0 (qs), y <-> i1 (qt), z <-> T (side)
+    const double b = Lfg0 * Lf1q;
+    V = b * lTe;
+    N = (c0 * Dfg0 * Lf1q + c1 * Lfg0 * Df1q) * lTe + c2 * b * dTe;
+  }
+}
+
+struct Q3Face {
+  double cm[3], cp[3], ca, cb, ce;
+  int32_t nf;
+  bool inner;
+};
+
+__global__ __launch_bounds__(256) void hex_q3_kernel(HexArgs a)
+{
+  constexpr int NB = 64;
+  __shared__ Q3Tab T;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  if (tid == 0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+#pragma unroll
+      for (int q = 0; q < 3; ++q) { T.Lv[r][q] = a.tab.Lv[r][q]; T.Dv[r][q] = a.tab.Dv[r][q]; }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) { T.Lf[r][q] = a.tab.Lf[r][q]; T.Df[r][q] = a.tab.Df[r][q]; }
+#pragma unroll
+      for (int q = 0; q < 2; ++q) { T.Le[r][q] = a.tab.Le[r][q]; T.De[r][q] = a.tab.De[r][q]; }
+    }
+#pragma unroll
+    for (int q = 0; q < 3; ++q) T.wv[q] = a.tab.wv[q];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) T.wf[q] = a.tab.wf[q];
+  }
+  __syncthreads();
+  const int r = lane & 15, g = lane >> 4, i0 = r & 3, i1 = r >> 2;
+  // per-lane volume factors (q0 = g; g = 3 is a zero-weight pad)
+  const bool gv = g < 3;
+  const int gq = gv ? g : 0;
+  const double Lv0g = gv ? T.Lv[i0][gq] : 0.0, Dv0g = gv ? T.Dv[i0][gq] : 0.0, wvg = gv ? T.wv[gq] : 0.0;
+  double P01[3][3];
+#pragma unroll
+  for (int q1 = 0; q1 < 3; ++q1) {
+    P01[0][q1] = Dv0g * T.Lv[i1][q1];
+    P01[1][q1] = Lv0g * T.Dv[i1][q1];
+    P01[2][q1] = Lv0g * T.Lv[i1][q1];
+  }
+  // per-lane face factors
+  const double Lfg0 = T.Lf[i0][g], Dfg0 = T.Df[i0][g], Lfg1 = T.Lf[i1][g], Dfg1 = T.Df[i1][g], wfg = T.wf[g];
+  double Lf1[4], Df1[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) { Lf1[q] = T.Lf[i1][q]; Df1[q] = T.Df[i1][q]; }
+  const double Le0[2] = {T.Le[i0][0], T.Le[i0][1]}, De0[2] = {T.De[i0][0], T.De[i0][1]};
+  const double Le1[2] = {T.Le[i1][0], T.Le[i1][1]}, De1[2] = {T.De[i1][0], T.De[i1][1]};
+  // wave-uniform factors of the column tile w (third index j2 = w)
+  double LvW[3], DvW[3], LfW[4], DfW[4], LeW[2], DeW[2];
+#pragma unroll
+  for (int q = 0; q < 3; ++q) { LvW[q] = T.Lv[w][q]; DvW[q] = T.Dv[w][q]; }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) { LfW[q] = T.Lf[w][q]; DfW[q] = T.Df[w][q]; }
+#pragma unroll
+  for (int q = 0; q < 2; ++q) { LeW[q] = T.Le[w][q]; DeW[q] = T.De[w][q]; }
+
+  const int col = w * 16 + r;
+  const int64_t n_own = a.own_end - a.own_begin;
+  for (int64_t k = blockIdx.x; k < n_own; k += gridDim.x) {
+    const int64_t e = a.own_begin + k;
+    ElemGeo G;
+    elem_geo(a, e, G);
+    double A[3][3];
+    elem_tensor(a, e, A);
+    const double ke = a.kkind == HDD_FN_PER_ELEM ? a.kper[e] : a.kc;
+    int32_t nbr[6];
+#pragma unroll
+    for (int f = 0; f < 6; ++f) nbr[f] = a.nbrs[f * a.n_local + e];
+    int nblk = 1;
+#pragma unroll
+    for (int f = 0; f < 6; ++f) nblk += nbr[f] >= 0;
+    const int64_t rl = int64_t(NB) * nblk;
+    auto pos_of = [&](int64_t x) {
+      int p = e < x;
+#pragma unroll
+      for (int f = 0; f < 6; ++f) p += (nbr[f] >= 0 && nbr[f] < x);
+      return p;
+    };
+    double* out = a.vals + a.elem_ptr[k];
+
+    // ---- volume: G_q = w_q |det J| kappa M,  M = J^{-1} A J^{-T} ----
+    double M[3][3];
+    {
+      double JA[3][3];
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) JA[i][j] = G.Ji[i][0] * A[0][j] + G.Ji[i][1] * A[1][j] + G.Ji[i][2] * A[2][j];
+      const double gf = fabs(G.det) * ke;
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+          M[i][j] = gf * (JA[i][0] * G.Ji[j][0] + JA[i][1] * G.Ji[j][1] + JA[i][2] * G.Ji[j][2]);
+    }
+    dbl4 S[4];
+#pragma unroll
+    for (int I = 0; I < 4; ++I) S[I] = dbl4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int q2 = 0; q2 < 3; ++q2)
+#pragma unroll
+      for (int q1 = 0; q1 < 3; ++q1) {
+        const double wq = wvg * T.wv[q1] * T.wv[q2];
+        const double D0 = P01[0][q1] * LvW[q2], D1 = P01[1][q1] * LvW[q2], D2 = P01[2][q1] * DvW[q2];
+#pragma unroll
+        for (int ax = 0; ax < 3; ++ax) {
+          const double b = wq * (M[ax][0] * D0 + M[ax][1] * D1 + M[ax][2] * D2);
+#pragma unroll
+          for (int I = 0; I < 4; ++I) {
+            const double t2 = ax == 2 ? T.Dv[I][q2] : T.Lv[I][q2];
+            S[I] = mfma(P01[ax][q1] * t2, b, S[I]);
+          }
+        }
+      }
+
+    // ---- faces ----
+#pragma unroll
+    for (int f = 0; f < 6; ++f) {
+      constexpr int dummy = 0;
+      (void)dummy;
+      const int32_t nf = nbr[f];
+      if (nf == HDD_NBR_NEUMANN) continue;
+      const bool inner = nf >= 0;
+      const int af = f >> 1, sd = f & 1;
+      const double sg = sd ? 1.0 : -1.0;
+      double n[3] = {sg * G.Ji[af][0], sg * G.Ji[af][1], sg * G.Ji[af][2]};
+      const double nn = sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+      n[0] /= nn; n[1] /= nn; n[2] /= nn;
+      const double fvol = fabs(G.det) * nn;
+      const double hpow = pow(fvol, a.beta);
+      double An[3], cm[3];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) An[i] = A[i][0] * n[0] + A[i][1] * n[1] + A[i][2] * n[2];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) cm[i] = G.Ji[i][0] * An[0] + G.Ji[i][1] * An[1] + G.Ji[i][2] * An[2];
+      const double dm = n[0] * An[0] + n[1] * An[1] + n[2] * An[2];
+      double cp[3] = {0.0, 0.0, 0.0}, wm = 1.0, wp = 0.0, gam = dm, sig = a.sigma_boundary, kn = 0.0;
+      if (inner) {
+        ElemGeo Gn;
+        elem_geo(a, nf, Gn);
+        double Ao[3][3], Ano[3];
+        elem_tensor(a, nf, Ao);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) Ano[i] = Ao[i][0] * n[0] + Ao[i][1] * n[1] + Ao[i][2] * n[2];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) cp[i] = Gn.Ji[i][0] * Ano[0] + Gn.Ji[i][1] * Ano[1] + Gn.Ji[i][2] * Ano[2];
+        const double dp = n[0] * Ano[0] + n[1] * Ano[1] + n[2] * Ano[2];
+        gam = dp * dm / (dp + dm);
+        wp = dm / (dp + dm);
+        wm = dp / (dp + dm);
+        sig = a.sigma_inner;
+        kn = a.kkind == HDD_FN_PER_ELEM ? a.kper[nf] : a.kc;
+      }
+      const double ca = fvol * wm * ke, cb = fvol * wp * kn;
+      const double ce = fvol * sig * (inner ? ke * kn : ke) * gam / hpow;
+      dbl4 E[4];
+#pragma unroll
+      for (int I = 0; I < 4; ++I) E[I] = dbl4{0.0, 0.0, 0.0, 0.0};
+      const int so = sd, sn = 1 - sd;   // own / neighbour side of the face planes
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        const int qt = s & 3;
+        const bool vpart = s < 4;
+        const double wq = wfg * T.wf[qt];
+        const double al = ca * wq, be = cb * wq, et = ce * wq;
+        // column side (third index w): own and neighbour values
+        double Vo, No, Vn = 0.0, Nn = 0.0;
+        switch (af) {
+          case 0:
+            q3_face_eval<0>(Le0[so], De0[so], Le1[so], De1[so], Lfg0, Dfg0, Lfg1, Dfg1, Lf1[qt], Df1[qt], LfW[qt],
+                            DfW[qt], LeW[so], DeW[so], cm[0], cm[1], cm[2], Vo, No);
+            if (inner)
+              q3_face_eval<0>(Le0[sn], De0[sn], Le1[sn], De1[sn], Lfg0, Dfg0, Lfg1, Dfg1, Lf1[qt], Df1[qt], LfW[qt],
+                              DfW[qt], LeW[sn], DeW[sn], cp[0], cp[1], cp[2], Vn, Nn);
+            break;
+          case 1:
+            q3_face_eval<1>(Le0[so], De0[so], Le1[so], De1[so], Lfg0, Dfg0, Lfg1, Dfg1, Lf1[qt], Df1[qt], LfW[qt],
+                            DfW[qt], LeW[so], DeW[so], cm[0], cm[1], cm[2], Vo, No);
+            if (inner)
+              q3_face_eval<1>(Le0[sn], De0[sn], Le1[sn], De1[sn], Lfg0, Dfg0, Lfg1, Dfg1, Lf1[qt], Df1[qt], LfW[qt],
+                              DfW[qt], LeW[sn], DeW[sn], cp[0], cp[1], cp[2], Vn, Nn);
+            break;
+          default:
+            q3_face_eval<2>(Le0[so], De0[so], Le1[so], De1[so], Lfg0, Dfg0, Lfg1, Dfg1, Lf1[qt], Df1[qt], LfW[qt],
+                            DfW[qt], LeW[so], DeW[so], cm[0], cm[1], cm[2], Vo, No);
+            if (inner)
+              q3_face_eval<2>(Le0[sn], De0[sn], Le1[sn], De1[sn], Lfg0, Dfg0, Lfg1, Dfg1, Lf1[qt], Df1[qt], LfW[qt],
+                              DfW[qt], LeW[sn], DeW[sn], cp[0], cp[1], cp[2], Vn, Nn);
+            break;
+        }
+        const double bE = vpart ? et * Vo - al * No : -al * Vo;
+        const double bN = vpart ? -be * Nn - et * Vn : al * Vn;
+#pragma unroll
+        for (int I = 0; I < 4; ++I) {
+          // z faces: the V part of the row side is supported on the plane row tile I = 3 sd only
+          if (af == 2 && vpart && I != 3 * sd) continue;
+          double Va, Na;
+          const double lTf = T.Lf[I][qt], dTf = T.Df[I][qt], lTe = T.Le[I][so], dTe = T.De[I][so];
+          switch (af) {
+            case 0:
+              q3_face_eval<0>(Le0[so], De0[so], Le1[so], De1[so], Lfg0, Dfg0, Lfg1, Dfg1, Lf1[qt], Df1[qt], lTf, dTf,
+                              lTe, dTe, cm[0], cm[1], cm[2], Va, Na);
+              break;
+            case 1:
+              q3_face_eval<1>(Le0[so], De0[so], Le1[so], De1[so], Lfg0, Dfg0, Lfg1, Dfg1, Lf1[qt], Df1[qt], lTf, dTf,
+                              lTe, dTe, cm[0], cm[1], cm[2], Va, Na);
+              break;
+            default:
+              q3_face_eval<2>(Le0[so], De0[so], Le1[so], De1[so], Lfg0, Dfg0, Lfg1, Dfg1, Lf1[qt], Df1[qt], lTf, dTf,
+                              lTe, dTe, cm[0], cm[1], cm[2], Va, Na);
+              break;
+          }
+          const double av = vpart ? Va : Na;
+          S[I] = mfma(av, bE, S[I]);
+          if (inner) E[I] = mfma(av, bN, E[I]);
+        }
+      }
+      if (inner) {
+        const int64_t cofs = int64_t(pos_of(nf)) * NB;
+#pragma unroll
+        for (int I = 0; I < 4; ++I)
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr) out[(I * 16 + g + 4 * rr) * rl + cofs + col] = E[I][rr];
+      }
+    }
+    const int64_t sofs = int64_t(pos_of(e)) * NB;
+#pragma unroll
+    for (int I = 0; I < 4; ++I)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) out[(I * 16 + g + 4 * rr) * rl + sofs + col] = S[I][rr];
+  }
+}
+
+static hipError_t launch_hex_q3(const HexArgs& a, hipStream_t s)
+{
+  const int64_t n_own = a.own_end - a.own_begin;
+  if (n_own <= 0) return hipSuccess;
+  const int64_t grid = std::min<int64_t>(n_own, 1 << 20);
+  hipLaunchKernelGGL(hex_q3_kernel, dim3(unsigned(grid)), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
 template <int P, int SM>
 static hipError_t launch_hex_t(const HexArgs& a, hipStream_t s)
 {
@@ -397,6 +679,8 @@ hipError_t launch_hex(const HexArgs& a, int degree, int nq1v, int nq1f, hipStrea
     *supported = false;
     return hipSuccess;
   }
+  static const bool generic = getenv("HDD_HEX_GENERIC") != nullptr;   // A/B against the LDS-table kernel
+  if (degree == 3 && sm == 0 && a.kkind != HDD_FN_SINUSOID && !generic) return launch_hex_q3(a, s);
   switch (degree * 2 + sm) {
     case 2: return launch_hex_t<1, 0>(a, s);
     case 3: return launch_hex_t<1, 1>(a, s);
