@@ -19,7 +19,26 @@
 
 struct hdd_ctx {
   int device = 0;
+  void* ws = nullptr;       // device workspace (per-element coefficient records of the p=3 hex kernel)
+  size_t ws_bytes = 0;
 };
+
+// grows the context workspace; allocation happens only on the first call of a size class, so warm the
+// context up once before capturing hdd_swipdg_assemble into a hipGraph
+static hipError_t ctx_workspace(hdd_ctx* ctx, size_t bytes, void** out)
+{
+  if (bytes > ctx->ws_bytes) {
+    if (ctx->ws) (void)hipFree(ctx->ws);
+    ctx->ws = nullptr;
+    ctx->ws_bytes = 0;
+    const size_t grow = bytes + bytes / 4;
+    hipError_t e = hipMalloc(&ctx->ws, grow);
+    if (e != hipSuccess) return e;
+    ctx->ws_bytes = grow;
+  }
+  *out = ctx->ws;
+  return hipSuccess;
+}
 
 using hdd::set_error;
 
@@ -43,7 +62,11 @@ extern "C" int hdd_ctx_create(int hip_device, hdd_ctx** out)
   return HDD_OK;
 }
 
-extern "C" void hdd_ctx_destroy(hdd_ctx* ctx) { delete ctx; }
+extern "C" void hdd_ctx_destroy(hdd_ctx* ctx)
+{
+  if (ctx && ctx->ws) (void)hipFree(ctx->ws);
+  delete ctx;
+}
 
 static int fn_order(const hdd_scalar_fn& f) { return f.kind == HDD_FN_SINUSOID ? f.order : 0; }
 
@@ -153,6 +176,12 @@ static int assemble_hex(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_fn* ka
       for (int q = 0; q < nq1v; ++q) lagrange_1d(deg, r, a.tab.sv[q], &a.tab.Lv[r][q], &a.tab.Dv[r][q]);
       for (int q = 0; q < nq1f; ++q) lagrange_1d(deg, r, a.tab.sf[q], &a.tab.Lf[r][q], &a.tab.Df[r][q]);
       for (int q = 0; q < 2; ++q) lagrange_1d(deg, r, double(q), &a.tab.Le[r][q], &a.tab.De[r][q]);
+    }
+    if (hex_uses_records(a, deg, nq1v, nq1f)) {
+      void* ws = nullptr;
+      e = ctx_workspace(ctx, size_t(std::max<int64_t>(1, m->own_end - m->own_begin)) * HEX_REC * sizeof(double), &ws);
+      if (e != hipSuccess) return hip_fail(e, "hdd_swipdg_assemble: workspace");
+      a.ws = static_cast<double*>(ws);
     }
     bool supported = false;
     e = launch_hex(a, deg, nq1v, nq1f, static_cast<hipStream_t>(stream), &supported);

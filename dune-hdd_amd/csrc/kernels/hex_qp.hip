@@ -27,6 +27,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstdlib>
+#include <type_traits>
 
 #include "swipdg_kernels.hh"
 
@@ -388,12 +389,6 @@ __global__ __launch_bounds__((HexCfg<P, SM>::THREADS)) void hex_qp_kernel(HexArg
 //   volume K: k-step s = (a, q1, q2) (27 steps, g = q0 with q0 = 3 a zero-weight pad), faces K: 8 steps,
 //   s < 4: [V] with qt = s, s >= 4: [N] with qt = s - 4 (qs = g).
 // ---------------------------------------------------------------------------------------------------
-struct Q3Tab {
-  double Lv[4][3], Dv[4][3], wv[3];   // volume (3 Gauss points per direction)
-  double Lf[4][4], Df[4][4], wf[4];   // faces (4 points)
-  double Le[4][2], De[4][2];          // on the face planes x = 0 / 1
-};
-
 // value and (c . reference gradient) of the basis function with lane indices (i0, i1) and third index
 // T (factors lT*, uniform) at the face point (qs = g, qt) of a face with axis AF, side value table column
 template <int AF>
@@ -418,32 +413,112 @@ __device__ __forceinline__ void q3_face_eval(double Le0, double De0, double Le1,
   }
 }
 
-struct Q3Face {
-  double cm[3], cp[3], ca, cb, ce;
-  int32_t nf;
-  bool inner;
-};
+// Per-element coefficient record (HEX_REC doubles), written by hex_q3_setup_kernel (one thread per
+// element: geometry, neighbour geometry, normals, |F|^beta, weights, penalties, block positions) and read
+// by hex_q3_kernel with scalar loads, so the MFMA waves carry no dependent global-load chains:
+//   [0] value offset of the element's row block (int64)   [1] nblk (lo 32) | position of the self block (hi 32)
+//   [2..7] M = |det J| kappa J^{-1} A J^{-T} (xx xy xz yy yz zz)
+//   [8 + 10 f + 0..8] face f: cm[3] = J^{-1} A^- n, cp[3] = J^{-1}_+ A^+ n, ca, cb, ce (alpha / beta / eta
+//   without the quadrature weight);  [8 + 10 f + 9]: kind (lo 32: -2 Neumann, -1 Dirichlet, 1 inner) | block position (hi 32)
+__device__ __forceinline__ double i2d(int64_t v) { return __longlong_as_double(v); }
+__device__ __forceinline__ int64_t d2i(double v) { return __double_as_longlong(v); }
 
-__global__ __launch_bounds__(256) void hex_q3_kernel(HexArgs a)
+__global__ __launch_bounds__(256) void hex_q3_setup_kernel(HexArgs a)
+{
+  const int64_t k = blockIdx.x * int64_t(blockDim.x) + threadIdx.x;
+  const int64_t n_own = a.own_end - a.own_begin;
+  if (k >= n_own) return;
+  const int64_t e = a.own_begin + k;
+  double* R = a.ws + k * HEX_REC;
+  ElemGeo G;
+  elem_geo(a, e, G);
+  double A[3][3];
+  elem_tensor(a, e, A);
+  const double ke = a.kkind == HDD_FN_PER_ELEM ? a.kper[e] : a.kc;
+  int32_t nbr[6];
+#pragma unroll
+  for (int f = 0; f < 6; ++f) nbr[f] = a.nbrs[f * a.n_local + e];
+  int nblk = 1;
+#pragma unroll
+  for (int f = 0; f < 6; ++f) nblk += nbr[f] >= 0;
+  auto pos_of = [&](int64_t x) {
+    int p = e < x;
+#pragma unroll
+    for (int f = 0; f < 6; ++f) p += (nbr[f] >= 0 && nbr[f] < x);
+    return p;
+  };
+  R[0] = i2d(a.elem_ptr[k]);
+  R[1] = i2d(int64_t(uint32_t(nblk)) | (int64_t(pos_of(e)) << 32));
+  {
+    double JA[3][3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) JA[i][j] = G.Ji[i][0] * A[0][j] + G.Ji[i][1] * A[1][j] + G.Ji[i][2] * A[2][j];
+    const double gf = fabs(G.det) * ke;
+    const int ij[6][2] = {{0, 0}, {0, 1}, {0, 2}, {1, 1}, {1, 2}, {2, 2}};
+#pragma unroll
+    for (int m = 0; m < 6; ++m) {
+      const int i = ij[m][0], j = ij[m][1];
+      R[2 + m] = gf * (JA[i][0] * G.Ji[j][0] + JA[i][1] * G.Ji[j][1] + JA[i][2] * G.Ji[j][2]);
+    }
+  }
+#pragma unroll
+  for (int f = 0; f < 6; ++f) {
+    double* F = R + 8 + 10 * f;
+    const int32_t nf = nbr[f];
+    const int af = f >> 1, sd = f & 1;
+    const bool inner = nf >= 0;
+    const double sg = sd ? 1.0 : -1.0;
+    double n[3] = {sg * G.Ji[af][0], sg * G.Ji[af][1], sg * G.Ji[af][2]};
+    const double nn = sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+    n[0] /= nn; n[1] /= nn; n[2] /= nn;
+    const double fvol = fabs(G.det) * nn;
+    const double hpow = pow(fvol, a.beta);
+    double An[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) An[i] = A[i][0] * n[0] + A[i][1] * n[1] + A[i][2] * n[2];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) F[i] = G.Ji[i][0] * An[0] + G.Ji[i][1] * An[1] + G.Ji[i][2] * An[2];
+    const double dm = n[0] * An[0] + n[1] * An[1] + n[2] * An[2];
+    double cp[3] = {0.0, 0.0, 0.0}, wm = 1.0, wp = 0.0, gam = dm, sig = a.sigma_boundary, kn = 0.0;
+    if (inner) {
+      ElemGeo Gn;
+      elem_geo(a, nf, Gn);
+      double Ao[3][3], Ano[3];
+      elem_tensor(a, nf, Ao);
+#pragma unroll
+      for (int i = 0; i < 3; ++i) Ano[i] = Ao[i][0] * n[0] + Ao[i][1] * n[1] + Ao[i][2] * n[2];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) cp[i] = Gn.Ji[i][0] * Ano[0] + Gn.Ji[i][1] * Ano[1] + Gn.Ji[i][2] * Ano[2];
+      const double dp = n[0] * Ano[0] + n[1] * Ano[1] + n[2] * Ano[2];
+      gam = dp * dm / (dp + dm);
+      wp = dm / (dp + dm);
+      wm = dp / (dp + dm);
+      sig = a.sigma_inner;
+      kn = a.kkind == HDD_FN_PER_ELEM ? a.kper[nf] : a.kc;
+    }
+    F[3] = cp[0]; F[4] = cp[1]; F[5] = cp[2];
+    F[6] = fvol * wm * ke;
+    F[7] = fvol * wp * kn;
+    F[8] = fvol * sig * (inner ? ke * kn : ke) * gam / hpow;
+    const int32_t kind = inner ? 1 : nf;
+    F[9] = i2d(int64_t(uint32_t(kind)) | (int64_t(inner ? pos_of(nf) : 0) << 32));
+  }
+}
+
+typedef const double __attribute__((address_space(4)))* cdptr;   // constant AS: uniform loads -> s_load
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void hex_q3_kernel(HexArgs a)
 {
   constexpr int NB = 64;
-  __shared__ Q3Tab T;
+  __shared__ HexTables T;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  if (tid == 0) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-#pragma unroll
-      for (int q = 0; q < 3; ++q) { T.Lv[r][q] = a.tab.Lv[r][q]; T.Dv[r][q] = a.tab.Dv[r][q]; }
-#pragma unroll
-      for (int q = 0; q < 4; ++q) { T.Lf[r][q] = a.tab.Lf[r][q]; T.Df[r][q] = a.tab.Df[r][q]; }
-#pragma unroll
-      for (int q = 0; q < 2; ++q) { T.Le[r][q] = a.tab.Le[r][q]; T.De[r][q] = a.tab.De[r][q]; }
-    }
-#pragma unroll
-    for (int q = 0; q < 3; ++q) T.wv[q] = a.tab.wv[q];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) T.wf[q] = a.tab.wf[q];
+  {   // flat parallel copy of the by-value tables
+    const double* src = &a.tab.sv[0];
+    double* dst = &T.sv[0];
+    for (int i = tid; i < int(sizeof(HexTables) / sizeof(double)); i += blockDim.x) dst[i] = src[i];
   }
   __syncthreads();
   const int r = lane & 15, g = lane >> 4, i0 = r & 3, i1 = r >> 2;
@@ -460,190 +535,114 @@ __global__ __launch_bounds__(256) void hex_q3_kernel(HexArgs a)
   }
   // per-lane face factors
   const double Lfg0 = T.Lf[i0][g], Dfg0 = T.Df[i0][g], Lfg1 = T.Lf[i1][g], Dfg1 = T.Df[i1][g], wfg = T.wf[g];
-  double Lf1[4], Df1[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) { Lf1[q] = T.Lf[i1][q]; Df1[q] = T.Df[i1][q]; }
   const double Le0[2] = {T.Le[i0][0], T.Le[i0][1]}, De0[2] = {T.De[i0][0], T.De[i0][1]};
   const double Le1[2] = {T.Le[i1][0], T.Le[i1][1]}, De1[2] = {T.De[i1][0], T.De[i1][1]};
-  // wave-uniform factors of the column tile w (third index j2 = w)
-  double LvW[3], DvW[3], LfW[4], DfW[4], LeW[2], DeW[2];
-#pragma unroll
-  for (int q = 0; q < 3; ++q) { LvW[q] = T.Lv[w][q]; DvW[q] = T.Dv[w][q]; }
-#pragma unroll
-  for (int q = 0; q < 4; ++q) { LfW[q] = T.Lf[w][q]; DfW[q] = T.Df[w][q]; }
-#pragma unroll
-  for (int q = 0; q < 2; ++q) { LeW[q] = T.Le[w][q]; DeW[q] = T.De[w][q]; }
+  const double LeW[2] = {T.Le[w][0], T.Le[w][1]}, DeW[2] = {T.De[w][0], T.De[w][1]};
 
   const int col = w * 16 + r;
   const int64_t n_own = a.own_end - a.own_begin;
   for (int64_t k = blockIdx.x; k < n_own; k += gridDim.x) {
-    const int64_t e = a.own_begin + k;
-    ElemGeo G;
-    elem_geo(a, e, G);
-    double A[3][3];
-    elem_tensor(a, e, A);
-    const double ke = a.kkind == HDD_FN_PER_ELEM ? a.kper[e] : a.kc;
-    int32_t nbr[6];
-#pragma unroll
-    for (int f = 0; f < 6; ++f) nbr[f] = a.nbrs[f * a.n_local + e];
-    int nblk = 1;
-#pragma unroll
-    for (int f = 0; f < 6; ++f) nblk += nbr[f] >= 0;
-    const int64_t rl = int64_t(NB) * nblk;
-    auto pos_of = [&](int64_t x) {
-      int p = e < x;
-#pragma unroll
-      for (int f = 0; f < 6; ++f) p += (nbr[f] >= 0 && nbr[f] < x);
-      return p;
-    };
-    double* out = a.vals + a.elem_ptr[k];
+    const cdptr R = (cdptr)(a.ws + k * HEX_REC);
+    double* out = a.vals + d2i(R[0]);
+    const int64_t hdr = d2i(R[1]);
+    const int64_t rl = int64_t(NB) * int32_t(hdr & 0xffffffff);
+    const int64_t sofs = (hdr >> 32) * NB;
+    const double M[3][3] = {{R[2], R[3], R[4]}, {R[3], R[5], R[6]}, {R[4], R[6], R[7]}};
 
-    // ---- volume: G_q = w_q |det J| kappa M,  M = J^{-1} A J^{-T} ----
-    double M[3][3];
-    {
-      double JA[3][3];
-#pragma unroll
-      for (int i = 0; i < 3; ++i)
-#pragma unroll
-        for (int j = 0; j < 3; ++j) JA[i][j] = G.Ji[i][0] * A[0][j] + G.Ji[i][1] * A[1][j] + G.Ji[i][2] * A[2][j];
-      const double gf = fabs(G.det) * ke;
-#pragma unroll
-      for (int i = 0; i < 3; ++i)
-#pragma unroll
-        for (int j = 0; j < 3; ++j)
-          M[i][j] = gf * (JA[i][0] * G.Ji[j][0] + JA[i][1] * G.Ji[j][1] + JA[i][2] * G.Ji[j][2]);
-    }
+    // ---- volume ----
     dbl4 S[4];
 #pragma unroll
     for (int I = 0; I < 4; ++I) S[I] = dbl4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int q2 = 0; q2 < 3; ++q2)
+#pragma unroll 1
+    for (int q2 = 0; q2 < 3; ++q2) {
+      const double lw = T.Lv[w][q2], dw = T.Dv[w][q2];
+      const double lI[4] = {T.Lv[0][q2], T.Lv[1][q2], T.Lv[2][q2], T.Lv[3][q2]};
+      const double dI[4] = {T.Dv[0][q2], T.Dv[1][q2], T.Dv[2][q2], T.Dv[3][q2]};
+      const double w2 = T.wv[q2];
 #pragma unroll
       for (int q1 = 0; q1 < 3; ++q1) {
-        const double wq = wvg * T.wv[q1] * T.wv[q2];
-        const double D0 = P01[0][q1] * LvW[q2], D1 = P01[1][q1] * LvW[q2], D2 = P01[2][q1] * DvW[q2];
+        const double wq = wvg * T.wv[q1] * w2;
+        const double D0 = P01[0][q1] * lw, D1 = P01[1][q1] * lw, D2 = P01[2][q1] * dw;
 #pragma unroll
         for (int ax = 0; ax < 3; ++ax) {
           const double b = wq * (M[ax][0] * D0 + M[ax][1] * D1 + M[ax][2] * D2);
 #pragma unroll
-          for (int I = 0; I < 4; ++I) {
-            const double t2 = ax == 2 ? T.Dv[I][q2] : T.Lv[I][q2];
-            S[I] = mfma(P01[ax][q1] * t2, b, S[I]);
-          }
+          for (int I = 0; I < 4; ++I) S[I] = mfma(P01[ax][q1] * (ax == 2 ? dI[I] : lI[I]), b, S[I]);
         }
       }
+    }
 
     // ---- faces ----
-#pragma unroll
+#pragma unroll 1
     for (int f = 0; f < 6; ++f) {
-      constexpr int dummy = 0;
-      (void)dummy;
-      const int32_t nf = nbr[f];
-      if (nf == HDD_NBR_NEUMANN) continue;
-      const bool inner = nf >= 0;
+      const cdptr F = R + 8 + 10 * f;
+      const int64_t fk = d2i(F[9]);
+      const int kind = int32_t(fk & 0xffffffff);
+      if (kind == HDD_NBR_NEUMANN) continue;
+      const bool inner = kind > 0;
       const int af = f >> 1, sd = f & 1;
-      const double sg = sd ? 1.0 : -1.0;
-      double n[3] = {sg * G.Ji[af][0], sg * G.Ji[af][1], sg * G.Ji[af][2]};
-      const double nn = sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
-      n[0] /= nn; n[1] /= nn; n[2] /= nn;
-      const double fvol = fabs(G.det) * nn;
-      const double hpow = pow(fvol, a.beta);
-      double An[3], cm[3];
-#pragma unroll
-      for (int i = 0; i < 3; ++i) An[i] = A[i][0] * n[0] + A[i][1] * n[1] + A[i][2] * n[2];
-#pragma unroll
-      for (int i = 0; i < 3; ++i) cm[i] = G.Ji[i][0] * An[0] + G.Ji[i][1] * An[1] + G.Ji[i][2] * An[2];
-      const double dm = n[0] * An[0] + n[1] * An[1] + n[2] * An[2];
-      double cp[3] = {0.0, 0.0, 0.0}, wm = 1.0, wp = 0.0, gam = dm, sig = a.sigma_boundary, kn = 0.0;
-      if (inner) {
-        ElemGeo Gn;
-        elem_geo(a, nf, Gn);
-        double Ao[3][3], Ano[3];
-        elem_tensor(a, nf, Ao);
-#pragma unroll
-        for (int i = 0; i < 3; ++i) Ano[i] = Ao[i][0] * n[0] + Ao[i][1] * n[1] + Ao[i][2] * n[2];
-#pragma unroll
-        for (int i = 0; i < 3; ++i) cp[i] = Gn.Ji[i][0] * Ano[0] + Gn.Ji[i][1] * Ano[1] + Gn.Ji[i][2] * Ano[2];
-        const double dp = n[0] * Ano[0] + n[1] * Ano[1] + n[2] * Ano[2];
-        gam = dp * dm / (dp + dm);
-        wp = dm / (dp + dm);
-        wm = dp / (dp + dm);
-        sig = a.sigma_inner;
-        kn = a.kkind == HDD_FN_PER_ELEM ? a.kper[nf] : a.kc;
-      }
-      const double ca = fvol * wm * ke, cb = fvol * wp * kn;
-      const double ce = fvol * sig * (inner ? ke * kn : ke) * gam / hpow;
+      const double cm[3] = {F[0], F[1], F[2]}, cp[3] = {F[3], F[4], F[5]};
+      const double ca = F[6], cb = F[7], ce = F[8];
+      const double Le0o = sd ? Le0[1] : Le0[0], De0o = sd ? De0[1] : De0[0];
+      const double Le1o = sd ? Le1[1] : Le1[0], De1o = sd ? De1[1] : De1[0];
+      const double Le0n = sd ? Le0[0] : Le0[1], De0n = sd ? De0[0] : De0[1];
+      const double Le1n = sd ? Le1[0] : Le1[1], De1n = sd ? De1[0] : De1[1];
+      const double LeWo = sd ? LeW[1] : LeW[0], DeWo = sd ? DeW[1] : DeW[0];
+      const double LeWn = sd ? LeW[0] : LeW[1], DeWn = sd ? DeW[0] : DeW[1];
       dbl4 E[4];
 #pragma unroll
       for (int I = 0; I < 4; ++I) E[I] = dbl4{0.0, 0.0, 0.0, 0.0};
-      const int so = sd, sn = 1 - sd;   // own / neighbour side of the face planes
+      // one face point row qt per iteration: k-step qt ([V] part) and k-step 4 + qt ([N] part) share every
+      // basis evaluation
+      auto face_steps = [&](auto afc) __attribute__((always_inline)) {
+        constexpr int AF = decltype(afc)::value;
+#pragma unroll 1
+        for (int qt = 0; qt < 4; ++qt) {
+          const double wq = wfg * T.wf[qt];
+          const double al = ca * wq, be = cb * wq, et = ce * wq;
+          const double lf1 = T.Lf[i1][qt], df1 = T.Df[i1][qt];
+          const double lfw = T.Lf[w][qt], dfw = T.Df[w][qt];
+          double Vo, No, Vn = 0.0, Nn = 0.0;
+          q3_face_eval<AF>(Le0o, De0o, Le1o, De1o, Lfg0, Dfg0, Lfg1, Dfg1, lf1, df1, lfw, dfw, LeWo, DeWo, cm[0],
+                           cm[1], cm[2], Vo, No);
+          if (inner)
+            q3_face_eval<AF>(Le0n, De0n, Le1n, De1n, Lfg0, Dfg0, Lfg1, Dfg1, lf1, df1, lfw, dfw, LeWn, DeWn, cp[0],
+                             cp[1], cp[2], Vn, Nn);
+          const double bEv = et * Vo - al * No, bNv = -be * Nn - et * Vn;   // [V] rows of K
+          const double bEn = -al * Vo, bNn = al * Vn;                       // [N] rows of K
+          double Va[4], Na[4];
 #pragma unroll
-      for (int s = 0; s < 8; ++s) {
-        const int qt = s & 3;
-        const bool vpart = s < 4;
-        const double wq = wfg * T.wf[qt];
-        const double al = ca * wq, be = cb * wq, et = ce * wq;
-        // column side (third index w): own and neighbour values
-        double Vo, No, Vn = 0.0, Nn = 0.0;
-        switch (af) {
-          case 0:
-            q3_face_eval<0>(Le0[so], De0[so], Le1[so], De1[so], Lfg0, Dfg0, Lfg1, Dfg1, Lf1[qt], Df1[qt], LfW[qt],
-                            DfW[qt], LeW[so], DeW[so], cm[0], cm[1], cm[2], Vo, No);
-            if (inner)
-              q3_face_eval<0>(Le0[sn], De0[sn], Le1[sn], De1[sn], Lfg0, Dfg0, Lfg1, Dfg1, Lf1[qt], Df1[qt], LfW[qt],
-                              DfW[qt], LeW[sn], DeW[sn], cp[0], cp[1], cp[2], Vn, Nn);
-            break;
-          case 1:
-            q3_face_eval<1>(Le0[so], De0[so], Le1[so], De1[so], Lfg0, Dfg0, Lfg1, Dfg1, Lf1[qt], Df1[qt], LfW[qt],
-                            DfW[qt], LeW[so], DeW[so], cm[0], cm[1], cm[2], Vo, No);
-            if (inner)
-              q3_face_eval<1>(Le0[sn], De0[sn], Le1[sn], De1[sn], Lfg0, Dfg0, Lfg1, Dfg1, Lf1[qt], Df1[qt], LfW[qt],
-                              DfW[qt], LeW[sn], DeW[sn], cp[0], cp[1], cp[2], Vn, Nn);
-            break;
-          default:
-            q3_face_eval<2>(Le0[so], De0[so], Le1[so], De1[so], Lfg0, Dfg0, Lfg1, Dfg1, Lf1[qt], Df1[qt], LfW[qt],
-                            DfW[qt], LeW[so], DeW[so], cm[0], cm[1], cm[2], Vo, No);
-            if (inner)
-              q3_face_eval<2>(Le0[sn], De0[sn], Le1[sn], De1[sn], Lfg0, Dfg0, Lfg1, Dfg1, Lf1[qt], Df1[qt], LfW[qt],
-                              DfW[qt], LeW[sn], DeW[sn], cp[0], cp[1], cp[2], Vn, Nn);
-            break;
-        }
-        const double bE = vpart ? et * Vo - al * No : -al * Vo;
-        const double bN = vpart ? -be * Nn - et * Vn : al * Vn;
+          for (int I = 0; I < 4; ++I)
+            q3_face_eval<AF>(Le0o, De0o, Le1o, De1o, Lfg0, Dfg0, Lfg1, Dfg1, lf1, df1, T.Lf[I][qt], T.Df[I][qt],
+                             T.Le[I][sd], T.De[I][sd], cm[0], cm[1], cm[2], Va[I], Na[I]);
+          // independent accumulators back to back (S[I] / E[I] reuse is 4-8 MFMAs apart)
 #pragma unroll
-        for (int I = 0; I < 4; ++I) {
-          // z faces: the V part of the row side is supported on the plane row tile I = 3 sd only
-          if (af == 2 && vpart && I != 3 * sd) continue;
-          double Va, Na;
-          const double lTf = T.Lf[I][qt], dTf = T.Df[I][qt], lTe = T.Le[I][so], dTe = T.De[I][so];
-          switch (af) {
-            case 0:
-              q3_face_eval<0>(Le0[so], De0[so], Le1[so], De1[so], Lfg0, Dfg0, Lfg1, Dfg1, Lf1[qt], Df1[qt], lTf, dTf,
-                              lTe, dTe, cm[0], cm[1], cm[2], Va, Na);
-              break;
-            case 1:
-              q3_face_eval<1>(Le0[so], De0[so], Le1[so], De1[so], Lfg0, Dfg0, Lfg1, Dfg1, Lf1[qt], Df1[qt], lTf, dTf,
-                              lTe, dTe, cm[0], cm[1], cm[2], Va, Na);
-              break;
-            default:
-              q3_face_eval<2>(Le0[so], De0[so], Le1[so], De1[so], Lfg0, Dfg0, Lfg1, Dfg1, Lf1[qt], Df1[qt], lTf, dTf,
-                              lTe, dTe, cm[0], cm[1], cm[2], Va, Na);
-              break;
+          for (int I = 0; I < 4; ++I)
+            if (AF != 2 || I == 3 * sd) S[I] = mfma(Va[I], bEv, S[I]);   // z faces: [V] rows live on tile 3 sd
+          if (inner) {
+#pragma unroll
+            for (int I = 0; I < 4; ++I)
+              if (AF != 2 || I == 3 * sd) E[I] = mfma(Va[I], bNv, E[I]);
           }
-          const double av = vpart ? Va : Na;
-          S[I] = mfma(av, bE, S[I]);
-          if (inner) E[I] = mfma(av, bN, E[I]);
+#pragma unroll
+          for (int I = 0; I < 4; ++I) S[I] = mfma(Na[I], bEn, S[I]);
+          if (inner) {
+#pragma unroll
+            for (int I = 0; I < 4; ++I) E[I] = mfma(Na[I], bNn, E[I]);
+          }
         }
-      }
+      };
+      if (af == 0) face_steps(std::integral_constant<int, 0>{});
+      else if (af == 1) face_steps(std::integral_constant<int, 1>{});
+      else face_steps(std::integral_constant<int, 2>{});
       if (inner) {
-        const int64_t cofs = int64_t(pos_of(nf)) * NB;
+        const int64_t cofs = (fk >> 32) * NB;
 #pragma unroll
         for (int I = 0; I < 4; ++I)
 #pragma unroll
           for (int rr = 0; rr < 4; ++rr) out[(I * 16 + g + 4 * rr) * rl + cofs + col] = E[I][rr];
       }
     }
-    const int64_t sofs = int64_t(pos_of(e)) * NB;
 #pragma unroll
     for (int I = 0; I < 4; ++I)
 #pragma unroll
@@ -655,9 +654,21 @@ static hipError_t launch_hex_q3(const HexArgs& a, hipStream_t s)
 {
   const int64_t n_own = a.own_end - a.own_begin;
   if (n_own <= 0) return hipSuccess;
+  hipLaunchKernelGGL(hex_q3_setup_kernel, dim3(unsigned((n_own + 255) / 256)), dim3(256), 0, s, a);
   const int64_t grid = std::min<int64_t>(n_own, 1 << 20);
   hipLaunchKernelGGL(hex_q3_kernel, dim3(unsigned(grid)), dim3(256), 0, s, a);
   return hipGetLastError();
+}
+
+static bool hex_generic_forced()
+{
+  static const bool generic = getenv("HDD_HEX_GENERIC") != nullptr;   // A/B against the LDS-table kernel
+  return generic;
+}
+
+bool hex_uses_records(const HexArgs& a, int degree, int nq1v, int nq1f)
+{
+  return degree == 3 && nq1v == 3 && nq1f == 4 && a.kkind != HDD_FN_SINUSOID && !hex_generic_forced();
 }
 
 template <int P, int SM>
@@ -679,8 +690,10 @@ hipError_t launch_hex(const HexArgs& a, int degree, int nq1v, int nq1f, hipStrea
     *supported = false;
     return hipSuccess;
   }
-  static const bool generic = getenv("HDD_HEX_GENERIC") != nullptr;   // A/B against the LDS-table kernel
-  if (degree == 3 && sm == 0 && a.kkind != HDD_FN_SINUSOID && !generic) return launch_hex_q3(a, s);
+  if (hex_uses_records(a, degree, nq1v, nq1f)) {
+    if (!a.ws) return hipErrorInvalidValue;
+    return launch_hex_q3(a, s);
+  }
   switch (degree * 2 + sm) {
     case 2: return launch_hex_t<1, 0>(a, s);
     case 3: return launch_hex_t<1, 1>(a, s);

@@ -57,8 +57,12 @@ struct HexArgs {
   const double* kper;
   double* vals;
   double sigma_inner, sigma_boundary, beta;
+  double* ws;                   // p=3 register kernel: per-element coefficient records [n_own][HEX_REC]
   HexTables tab;
 };
+
+constexpr int HEX_REC = 72;     // doubles per element record (see hex_qp.hip)
+bool hex_uses_records(const HexArgs& a, int degree, int nq1v, int nq1f);
 
 // degree p in 1..3; (nq1v, nq1f) Gauss points per direction; *supported = false if no kernel matches
 hipError_t launch_hex(const HexArgs& a, int degree, int nq1v, int nq1f, hipStream_t s, bool* supported);

@@ -9,8 +9,10 @@
  *     hdd_last_error(NULL) for functions without a context) returns the message of the last failure
  *     of the calling thread;
  *   - device work is enqueued on the hipStream_t passed as `stream` (NULL = legacy default stream) and
- *     is NOT synchronised; no allocation or synchronisation happens inside hdd_swipdg_assemble /
- *     hdd_affine_lincomb / hdd_soa_gather / hdd_soa_scatter, so they are hipGraph-capturable;
+ *     is NOT synchronised; no synchronisation happens inside hdd_swipdg_assemble / hdd_affine_lincomb /
+ *     hdd_soa_gather / hdd_soa_scatter, and no allocation either except that hdd_swipdg_assemble on
+ *     HDD_HEX p=3 meshes grows a context-owned workspace (576 B per owned element) the first time a
+ *     context sees a larger mesh: warm a context up once, then the calls are hipGraph-capturable;
  *   - one context per thread at a time (thread-compatible, like the reference's single-threaded init()).
  *
  * Numbering: DoF (row / column) of local basis function i of element g is g*nb + i (element-blocked,
