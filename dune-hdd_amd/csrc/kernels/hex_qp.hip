@@ -537,11 +537,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const double Lfg0 = T.Lf[i0][g], Dfg0 = T.Df[i0][g], Lfg1 = T.Lf[i1][g], Dfg1 = T.Df[i1][g], wfg = T.wf[g];
   const double Le0[2] = {T.Le[i0][0], T.Le[i0][1]}, De0[2] = {T.De[i0][0], T.De[i0][1]};
   const double Le1[2] = {T.Le[i1][0], T.Le[i1][1]}, De1[2] = {T.De[i1][0], T.De[i1][1]};
-  const double LeW[2] = {T.Le[w][0], T.Le[w][1]}, DeW[2] = {T.De[w][0], T.De[w][1]};
 
-  const int col = w * 16 + r;
   const int64_t n_own = a.own_end - a.own_begin;
   for (int64_t k = blockIdx.x; k < n_own; k += gridDim.x) {
+    // column tile of this wave, rotated per element: the z-face skips below then even out over the SIMDs
+    const int wc = (w + int(k)) & 3;
+    const double LeW[2] = {T.Le[wc][0], T.Le[wc][1]}, DeW[2] = {T.De[wc][0], T.De[wc][1]};
+    const int col = wc * 16 + r;
     const cdptr R = (cdptr)(a.ws + k * HEX_REC);
     double* out = a.vals + d2i(R[0]);
     const int64_t hdr = d2i(R[1]);
@@ -555,7 +557,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     for (int I = 0; I < 4; ++I) S[I] = dbl4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll 1
     for (int q2 = 0; q2 < 3; ++q2) {
-      const double lw = T.Lv[w][q2], dw = T.Dv[w][q2];
+      const double lw = T.Lv[wc][q2], dw = T.Dv[wc][q2];
       const double lI[4] = {T.Lv[0][q2], T.Lv[1][q2], T.Lv[2][q2], T.Lv[3][q2]};
       const double dI[4] = {T.Dv[0][q2], T.Dv[1][q2], T.Dv[2][q2], T.Dv[3][q2]};
       const double w2 = T.wv[q2];
@@ -601,7 +603,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
           const double wq = wfg * T.wf[qt];
           const double al = ca * wq, be = cb * wq, et = ce * wq;
           const double lf1 = T.Lf[i1][qt], df1 = T.Df[i1][qt];
-          const double lfw = T.Lf[w][qt], dfw = T.Df[w][qt];
+          const double lfw = T.Lf[wc][qt], dfw = T.Df[wc][qt];
           double Vo, No, Vn = 0.0, Nn = 0.0;
           q3_face_eval<AF>(Le0o, De0o, Le1o, De1o, Lfg0, Dfg0, Lfg1, Dfg1, lf1, df1, lfw, dfw, LeWo, DeWo, cm[0],
                            cm[1], cm[2], Vo, No);
@@ -624,9 +626,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             for (int I = 0; I < 4; ++I)
               if (AF != 2 || I == 3 * sd) E[I] = mfma(Va[I], bNv, E[I]);
           }
+          // [N] rows of K: B = -alpha V- / alpha V+ at the columns; on z faces V vanishes off the face plane,
+          // i.e. outside column tile 3 sd (own side) / 3 (1 - sd) (neighbour side): wave-uniform skips
+          if (AF != 2 || wc == 3 * sd) {
 #pragma unroll
-          for (int I = 0; I < 4; ++I) S[I] = mfma(Na[I], bEn, S[I]);
-          if (inner) {
+            for (int I = 0; I < 4; ++I) S[I] = mfma(Na[I], bEn, S[I]);
+          }
+          if (inner && (AF != 2 || wc == 3 * (1 - sd))) {
 #pragma unroll
             for (int I = 0; I < 4; ++I) E[I] = mfma(Na[I], bNn, E[I]);
           }
