@@ -68,7 +68,10 @@ extern "C" void hdd_ctx_destroy(hdd_ctx* ctx)
   delete ctx;
 }
 
-static int fn_order(const hdd_scalar_fn& f) { return f.kind == HDD_FN_SINUSOID ? f.order : 0; }
+static int fn_order(const hdd_scalar_fn& f)
+{
+  return (f.kind == HDD_FN_SINUSOID || f.kind == HDD_FN_COS_PRODUCT) ? f.order : 0;
+}
 
 // ---------------------------------------------------------------------------------------------------
 // HDD_HEX: Q_p on affine hexahedra (hex_qp.hip)
@@ -557,4 +560,143 @@ extern "C" int hdd_pattern_fill_device(hdd_ctx* ctx, const hdd_mesh* m, int32_t 
   e = hdd::dev::launch_pattern_fill(m->neighbors, nf, nb, m->n_local, m->own_begin, m->own_end, d_global_id,
                                     d_elem_ptr, d_row_ptr, d_col, static_cast<hipStream_t>(stream));
   return e == hipSuccess ? HDD_OK : hip_fail(e, "hdd_pattern_fill_device: launch");
+}
+
+// ------------------------------------------------------------------------------------------------
+// right-hand side (rhs.hip): host-side quadrature rules
+// ------------------------------------------------------------------------------------------------
+namespace {
+// simplex rules on the reference triangle (area 1/2): centroid (order <= 1), 3-point interior (2),
+// Dunavant 6-point (3..4), collapsed Gauss-Legendre (Duffy) beyond
+int simplex_rule(int order, double (*q)[4], int cap)
+{
+  if (order <= 1) {
+    q[0][0] = q[0][1] = 1.0 / 3.0; q[0][2] = 0.0; q[0][3] = 0.5;
+    return 1;
+  }
+  if (order == 2) {
+    const double a = 1.0 / 6.0, b = 2.0 / 3.0;
+    const double P[3][2] = {{a, a}, {b, a}, {a, b}};
+    for (int k = 0; k < 3; ++k) { q[k][0] = P[k][0]; q[k][1] = P[k][1]; q[k][2] = 0.0; q[k][3] = 1.0 / 6.0; }
+    return 3;
+  }
+  if (order <= 4) {
+    const double a = 0.44594849091596488632, wa = 0.22338158967801146570;
+    const double b = 0.091576213509770743460, wb = 0.10995174365532186764;
+    const double P[6][3] = {{a, a, wa}, {1 - 2 * a, a, wa}, {a, 1 - 2 * a, wa},
+                            {b, b, wb}, {1 - 2 * b, b, wb}, {b, 1 - 2 * b, wb}};
+    for (int k = 0; k < 6; ++k) { q[k][0] = P[k][0]; q[k][1] = P[k][1]; q[k][2] = 0.0; q[k][3] = 0.5 * P[k][2]; }
+    return 6;
+  }
+  const int n = (order + 3) / 2;
+  if (n * n > cap) return -1;
+  double s[16], w[16];
+  gauss_legendre01(n, s, w);
+  int k = 0;
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j, ++k) {
+      q[k][0] = s[i]; q[k][1] = s[j] * (1.0 - s[i]); q[k][2] = 0.0; q[k][3] = w[i] * w[j] * (1.0 - s[i]);
+    }
+  return n * n;
+}
+
+int tensor_rule(int dim, int order, double (*q)[4], int cap)
+{
+  const int n = std::max(1, (order + 2) / 2);
+  int tot = 1;
+  for (int a = 0; a < dim; ++a) tot *= n;
+  if (tot > cap || n > 16) return -1;
+  double s[16], w[16];
+  gauss_legendre01(n, s, w);
+  for (int m = 0; m < tot; ++m) {
+    int r = m;
+    q[m][0] = q[m][1] = q[m][2] = 0.0;
+    q[m][3] = 1.0;
+    for (int a = 0; a < dim; ++a) {
+      q[m][a] = s[r % n];
+      q[m][3] *= w[r % n];
+      r /= n;
+    }
+  }
+  return tot;
+}
+
+int face_rule(int fdim, int order, double (*q)[3], int cap)
+{
+  double t[64][4];
+  const int nq = tensor_rule(fdim, order, t, std::min(cap, 64));
+  for (int k = 0; k < nq; ++k) { q[k][0] = t[k][0]; q[k][1] = t[k][1]; q[k][2] = t[k][3]; }
+  return nq;
+}
+
+hdd::dev::KappaArg kap_arg(const hdd_scalar_fn* f)
+{
+  if (!f) return hdd::dev::KappaArg{HDD_FN_CONST, 0, 0.0, 0.0, 0.0, 0.0, nullptr};
+  return hdd::dev::KappaArg{f->kind, f->order, f->c, f->b, f->kx, f->ky, f->per_elem};
+}
+}  // namespace
+
+extern "C" int hdd_swipdg_rhs(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_fn* force, const hdd_scalar_fn* kappa,
+                              const hdd_tensor_fn* tensor, const hdd_scalar_fn* dirichlet,
+                              const hdd_scalar_fn* neumann, const hdd_swipdg_params* p, double* d_rhs, void* stream)
+{
+  using namespace hdd::dev;
+  if (!ctx || !m || !p || !d_rhs) return set_error(HDD_ERR_INVALID, "hdd_swipdg_rhs: null argument");
+  if (m->elem_type != HDD_SIMPLEX && m->elem_type != HDD_CUBE && m->elem_type != HDD_HEX)
+    return set_error(HDD_ERR_UNSUPPORTED, "hdd_swipdg_rhs: unknown element type");
+  if (!m->coords || !m->neighbors) return set_error(HDD_ERR_INVALID, "hdd_swipdg_rhs: mesh arrays missing");
+  if (m->own_begin < 0 || m->own_end > m->n_local || m->own_begin > m->own_end)
+    return set_error(HDD_ERR_RANGE, "hdd_swipdg_rhs: 0 <= own_begin <= own_end <= n_local violated");
+  if (dirichlet && (!kappa || !tensor))
+    return set_error(HDD_ERR_INVALID, "hdd_swipdg_rhs: the Dirichlet functional needs kappa and the tensor");
+  for (const hdd_scalar_fn* f : {force, kappa, dirichlet, neumann})
+    if (f && f->kind == HDD_FN_PER_ELEM && !f->per_elem)
+      return set_error(HDD_ERR_INVALID, "hdd_swipdg_rhs: per_elem function without values");
+  if (tensor && tensor->kind != HDD_TENSOR_CONST && !tensor->per_elem)
+    return set_error(HDD_ERR_INVALID, "hdd_swipdg_rhs: tensor per_elem missing");
+  const int deg = m->elem_type == HDD_HEX ? std::max(1, int(m->degree)) : 1;
+  if (m->elem_type != HDD_HEX && m->degree > 1)
+    return set_error(HDD_ERR_UNSUPPORTED, "hdd_swipdg_rhs: 2d meshes carry P1 / Q1 only");
+  if (deg > 3) return set_error(HDD_ERR_UNSUPPORTED, "hdd_swipdg_rhs: HDD_HEX supports p = 1..3");
+  const int dim = m->elem_type == HDD_HEX ? 3 : 2;
+  RhsArgs a{};
+  a.elem_type = m->elem_type;
+  a.degree = deg;
+  a.nb = m->elem_type == HDD_SIMPLEX ? 3 : (m->elem_type == HDD_CUBE ? 4 : (deg + 1) * (deg + 1) * (deg + 1));
+  a.n_local = m->n_local;
+  a.own_begin = m->own_begin;
+  a.own_end = m->own_end;
+  a.coords = m->coords;
+  a.nbrs = m->neighbors;
+  a.tkind = tensor ? tensor->kind : HDD_TENSOR_CONST;
+  for (int r = 0; r < 6; ++r) a.tc[r] = tensor ? tensor->c[r] : 0.0;
+  a.tper = tensor ? tensor->per_elem : nullptr;
+  a.force = kap_arg(force);
+  a.kappa = kap_arg(kappa);
+  a.dirichlet = kap_arg(dirichlet);
+  a.neumann = kap_arg(neumann);
+  a.has_force = force != nullptr;
+  a.has_dirichlet = dirichlet != nullptr;
+  a.has_neumann = neumann != nullptr;
+  a.sigma_boundary = p->sigma_boundary;
+  a.beta = p->beta;
+  a.out = d_rhs;
+  if (force) {
+    const int order = fn_order(*force) + deg;
+    a.nqv = m->elem_type == HDD_SIMPLEX ? simplex_rule(order, a.qv, 64) : tensor_rule(dim, order, a.qv, 64);
+    if (a.nqv < 0) return set_error(HDD_ERR_UNSUPPORTED, "hdd_swipdg_rhs: force integration order too high");
+  }
+  if (dirichlet) {
+    const int order = std::max(fn_order(*dirichlet) + deg, fn_order(*kappa) + 0 + (deg - 1) + fn_order(*dirichlet));
+    a.nqd = face_rule(dim - 1, order, a.qd, 16);
+    if (a.nqd < 0) return set_error(HDD_ERR_UNSUPPORTED, "hdd_swipdg_rhs: Dirichlet integration order too high");
+  }
+  if (neumann) {
+    a.nqn = face_rule(dim - 1, fn_order(*neumann) + deg, a.qn, 16);
+    if (a.nqn < 0) return set_error(HDD_ERR_UNSUPPORTED, "hdd_swipdg_rhs: Neumann integration order too high");
+  }
+  hipError_t e = hipSetDevice(ctx->device);
+  if (e != hipSuccess) return hip_fail(e, "hdd_swipdg_rhs: hipSetDevice");
+  e = launch_rhs(a, static_cast<hipStream_t>(stream));
+  return e == hipSuccess ? HDD_OK : hip_fail(e, "hdd_swipdg_rhs: launch");
 }

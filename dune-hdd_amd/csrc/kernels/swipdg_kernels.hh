@@ -74,6 +74,25 @@ hipError_t launch_pattern_fill(const int32_t* nbrs, int32_t nf, int32_t nb, int6
                                int64_t own_end, const int64_t* gid, const int64_t* elem_ptr, int64_t* row_ptr,
                                int32_t* col, hipStream_t s);
 
+// right-hand side functionals (rhs.hip)
+struct RhsArgs {
+  int32_t elem_type, degree, nb, tkind;
+  int64_t n_local, own_begin, own_end;
+  const double* coords;
+  const int32_t* nbrs;
+  double tc[6];
+  const double* tper;
+  KappaArg force, kappa, dirichlet, neumann;
+  int32_t has_force, has_dirichlet, has_neumann, pad;
+  double sigma_boundary, beta;
+  int32_t nqv, nqd, nqn, pad2;
+  double qv[64][4];    // volume rule: reference point (3) + weight
+  double qd[16][3];    // Dirichlet face rule: face parameters (2) + weight
+  double qn[16][3];    // Neumann face rule
+  double* out;         // [nb * n_own]
+};
+hipError_t launch_rhs(const RhsArgs& a, hipStream_t s);
+
 int volume_points(int elem_type, int order);
 int face_points(int order);
 hipError_t launch_assemble(const AssembleArgs& a, int nqv, int nqf, hipStream_t s, bool* supported);

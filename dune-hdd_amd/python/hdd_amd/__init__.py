@@ -17,7 +17,7 @@ HEADER = os.path.abspath(os.path.join(ROOT, "..", "include", "hdd.h"))
 
 SIMPLEX, CUBE, HEX = 0, 1, 2
 NBR_DIRICHLET, NBR_NEUMANN = -1, -2
-FN_CONST, FN_PER_ELEM, FN_SINUSOID = 0, 1, 2
+FN_CONST, FN_PER_ELEM, FN_SINUSOID, FN_COS_PRODUCT = 0, 1, 2, 3
 TENSOR_CONST, TENSOR_ISO_PER_ELEM, TENSOR_SYM_PER_ELEM = 0, 1, 2
 BOUNDARY_ALL_DIRICHLET, BOUNDARY_ALL_NEUMANN = 0, 1
 MAX_COMP = 8
@@ -138,6 +138,7 @@ def lib():
         "hdd_swipdg_assemble_tiles": (_I32, [_VP, C.POINTER(MeshT), C.POINTER(ScalarFn), _I32, C.POINTER(TensorFn),
                                              C.POINTER(Params), C.POINTER(CsrT), _VP, _VP, _I64, _VP]),
         "hdd_affine_lincomb": (_I32, [_VP, _I64, _VP, _I32, _VP, _I32, _VP, _I64, _VP]),
+        "hdd_swipdg_rhs": (_I32, [_VP, C.POINTER(MeshT), _VP, _VP, _VP, _VP, _VP, C.POINTER(Params), _VP, _VP]),
         "hdd_block_operator_map": (_I32, [_VP, _I32, _I32, _VP, _VP, _VP, _VP, _VP, C.POINTER(_I64)]),
         "hdd_gather_values": (_I32, [_VP, _VP, _VP, _I64, _VP, _VP]),
         "hdd_soa_gather": (_I32, [_VP, _VP, _VP, _I32, _I64, _VP, _I64, _VP, _VP]),
@@ -480,6 +481,29 @@ def halo_tiles(local):
     padded[:local.n_own] = ghost
     bt = padded.reshape(n_tiles, 64).any(axis=1)
     return np.nonzero(~bt)[0].astype(np.int32), np.nonzero(bt)[0].astype(np.int32)
+
+
+def esv2007_force(dim=2):
+    """ESV2007 Testcase1Force (problems/ESV2007.hh:78, integration order 3): 1/2 pi^2 cos(pi x/2) cos(pi y/2);
+    in 3d (C5) (3/4) pi^2 prod cos(pi x_a / 2)."""
+    k = 0.5 * np.pi
+    return scalar_fn(FN_COS_PRODUCT, 0.25 * dim * np.pi ** 2, b=k if dim == 3 else 0.0, kx=k, ky=k, order=3)
+
+
+def rhs(ctx, dmesh, force=None, kappa=None, tensor=None, dirichlet=None, neumann=None, prm=None, out=None,
+        stream=None):
+    """hdd_swipdg_rhs: L2Volume(force) + DirichletBoundarySWIPDG(kappa, tensor, dirichlet) + L2Face(neumann)
+    (swipdg.hh:251-347) into a device vector [nb * n_own]."""
+    torch = _torch()
+    local = dmesh.local
+    if out is None:
+        out = torch.empty(local.nb * local.n_own, dtype=torch.float64, device=dmesh.coords.device)
+    ref = lambda x: None if x is None else C.cast(C.byref(x), C.c_void_p)
+    prm = prm or params_for(local.degree, local.dim)
+    s = stream if stream is not None else torch.cuda.current_stream(dmesh.coords.device).cuda_stream
+    _check(lib().hdd_swipdg_rhs(ctx.h, C.byref(dmesh.t), ref(force), ref(kappa), ref(tensor), ref(dirichlet),
+                                ref(neumann), C.byref(prm), out.data_ptr(), C.c_void_p(s)), "hdd_swipdg_rhs")
+    return out
 
 
 def affine_lincomb(ctx, comps, theta, out=None, stream=None):

@@ -46,7 +46,7 @@ typedef enum {
 enum { HDD_SIMPLEX = 0, HDD_CUBE = 1,                       /* P1 triangles / Q1 parallelograms (2d) */
        HDD_HEX = 2 };                                        /* Q_p (p = 1..3) on affine hexahedra (3d) */
 enum { HDD_NBR_DIRICHLET = -1, HDD_NBR_NEUMANN = -2 };       /* neighbour codes of domain-boundary faces */
-enum { HDD_FN_CONST = 0, HDD_FN_PER_ELEM = 1, HDD_FN_SINUSOID = 2 };
+enum { HDD_FN_CONST = 0, HDD_FN_PER_ELEM = 1, HDD_FN_SINUSOID = 2, HDD_FN_COS_PRODUCT = 3 };
 enum { HDD_TENSOR_CONST = 0, HDD_TENSOR_ISO_PER_ELEM = 1, HDD_TENSOR_SYM_PER_ELEM = 2 };
 enum { HDD_BOUNDARY_ALL_DIRICHLET = 0, HDD_BOUNDARY_ALL_NEUMANN = 1 };
 
@@ -186,7 +186,9 @@ typedef struct {              /* one diffusion-factor component kappa_q (a Stuff
   int32_t kind;               /* HDD_FN_* */
   int32_t order;              /* integration order of the function (Expression: integration_order) */
   double c;                   /* CONST value, SINUSOID offset a */
-  double b, kx, ky;           /* SINUSOID: a + b*sin(kx*x + ky*y) */
+  double b, kx, ky;           /* SINUSOID: a + b*sin(kx*x + ky*y);
+                                 COS_PRODUCT: a*cos(kx*x)*cos(ky*y) [*cos(b*z) in 3d when b != 0]
+                                 (ESV2007 Testcase1Force, problems/ESV2007.hh:78) -- right-hand sides */
   const double* per_elem;     /* PER_ELEM: device [n_local] */
 } hdd_scalar_fn;
 
@@ -234,6 +236,17 @@ int hdd_swipdg_assemble(hdd_ctx* ctx, const hdd_mesh* mesh, const hdd_scalar_fn*
 int hdd_swipdg_assemble_tiles(hdd_ctx* ctx, const hdd_mesh* mesh, const hdd_scalar_fn* kappa, int32_t n_comp,
                               const hdd_tensor_fn* tensor, const hdd_swipdg_params* params, const hdd_csr* pattern,
                               double* const* d_vals, const int32_t* d_tiles, int64_t n_tiles, void* stream);
+
+/* SWIPDG right-hand side -- replaces the functionals of SWIPDG::init() (swipdg.hh:251-347):
+ *   L2Volume(force) + DirichletBoundarySWIPDG(kappa, tensor, dirichlet) on Dirichlet faces
+ *   + L2Face(neumann) on Neumann faces, each of force / dirichlet / neumann nullable (absent = zero).
+ * Writes d_rhs[k*nb + i] for every owned element k (local order) and basis function i; one call per
+ * affine component of the right-hand side (the caller pairs kappa / dirichlet components as swipdg.hh
+ * does).  Integration orders: ord(f) + p; Neumann ord(g_N) + p; Dirichlet max(ord(g_D) + p,
+ * ord(kappa) + ord(A) + p - 1 + ord(g_D)). */
+int hdd_swipdg_rhs(hdd_ctx* ctx, const hdd_mesh* mesh, const hdd_scalar_fn* force, const hdd_scalar_fn* kappa,
+                   const hdd_tensor_fn* tensor, const hdd_scalar_fn* dirichlet, const hdd_scalar_fn* neumann,
+                   const hdd_swipdg_params* params, double* d_rhs, void* stream);
 
 /* theta-lincomb of affine components on a shared pattern -- replaces
  * AffinelyDecomposedContainer::freeze_parameter(mu) as used by ContainerBasedDefault::uncached_solve

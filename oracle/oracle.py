@@ -355,3 +355,44 @@ def qp_esv2007_errors(grid, elem_index=None):
     l2, h1 = C.c_double(), C.c_double()
     _qp_lib().or_qp_error_esv2007(C.byref(grid.t), _ptr(u), _ptr(ei), 2 * grid.p + 6, C.byref(l2), C.byref(h1))
     return l2.value, h1.value
+
+
+# ------------------------------------------------------------------------------------------------------
+# right-hand sides (SWIPDG::init() functionals, swipdg.hh:251-347)
+# ------------------------------------------------------------------------------------------------------
+FN_COS_PRODUCT = 3
+
+
+def esv2007_force(dim=2):
+    """Testcase1Force (problems/ESV2007.hh:78), integration order 3; 3d: (d pi^2 / 4) prod cos(pi x_a / 2)."""
+    k = 0.5 * np.pi
+    return scalar(FN_COS_PRODUCT, 0.25 * dim * np.pi ** 2, k if dim == 3 else 0.0, k, k, order=3)
+
+
+def rhs_swipdg(grid, force=None, kappa=None, A=None, dirichlet=None, neumann=None, prm=None, elem_index=None):
+    L = lib()
+    L.or_rhs_swipdg.argtypes = [C.c_void_p] + [C.c_void_p] * 5 + [C.c_void_p, C.c_void_p, C.c_void_p]
+    b = np.empty(grid.ne * grid.nb, np.float64)
+    ei = None if elem_index is None else np.ascontiguousarray(elem_index, np.int64)
+    kappa = kappa or scalar()
+    A = A or tensor()
+    prm = prm or params()
+    ref = lambda x: None if x is None else C.cast(C.byref(x), C.c_void_p)
+    L.or_rhs_swipdg(grid.h, ref(force), ref(kappa), ref(A), ref(dirichlet), ref(neumann), ref(prm), _ptr(ei),
+                    _ptr(b))
+    return b
+
+
+def qp_rhs_swipdg(grid, force=None, kappa=None, A=None, dirichlet=None, neumann=None, prm=None, elem_index=None):
+    L = _qp_lib()
+    L.or_qp_rhs_swipdg.restype = C.c_int
+    L.or_qp_rhs_swipdg.argtypes = [C.c_void_p] * 9
+    b = np.empty(grid.ne * grid.nb, np.float64)
+    ei = None if elem_index is None else np.ascontiguousarray(elem_index, np.int64)
+    kappa = kappa or scalar()
+    A = A or qp_tensor(dim=grid.dim)
+    prm = prm or qp_params(grid)
+    ref = lambda x: None if x is None else C.cast(C.byref(x), C.c_void_p)
+    L.or_qp_rhs_swipdg(C.cast(C.byref(grid.t), C.c_void_p), ref(force), ref(kappa), ref(A), ref(dirichlet),
+                       ref(neumann), ref(prm), _ptr(ei), _ptr(b))
+    return b

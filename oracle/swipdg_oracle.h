@@ -12,7 +12,7 @@ extern "C" {
 #endif
 
 enum { OR_SIMPLEX = 0, OR_CUBE = 1 };
-enum { OR_FN_CONST = 0, OR_FN_PER_ELEM = 1, OR_FN_SINUSOID = 2 };
+enum { OR_FN_CONST = 0, OR_FN_PER_ELEM = 1, OR_FN_SINUSOID = 2, OR_FN_COS_PRODUCT = 3 };
 enum { OR_TENSOR_CONST = 0, OR_TENSOR_ISO_PER_ELEM = 1, OR_TENSOR_SYM_PER_ELEM = 2 };
 enum { OR_BOUNDARY_DIRICHLET = 0, OR_BOUNDARY_NEUMANN = 1 };
 
@@ -29,7 +29,7 @@ typedef struct {
   int32_t kind;               /* OR_FN_* */
   int32_t order;              /* integration order attributed to the function (expression functions) */
   double c;                   /* constant value / sinusoid offset a */
-  double b, kx, ky;           /* sinusoid: a + b*sin(kx*x + ky*y) */
+  double b, kx, ky;           /* sinusoid: a + b*sin(kx*x + ky*y); cos product: a*cos(kx*x)*cos(ky*y)[*cos(b*z)] */
   const double* per_elem;     /* OR_FN_PER_ELEM: [n_elements] */
 } or_scalar_t;
 
@@ -65,6 +65,11 @@ int or_assemble_block_swipdg(void* g, const int32_t* subdomain, int32_t n_sub, c
                              const or_tensor_t* A, const or_params_t* p, const int64_t* elem_index,
                              const int64_t* row_ptr, const int32_t* col, double* val);
 int or_rhs_l2(void* g, int force_kind, int force_order, const int64_t* elem_index, double* b);
+/* SWIPDG right-hand side (swipdg.hh:251-347): L2Volume(force) + DirichletBoundarySWIPDG(kappa, A, g_D) on
+ * Dirichlet faces + L2Face(g_N) on Neumann faces; any of force / dirichlet / neumann may be NULL */
+int or_rhs_swipdg(void* g, const or_scalar_t* force, const or_scalar_t* kappa, const or_tensor_t* A,
+                  const or_scalar_t* dirichlet, const or_scalar_t* neumann, const or_params_t* p,
+                  const int64_t* elem_index, double* b);
 int or_error_norms_esv2007(void* g, const double* u, const int64_t* elem_index, int order, double* l2, double* h1);
 
 #ifdef __cplusplus

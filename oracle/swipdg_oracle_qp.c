@@ -223,6 +223,8 @@ static double eval_scalar(const or_qp_scalar_t* s, int64_t e, const double* x)
     case OR_QP_FN_CONST: return s->c;
     case OR_QP_FN_PER_ELEM: return s->per_elem[e];
     case OR_QP_FN_SINUSOID: return s->c + s->b * sin(s->kx * x[0] + s->ky * x[1]);
+    case OR_QP_FN_COS_PRODUCT:   /* z factor only for b != 0 (3d data); 2d callers leave b = 0 */
+      return s->c * cos(s->kx * x[0]) * cos(s->ky * x[1]) * (s->b != 0.0 ? cos(s->b * x[2]) : 1.0);
     default: return 0.0;
   }
 }
@@ -246,7 +248,10 @@ static void eval_tensor(const qgrid_t* g, const or_qp_tensor_t* t, int64_t e, do
   }
 }
 
-static int scalar_order(const or_qp_scalar_t* s) { return s->kind == OR_QP_FN_SINUSOID ? s->order : 0; }
+static int scalar_order(const or_qp_scalar_t* s)
+{
+  return (s->kind == OR_QP_FN_SINUSOID || s->kind == OR_QP_FN_COS_PRODUCT) ? s->order : 0;
+}
 
 static inline int64_t gid_of(const int64_t* elem_index, int64_t e) { return elem_index ? elem_index[e] : e; }
 
@@ -545,6 +550,70 @@ int or_qp_assemble(const or_qp_grid_t* in, const or_qp_scalar_t* kappa, const or
     }
   }
   free(buf);
+  free(q);
+  return 0;
+}
+
+/* SWIPDG right-hand side (see or_rhs_swipdg in swipdg_oracle.c for the functionals and orders) */
+int or_qp_rhs_swipdg(const or_qp_grid_t* in, const or_qp_scalar_t* force, const or_qp_scalar_t* kappa,
+                     const or_qp_tensor_t* A, const or_qp_scalar_t* dirichlet, const or_qp_scalar_t* neumann,
+                     const or_qp_params_t* prm, const int64_t* elem_index, double* b)
+{
+  qgrid_t g;
+  if (init_grid(in, &g)) return -1;
+  const int nb = g.nb, d = g.dim;
+  qrule_t* q = (qrule_t*)malloc(sizeof(qrule_t));
+  memset(b, 0, sizeof(double) * (size_t)(g.ne * nb));
+  double phi[125], gh[125][3], gp[3];
+  for (int64_t e = 0; e < g.ne; ++e) {
+    geo_t G;
+    geometry(&g, e, &G);
+    double* be = b + gid_of(elem_index, e) * nb;
+    if (force) {
+      tensor_rule(d, scalar_order(force) + g.p, q);
+      for (int k = 0; k < q->n; ++k) {
+        double x[3];
+        shape(&g, q->x[k], phi, gh);
+        global_pt(&G, q->x[k], x);
+        const double fv = eval_scalar(force, e, x) * q->w[k] * fabs(G.det);
+        for (int i = 0; i < nb; ++i) be[i] += fv * phi[i];
+      }
+    }
+    for (int f = 0; f < g.nf; ++f) {
+      if (neighbour(&g, e, f) >= 0) continue;
+      const int dir = prm->boundary_kind == OR_QP_BOUNDARY_DIRICHLET;
+      const or_qp_scalar_t* data = dir ? dirichlet : neumann;
+      if (!data) continue;
+      double n[3], fvol, Am[3][3], An[3];
+      face_normal(&G, f, n, &fvol);
+      eval_tensor(&g, A, e, Am);
+      matvec(d, Am, n, An);
+      const double gamma = dot(d, n, An), hpow = pow(fvol, prm->beta);
+      int order = scalar_order(data) + g.p;
+      if (dir) {
+        const int o2 = scalar_order(kappa) + 0 + (g.p - 1) + scalar_order(data);
+        if (o2 > order) order = o2;
+      }
+      tensor_rule(d - 1, order, q);
+      for (int k = 0; k < q->n; ++k) {
+        double xin[3], x[3];
+        face_ref_point(d, f, q->x[k], xin);
+        global_pt(&G, xin, x);
+        shape(&g, xin, phi, gh);
+        const double gv = eval_scalar(data, e, x) * q->w[k] * fvol;
+        if (dir) {
+          const double kap = eval_scalar(kappa, e, x);
+          const double pen = prm->sigma_boundary * kap * gamma / hpow;
+          for (int i = 0; i < nb; ++i) {
+            map_grad(&G, gh[i], gp);
+            be[i] += gv * (-kap * dot(d, An, gp) + pen * phi[i]);
+          }
+        } else {
+          for (int i = 0; i < nb; ++i) be[i] += gv * phi[i];
+        }
+      }
+    }
+  }
   free(q);
   return 0;
 }

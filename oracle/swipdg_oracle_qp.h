@@ -11,7 +11,7 @@
 extern "C" {
 #endif
 
-enum { OR_QP_FN_CONST = 0, OR_QP_FN_PER_ELEM = 1, OR_QP_FN_SINUSOID = 2 };
+enum { OR_QP_FN_CONST = 0, OR_QP_FN_PER_ELEM = 1, OR_QP_FN_SINUSOID = 2, OR_QP_FN_COS_PRODUCT = 3 };
 enum { OR_QP_TENSOR_CONST = 0, OR_QP_TENSOR_ISO_PER_ELEM = 1, OR_QP_TENSOR_SYM_PER_ELEM = 2 };
 enum { OR_QP_BOUNDARY_DIRICHLET = 0, OR_QP_BOUNDARY_NEUMANN = 1 };
 
@@ -24,7 +24,7 @@ typedef struct {
 
 typedef struct {
   int32_t kind, order;
-  double c, b, kx, ky;        /* sinusoid: c + b sin(kx x + ky y) */
+  double c, b, kx, ky;        /* sinusoid: c + b sin(kx x + ky y); cos product: c cos(kx x) cos(ky y) [cos(b z) if b != 0] */
   const double* per_elem;
 } or_qp_scalar_t;
 
@@ -45,6 +45,9 @@ int or_qp_pattern(const or_qp_grid_t* g, const int64_t* elem_index, int64_t* row
 int or_qp_assemble(const or_qp_grid_t* g, const or_qp_scalar_t* kappa, const or_qp_tensor_t* A,
                    const or_qp_params_t* p, const int64_t* elem_index, const int64_t* row_ptr, const int32_t* col,
                    double* val);
+int or_qp_rhs_swipdg(const or_qp_grid_t* g, const or_qp_scalar_t* force, const or_qp_scalar_t* kappa,
+                     const or_qp_tensor_t* A, const or_qp_scalar_t* dirichlet, const or_qp_scalar_t* neumann,
+                     const or_qp_params_t* p, const int64_t* elem_index, double* b);
 int or_qp_rhs_esv2007(const or_qp_grid_t* g, int force_order, const int64_t* elem_index, double* b);
 int or_qp_error_esv2007(const or_qp_grid_t* g, const double* u, const int64_t* elem_index, int order, double* l2,
                         double* h1);

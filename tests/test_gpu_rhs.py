@@ -1,0 +1,107 @@
+"""GPU right-hand side (hdd_swipdg_rhs, rhs.hip) against the oracle's restatement of the SWIPDG::init()
+functionals (swipdg.hh:251-347), entry-wise (|db| <= 1e-12 max|b|), for P1 triangles, Q1 quadrilaterals and
+Q_p hexahedra; and the complete GPU-assembled system (matrix + right-hand side, solved on the host)
+reproducing the reference's ESV2007 expectation table."""
+import numpy as np
+import pytest
+import scipy.sparse.linalg as spla
+
+import oracle as O
+from hex_tools import lex_to_product
+from mesh_tools import nvb_mesh
+from test_oracle_pinning import ALU_H1, ALU_L2, sig3
+
+H = pytest.importorskip("hdd_amd")
+pytestmark = pytest.mark.gpu
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def _close(got, ref):
+    return np.max(np.abs(got - ref)) <= 1e-12 * max(1.0, np.max(np.abs(ref)))
+
+
+@pytest.mark.parametrize("et", [H.SIMPLEX, H.CUBE])
+def test_rhs_2d(ctx, et):
+    torch = _torch()
+    n = (7, 5)
+    grid = H.Grid.structured(et, *n, (-1, -1), (1, 1))
+    loc = grid.local()
+    dm = H.DeviceMesh(loc)
+    og = O.Grid(*(O.kuhn_grid if et == H.SIMPLEX else O.cube_grid)(*n, (-1, -1), (1, 1)))
+    kel = np.random.default_rng(2).uniform(0.5, 2.0, grid.ne)
+    kdev = torch.from_numpy(kel).cuda()
+    T = np.random.default_rng(3).uniform(0.5, 2.0, grid.ne)
+    Tdev = torch.from_numpy(T).cuda()
+    cases = [
+        (dict(force=H.esv2007_force()), dict(force=O.esv2007_force()), O.BOUNDARY_DIRICHLET),
+        (dict(force=H.scalar_fn(H.FN_SINUSOID, 0.3, b=1.5, kx=2.0, ky=-1.0, order=3)),
+         dict(force=O.scalar(O.FN_SINUSOID, 0.3, 1.5, 2.0, -1.0, order=3)), O.BOUNDARY_DIRICHLET),
+        (dict(force=H.scalar_fn(H.FN_PER_ELEM, per_elem=kdev)), dict(force=O.scalar(O.FN_PER_ELEM, per_elem=kel)),
+         O.BOUNDARY_DIRICHLET),
+        (dict(dirichlet=H.scalar_fn(H.FN_SINUSOID, 1.0, b=0.5, kx=1.3, ky=0.7, order=3),
+              kappa=H.scalar_fn(H.FN_PER_ELEM, per_elem=kdev), tensor=H.tensor_fn(H.TENSOR_ISO_PER_ELEM, per_elem=Tdev)),
+         dict(dirichlet=O.scalar(O.FN_SINUSOID, 1.0, 0.5, 1.3, 0.7, order=3), kappa=O.scalar(O.FN_PER_ELEM, per_elem=kel),
+              A=O.tensor(O.TENSOR_ISO_PER_ELEM, per_elem=T)), O.BOUNDARY_DIRICHLET),
+        (dict(neumann=H.scalar_fn(H.FN_COS_PRODUCT, 2.0, kx=0.4, ky=0.9, order=2)),
+         dict(neumann=O.scalar(O.FN_COS_PRODUCT, 2.0, 0.0, 0.4, 0.9, order=2)), O.BOUNDARY_NEUMANN),
+    ]
+    for hk, ok, bkind in cases:
+        g2 = grid if bkind == O.BOUNDARY_DIRICHLET else H.Grid.structured(et, *n, (-1, -1), (1, 1),
+                                                                          boundary=H.BOUNDARY_ALL_NEUMANN)
+        dmm = dm if g2 is grid else H.DeviceMesh(g2.local())
+        b = H.rhs(ctx, dmm, prm=H.params(), **hk)
+        torch.cuda.synchronize()
+        ref = O.rhs_swipdg(og, prm=O.params(boundary=bkind), **ok)
+        assert _close(b.cpu().numpy(), ref), hk
+
+
+@pytest.mark.parametrize("deg", [1, 2, 3])
+def test_rhs_hex(ctx, deg):
+    torch = _torch()
+    n, lo, up = (3, 2, 4), (-1.0, 0.0, 0.5), (1.0, 1.5, 2.0)
+    for boundary, bk in [(H.BOUNDARY_ALL_DIRICHLET, O.BOUNDARY_DIRICHLET), (H.BOUNDARY_ALL_NEUMANN, O.BOUNDARY_NEUMANN)]:
+        g = H.Grid.structured3d(n, lo, up, p=(2, 1, 1), degree=deg, boundary=boundary)
+        ei = lex_to_product(g, n, lo, up)
+        q = O.QpGrid(3, deg, n, lo, up)
+        dm = H.DeviceMesh(g.local())
+        prm = H.params_for(deg, 3)
+        oprm = O.qp_params(q, boundary=bk)
+        hk = dict(force=H.esv2007_force(3))
+        ok = dict(force=O.esv2007_force(3))
+        if bk == O.BOUNDARY_DIRICHLET:
+            hk.update(dirichlet=H.scalar_fn(H.FN_SINUSOID, 1.0, b=0.5, kx=1.3, ky=0.7, order=3),
+                      kappa=H.scalar_fn(H.FN_CONST, 2.0), tensor=H.tensor_fn(dim=3))
+            ok.update(dirichlet=O.scalar(O.FN_SINUSOID, 1.0, 0.5, 1.3, 0.7, order=3), kappa=O.scalar(O.FN_CONST, 2.0))
+        else:
+            hk.update(neumann=H.scalar_fn(H.FN_CONST, 0.75))
+            ok.update(neumann=O.scalar(O.FN_CONST, 0.75))
+        b = H.rhs(ctx, dm, prm=prm, **hk)
+        torch.cuda.synchronize()
+        ref = O.qp_rhs_swipdg(q, prm=oprm, elem_index=ei, **ok)
+        assert _close(b.cpu().numpy(), ref), (deg, boundary)
+
+
+def test_alu_p1_table_from_gpu_system(ctx):
+    """GPU matrix + GPU right-hand side -> host solve -> ESV2007 ALU table (3 s.f.)."""
+    torch = _torch()
+    l2s, h1s = [], []
+    for lvl in range(4):
+        et, c, ev = nvb_mesh(4, 2 + 2 * lvl)
+        grid = H.Grid.from_connectivity(H.SIMPLEX, c, ev)
+        loc = grid.local()
+        dm = H.DeviceMesh(loc)
+        dp = H.DevicePattern(loc)
+        (val,) = H.assemble(ctx, dm, dp, [H.scalar_fn()], H.tensor_fn())
+        b = H.rhs(ctx, dm, force=H.esv2007_force(), prm=H.params())
+        torch.cuda.synchronize()
+        rp, col, _ = dp.host
+        u = spla.spsolve(O.to_scipy(rp, col, val.cpu().numpy()).tocsc(), b.cpu().numpy())
+        og = O.Grid(et, c, ev)
+        assert np.array_equal(loc.global_id, np.arange(grid.ne))   # no subdomains: element order kept
+        l2, h1 = O.error_norms_esv2007(og, u)
+        l2s.append(sig3(l2)); h1s.append(sig3(h1))
+    assert l2s == ALU_L2 and h1s == ALU_H1
