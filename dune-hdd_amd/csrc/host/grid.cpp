@@ -704,7 +704,7 @@ static int nb_of(int32_t et) { return et == HDD_SIMPLEX ? 3 : (et == HDD_CUBE ? 
 extern "C" int hdd_dg_pattern_count(int32_t nf, int32_t nb, int64_t n_local, int64_t own_begin, int64_t own_end,
                                     const int32_t* neighbors, int64_t* nnz)
 {
-  if (nf < 1 || nf > 6 || nb < 1) return set_error(HDD_ERR_INVALID, "hdd_dg_pattern_count: need 1 <= n_faces <= 6, nb >= 1");
+  if (nf < 0 || nf > 6 || nb < 1) return set_error(HDD_ERR_INVALID, "hdd_dg_pattern_count: need 0 <= n_faces <= 6, nb >= 1");
   if (!neighbors || !nnz || own_begin < 0 || own_end > n_local || own_begin > own_end)
     return set_error(HDD_ERR_INVALID, "hdd_dg_pattern_count: invalid argument");
   int64_t total = 0;
@@ -721,7 +721,7 @@ extern "C" int hdd_dg_pattern_fill(int32_t nf, int32_t nb, int64_t n_local, int6
                                    const int32_t* neighbors, const int64_t* global_id, int64_t* row_ptr,
                                    int32_t* col, int64_t* elem_ptr)
 {
-  if (nf < 1 || nf > 6 || nb < 1) return set_error(HDD_ERR_INVALID, "hdd_dg_pattern_fill: need 1 <= n_faces <= 6, nb >= 1");
+  if (nf < 0 || nf > 6 || nb < 1) return set_error(HDD_ERR_INVALID, "hdd_dg_pattern_fill: need 0 <= n_faces <= 6, nb >= 1");
   if (!neighbors || !row_ptr || !col || own_begin < 0 || own_end > n_local || own_begin > own_end)
     return set_error(HDD_ERR_INVALID, "hdd_dg_pattern_fill: invalid argument");
   int64_t off = 0;

@@ -700,3 +700,80 @@ extern "C" int hdd_swipdg_rhs(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_
   e = launch_rhs(a, static_cast<hipStream_t>(stream));
   return e == hipSuccess ? HDD_OK : hip_fail(e, "hdd_swipdg_rhs: launch");
 }
+
+extern "C" int hdd_product_assemble(hdd_ctx* ctx, const hdd_mesh* m, int32_t product, const hdd_scalar_fn* kappa,
+                                    const hdd_tensor_fn* tensor, const hdd_swipdg_params* p, const hdd_csr* pattern,
+                                    double* d_vals, void* stream)
+{
+  using namespace hdd::dev;
+  if (!ctx || !m || !p || !pattern || !d_vals || !pattern->elem_ptr)
+    return set_error(HDD_ERR_INVALID, "hdd_product_assemble: null argument");
+  if (product < HDD_PRODUCT_L2 || product > HDD_PRODUCT_PENALTY)
+    return set_error(HDD_ERR_INVALID, "hdd_product_assemble: unknown product");
+  if (m->elem_type != HDD_SIMPLEX && m->elem_type != HDD_CUBE && m->elem_type != HDD_HEX)
+    return set_error(HDD_ERR_UNSUPPORTED, "hdd_product_assemble: unknown element type");
+  if (m->own_begin < 0 || m->own_end > m->n_local || m->own_begin > m->own_end)
+    return set_error(HDD_ERR_RANGE, "hdd_product_assemble: 0 <= own_begin <= own_end <= n_local violated");
+  const bool needs_coeff = product == HDD_PRODUCT_ELLIPTIC || product == HDD_PRODUCT_PENALTY;
+  if (needs_coeff && (!kappa || !tensor))
+    return set_error(HDD_ERR_INVALID, "hdd_product_assemble: elliptic / penalty products need kappa and the tensor");
+  if (needs_coeff && kappa->kind == HDD_FN_PER_ELEM && !kappa->per_elem)
+    return set_error(HDD_ERR_INVALID, "hdd_product_assemble: kappa per_elem missing");
+  if (needs_coeff && tensor->kind != HDD_TENSOR_CONST && !tensor->per_elem)
+    return set_error(HDD_ERR_INVALID, "hdd_product_assemble: tensor per_elem missing");
+  const int deg = m->elem_type == HDD_HEX ? std::max(1, int(m->degree)) : 1;
+  if (m->elem_type != HDD_HEX && m->degree > 1)
+    return set_error(HDD_ERR_UNSUPPORTED, "hdd_product_assemble: 2d meshes carry P1 / Q1 only");
+  if (deg > 3) return set_error(HDD_ERR_UNSUPPORTED, "hdd_product_assemble: HDD_HEX supports p = 1..3");
+  const int nb = m->elem_type == HDD_SIMPLEX ? 3 : (m->elem_type == HDD_CUBE ? 4 : (deg + 1) * (deg + 1) * (deg + 1));
+  if (pattern->n_rows != int64_t(nb) * (m->own_end - m->own_begin))
+    return set_error(HDD_ERR_INVALID, "hdd_product_assemble: pattern rows != nb * owned elements");
+  ProductArgs a{};
+  a.elem_type = m->elem_type;
+  a.degree = deg;
+  a.nb = nb;
+  a.kind = product;
+  a.n_local = m->n_local;
+  a.own_begin = m->own_begin;
+  a.own_end = m->own_end;
+  a.coords = m->coords;
+  a.nbrs = m->neighbors;
+  a.elem_ptr = pattern->elem_ptr;
+  a.tkind = tensor ? tensor->kind : HDD_TENSOR_CONST;
+  for (int r = 0; r < 6; ++r) a.tc[r] = tensor ? tensor->c[r] : 0.0;
+  a.tper = tensor ? tensor->per_elem : nullptr;
+  a.kappa = kap_arg(kappa);
+  a.sigma_inner = p->sigma_inner;
+  a.sigma_boundary = p->sigma_boundary;
+  a.beta = p->beta;
+  a.vals = d_vals;
+  // integrand orders + over_integrate (= 2): test + ansatz order [+ kappa + A]; gradients count p - 1
+  const int over = 2, ko = kappa ? fn_order(*kappa) : 0;
+  if (product <= HDD_PRODUCT_ELLIPTIC) {
+    int order = product == HDD_PRODUCT_L2 ? 2 * deg + over : 2 * (deg - 1) + over;
+    if (product == HDD_PRODUCT_ELLIPTIC) order += ko;
+    if (m->elem_type == HDD_SIMPLEX) {
+      a.nqv = simplex_rule(order, a.qv, 64);
+      if (a.nqv < 0) return set_error(HDD_ERR_UNSUPPORTED, "hdd_product_assemble: integration order too high");
+    } else {
+      const int n1 = std::max(1, (order + 2) / 2);
+      if (n1 > 16) return set_error(HDD_ERR_UNSUPPORTED, "hdd_product_assemble: integration order too high");
+      double s[16], w[16];
+      gauss_legendre01(n1, s, w);
+      for (int q = 0; q < n1; ++q) { a.qv[q][0] = s[q]; a.qv[q][3] = w[q]; }
+      a.nqv = n1;
+    }
+  } else {
+    const int order = product == HDD_PRODUCT_BOUNDARY_L2 ? 2 * deg + over : ko + 2 * deg + over;
+    const int n1 = std::max(1, (order + 2) / 2);
+    if (n1 > 16) return set_error(HDD_ERR_UNSUPPORTED, "hdd_product_assemble: integration order too high");
+    double s[16], w[16];
+    gauss_legendre01(n1, s, w);
+    for (int q = 0; q < n1; ++q) { a.qf[q][0] = s[q]; a.qf[q][1] = w[q]; }
+    a.nq1f = n1;
+  }
+  hipError_t e = hipSetDevice(ctx->device);
+  if (e != hipSuccess) return hip_fail(e, "hdd_product_assemble: hipSetDevice");
+  e = launch_product(a, static_cast<hipStream_t>(stream));
+  return e == hipSuccess ? HDD_OK : hip_fail(e, "hdd_product_assemble: launch");
+}

@@ -1,4 +1,4 @@
-// dune-hdd_amd/csrc/kernels/rhs.hip
+// dune-hdd_amd/csrc/kernels/rhs.hip -- right-hand sides and products of SWIPDG::init()
 //
 // SWIPDG right-hand side: the functionals SWIPDG::init() adds to its walk
 // (dune/hdd/linearelliptic/discretizations/swipdg.hh:251-347):
@@ -211,6 +211,259 @@ __global__ __launch_bounds__(256) void rhs_kernel(RhsArgs a)
     }
     a.out[t] = acc;
   }
+}
+
+// ---------------------------------------------------------------------------------------------------
+// products of SWIPDG::init() (swipdg.hh:358-508, over_integrate = 2): one thread per matrix entry
+//   L2 phi_i phi_j, H1_SEMI grad.grad, ELLIPTIC kappa (A grad phi_j).grad phi_i, BOUNDARY_L2 on every
+//   boundary face -- element-local blocks (volume pattern, row length nb);
+//   PENALTY: sigma kappa^- kappa^+ gamma / |F|^beta [u][v] on inner faces and the boundary penalty on Dirichlet
+//   faces -- SWIPDG face pattern (owner-computes rows: self block and one block per inner face).
+// ---------------------------------------------------------------------------------------------------
+struct PGeo {
+  double v0[3], J[3][3], Ji[3][3], det;
+};
+
+__device__ void p_geo(const ProductArgs& a, int64_t e, int dim, PGeo& G)
+{
+  const int vcol[3] = {1, 2, 4};
+  const int64_t n = a.n_local;
+  for (int r = 0; r < 3; ++r)
+    for (int c = 0; c < 3; ++c) { G.J[r][c] = r == c; G.Ji[r][c] = r == c; }
+  for (int c = 0; c < 3; ++c) G.v0[c] = 0.0;
+  for (int c = 0; c < dim; ++c) G.v0[c] = a.coords[c * n + e];
+  for (int j = 0; j < dim; ++j)
+    for (int c = 0; c < dim; ++c) G.J[c][j] = a.coords[(dim * vcol[j] + c) * n + e] - G.v0[c];
+  double(*J)[3] = G.J;
+  if (dim == 2) {
+    G.det = J[0][0] * J[1][1] - J[0][1] * J[1][0];
+    G.Ji[0][0] = J[1][1] / G.det; G.Ji[0][1] = -J[0][1] / G.det;
+    G.Ji[1][0] = -J[1][0] / G.det; G.Ji[1][1] = J[0][0] / G.det;
+  } else {
+    const double c00 = J[1][1] * J[2][2] - J[1][2] * J[2][1];
+    const double c01 = J[1][2] * J[2][0] - J[1][0] * J[2][2];
+    const double c02 = J[1][0] * J[2][1] - J[1][1] * J[2][0];
+    G.det = J[0][0] * c00 + J[0][1] * c01 + J[0][2] * c02;
+    G.Ji[0][0] = c00 / G.det; G.Ji[1][0] = c01 / G.det; G.Ji[2][0] = c02 / G.det;
+    G.Ji[0][1] = (J[0][2] * J[2][1] - J[0][1] * J[2][2]) / G.det;
+    G.Ji[1][1] = (J[0][0] * J[2][2] - J[0][2] * J[2][0]) / G.det;
+    G.Ji[2][1] = (J[0][1] * J[2][0] - J[0][0] * J[2][1]) / G.det;
+    G.Ji[0][2] = (J[0][1] * J[1][2] - J[0][2] * J[1][1]) / G.det;
+    G.Ji[1][2] = (J[0][2] * J[1][0] - J[0][0] * J[1][2]) / G.det;
+    G.Ji[2][2] = (J[0][0] * J[1][1] - J[0][1] * J[1][0]) / G.det;
+  }
+}
+
+__device__ void p_tensor(const ProductArgs& a, int64_t e, int dim, double A[3][3])
+{
+  for (int r = 0; r < 3; ++r)
+    for (int c = 0; c < 3; ++c) A[r][c] = 0.0;
+  if (a.tkind == HDD_TENSOR_ISO_PER_ELEM) {
+    for (int c = 0; c < dim; ++c) A[c][c] = a.tper[e];
+    return;
+  }
+  const int ns = dim == 2 ? 3 : 6;
+  double cc[6];
+  for (int r = 0; r < ns; ++r) cc[r] = a.tkind == HDD_TENSOR_SYM_PER_ELEM ? a.tper[r * a.n_local + e] : a.tc[r];
+  if (dim == 2) {
+    A[0][0] = cc[0]; A[0][1] = A[1][0] = cc[1]; A[1][1] = cc[2];
+  } else {
+    A[0][0] = cc[0]; A[0][1] = A[1][0] = cc[1]; A[0][2] = A[2][0] = cc[2];
+    A[1][1] = cc[3]; A[1][2] = A[2][1] = cc[4]; A[2][2] = cc[5];
+  }
+}
+
+// reference face: corner r0, spanning vectors t1, t2, reference outer normal nr
+__device__ void p_face(int et, int f, double* r0, double* t1, double* t2, double* nr)
+{
+  for (int c = 0; c < 3; ++c) { r0[c] = 0.0; t1[c] = 0.0; t2[c] = 0.0; nr[c] = 0.0; }
+  if (et == HDD_SIMPLEX) {
+    const double P[3][2] = {{0, 0}, {1, 0}, {0, 1}};
+    const int fv[3][2] = {{0, 1}, {0, 2}, {1, 2}};
+    const double N[3][2] = {{0, -1}, {-1, 0}, {1, 1}};
+    for (int c = 0; c < 2; ++c) {
+      r0[c] = P[fv[f][0]][c];
+      t1[c] = P[fv[f][1]][c] - P[fv[f][0]][c];
+      nr[c] = N[f][c];
+    }
+    return;
+  }
+  const int dim = et == HDD_HEX ? 3 : 2;
+  const int af = f >> 1, sd = f & 1;
+  r0[af] = sd;
+  nr[af] = sd ? 1.0 : -1.0;
+  int b0 = -1, b1 = -1;
+  for (int c = 0; c < dim; ++c)
+    if (c != af) { if (b0 < 0) b0 = c; else b1 = c; }
+  t1[b0] = 1.0;
+  if (dim == 3) t2[b1] = 1.0;
+}
+
+__global__ __launch_bounds__(256) void product_kernel(ProductArgs a)
+{
+  const int et = a.elem_type, dim = et == HDD_HEX ? 3 : 2, nb = a.nb;
+  const int nf = et == HDD_SIMPLEX ? 3 : (et == HDD_CUBE ? 4 : 6);
+  const bool penalty = a.kind == HDD_PRODUCT_PENALTY;
+  const int64_t n_own = a.own_end - a.own_begin;
+  const int64_t n = a.n_local;
+  const int64_t width = penalty ? int64_t(nb) * 7 : nb;     // entries per row (upper bound for the penalty)
+  const int64_t total = n_own * nb * width;
+  for (int64_t t = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; t < total; t += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t k = t / (nb * width);
+    const int i = int((t / width) % nb);
+    const int64_t cidx = t % width;
+    const int64_t e = a.own_begin + k;
+    int32_t nbr[6];
+    int nblk = 1;
+    for (int f = 0; f < nf; ++f) {
+      nbr[f] = a.nbrs[f * n + e];
+      nblk += nbr[f] >= 0;
+    }
+    const int64_t rl = penalty ? int64_t(nb) * nblk : nb;
+    if (cidx >= rl) continue;
+    const int blk = int(cidx / nb), j = int(cidx % nb);
+    PGeo G;
+    p_geo(a, e, dim, G);
+    double acc = 0.0, xh[3] = {0, 0, 0}, x[3] = {0, 0, 0}, vi, vj, gi[3], gj[3];
+    if (a.kind <= HDD_PRODUCT_ELLIPTIC) {
+      double A[3][3];
+      if (a.kind == HDD_PRODUCT_ELLIPTIC) p_tensor(a, e, dim, A);
+      const int nq = et == HDD_SIMPLEX ? a.nqv : (dim == 2 ? a.nqv * a.nqv : a.nqv * a.nqv * a.nqv);
+      for (int q = 0; q < nq; ++q) {
+        double w;
+        if (et == HDD_SIMPLEX) {
+          xh[0] = a.qv[q][0]; xh[1] = a.qv[q][1]; w = a.qv[q][3];
+        } else {
+          int r = q;
+          w = 1.0;
+          for (int c = 0; c < dim; ++c) { xh[c] = a.qv[r % a.nqv][0]; w *= a.qv[r % a.nqv][3]; r /= a.nqv; }
+        }
+        rhs_basis(et, a.degree, i, xh, vi, gi);
+        rhs_basis(et, a.degree, j, xh, vj, gj);
+        double v;
+        if (a.kind == HDD_PRODUCT_L2) {
+          v = vi * vj;
+        } else {
+          double pi[3] = {0, 0, 0}, pj[3] = {0, 0, 0};   // physical gradients J^{-T} grad_ref
+          for (int c = 0; c < dim; ++c)
+            for (int r = 0; r < dim; ++r) { pi[c] += G.Ji[r][c] * gi[r]; pj[c] += G.Ji[r][c] * gj[r]; }
+          if (a.kind == HDD_PRODUCT_H1_SEMI) {
+            v = 0.0;
+            for (int c = 0; c < dim; ++c) v += pi[c] * pj[c];
+          } else {
+            for (int c = 0; c < dim; ++c) {
+              x[c] = G.v0[c];
+              for (int r = 0; r < dim; ++r) x[c] += G.J[c][r] * xh[r];
+            }
+            v = 0.0;
+            for (int c = 0; c < dim; ++c)
+              for (int r = 0; r < dim; ++r) v += A[c][r] * pj[r] * pi[c];
+            v *= rhs_fn(a.kappa, e, x, dim);
+          }
+        }
+        acc += w * fabs(G.det) * v;
+      }
+      a.vals[a.elem_ptr[k] + int64_t(i) * rl + cidx] = acc;
+      continue;
+    }
+    // face products: which element does column block `blk` belong to (blocks sorted by element id)
+    int64_t col_elem = -1;
+    {
+      int64_t ids[7];
+      int m = 0;
+      ids[m++] = e;
+      for (int f = 0; f < nf; ++f)
+        if (nbr[f] >= 0) ids[m++] = nbr[f];
+      for (int p = 1; p < m; ++p)
+        for (int q = p; q > 0 && ids[q - 1] > ids[q]; --q) { const int64_t tmp = ids[q]; ids[q] = ids[q - 1]; ids[q - 1] = tmp; }
+      col_elem = ids[blk];
+    }
+    const int nq1 = a.nq1f, nqf = dim == 2 ? nq1 : nq1 * nq1;
+    double A[3][3];
+    if (penalty) p_tensor(a, e, dim, A);
+    for (int f = 0; f < nf; ++f) {
+      const bool inner = nbr[f] >= 0;
+      if (a.kind == HDD_PRODUCT_BOUNDARY_L2 && inner) continue;
+      if (penalty) {
+        if (!inner && nbr[f] != HDD_NBR_DIRICHLET) continue;
+        if (col_elem != e && nbr[f] != col_elem) continue;   // neighbour block: only its face
+      }
+      double r0[3], t1[3], t2[3], nr[3];
+      p_face(et, f, r0, t1, t2, nr);
+      double nv[3] = {0, 0, 0}, nn = 0.0;
+      for (int c = 0; c < dim; ++c)
+        for (int r = 0; r < dim; ++r) nv[c] += G.Ji[r][c] * nr[r];
+      for (int c = 0; c < dim; ++c) nn += nv[c] * nv[c];
+      nn = sqrt(nn);
+      for (int c = 0; c < dim; ++c) nv[c] /= nn;
+      double fvol;
+      if (dim == 2) {
+        const double dx = G.J[0][0] * t1[0] + G.J[0][1] * t1[1], dy = G.J[1][0] * t1[0] + G.J[1][1] * t1[1];
+        fvol = sqrt(dx * dx + dy * dy);
+      } else {
+        fvol = fabs(G.det) * nn;
+      }
+      double pen_c = 1.0;   // sigma gamma / |F|^beta (without kappa)
+      PGeo Gn;
+      if (penalty) {
+        double An[3] = {0, 0, 0}, dm = 0.0;
+        for (int c = 0; c < dim; ++c)
+          for (int r = 0; r < dim; ++r) An[c] += A[c][r] * nv[r];
+        for (int c = 0; c < dim; ++c) dm += nv[c] * An[c];
+        double gam = dm, sig = a.sigma_boundary;
+        if (inner) {
+          double Ao[3][3], Ano[3] = {0, 0, 0}, dp = 0.0;
+          p_tensor(a, nbr[f], dim, Ao);
+          for (int c = 0; c < dim; ++c)
+            for (int r = 0; r < dim; ++r) Ano[c] += Ao[c][r] * nv[r];
+          for (int c = 0; c < dim; ++c) dp += nv[c] * Ano[c];
+          gam = dp * dm / (dp + dm);
+          sig = a.sigma_inner;
+          p_geo(a, nbr[f], dim, Gn);
+        }
+        pen_c = sig * gam / pow(fvol, a.beta);
+      }
+      for (int q = 0; q < nqf; ++q) {
+        const int qs = q % nq1, qt = q / nq1;
+        const double s0 = a.qf[qs][0], s1 = dim == 3 ? a.qf[qt][0] : 0.0;
+        const double w = a.qf[qs][1] * (dim == 3 ? a.qf[qt][1] : 1.0);
+        for (int c = 0; c < dim; ++c) xh[c] = r0[c] + s0 * t1[c] + s1 * t2[c];
+        rhs_basis(et, a.degree, i, xh, vi, gi);
+        if (!penalty) {
+          rhs_basis(et, a.degree, j, xh, vj, gj);
+          acc += w * fvol * vi * vj;
+          continue;
+        }
+        for (int c = 0; c < dim; ++c) {
+          x[c] = G.v0[c];
+          for (int r = 0; r < dim; ++r) x[c] += G.J[c][r] * xh[r];
+        }
+        const double ke = rhs_fn(a.kappa, e, x, dim);
+        const double fac = w * fvol * pen_c * ke * (inner ? rhs_fn(a.kappa, nbr[f], x, dim) : 1.0);
+        if (col_elem == e) {
+          rhs_basis(et, a.degree, j, xh, vj, gj);
+          acc += fac * vi * vj;
+        } else {
+          double xo[3] = {0, 0, 0};   // neighbour's reference coordinates of x
+          for (int r = 0; r < dim; ++r)
+            for (int c = 0; c < dim; ++c) xo[r] += Gn.Ji[r][c] * (x[c] - Gn.v0[c]);
+          rhs_basis(et, a.degree, j, xo, vj, gj);
+          acc -= fac * vi * vj;
+        }
+      }
+    }
+    a.vals[a.elem_ptr[k] + int64_t(i) * rl + cidx] = acc;
+  }
+}
+
+hipError_t launch_product(const ProductArgs& a, hipStream_t s)
+{
+  const int64_t width = a.kind == HDD_PRODUCT_PENALTY ? int64_t(a.nb) * 7 : a.nb;
+  const int64_t total = (a.own_end - a.own_begin) * a.nb * width;
+  if (total <= 0) return hipSuccess;
+  const int64_t blocks = (total + 255) / 256;
+  hipLaunchKernelGGL(product_kernel, dim3(unsigned(blocks < (1 << 20) ? blocks : (1 << 20))), dim3(256), 0, s, a);
+  return hipGetLastError();
 }
 
 hipError_t launch_rhs(const RhsArgs& a, hipStream_t s)

@@ -93,6 +93,25 @@ struct RhsArgs {
 };
 hipError_t launch_rhs(const RhsArgs& a, hipStream_t s);
 
+// products (rhs.hip): l2, h1_semi, elliptic, boundary_l2 (element-local blocks) and the SWIPDG penalty
+struct ProductArgs {
+  int32_t elem_type, degree, nb, kind;
+  int64_t n_local, own_begin, own_end;
+  const double* coords;
+  const int32_t* nbrs;
+  const int64_t* elem_ptr;
+  int32_t tkind, nqv;            // nqv: explicit simplex volume points, else 1D Gauss points (tensor)
+  double tc[6];
+  const double* tper;
+  KappaArg kappa;
+  double sigma_inner, sigma_boundary, beta;
+  int32_t nq1f, pad;             // 1D Gauss points of the face rule (tensor product in 3d)
+  double qv[64][4];              // simplex: point (2) + pad + weight; tensor: qv[k][0] = point, qv[k][3] = weight
+  double qf[16][2];              // 1D face rule: point, weight
+  double* vals;
+};
+hipError_t launch_product(const ProductArgs& a, hipStream_t s);
+
 int volume_points(int elem_type, int order);
 int face_points(int order);
 hipError_t launch_assemble(const AssembleArgs& a, int nqv, int nqf, hipStream_t s, bool* supported);

@@ -18,6 +18,7 @@ HEADER = os.path.abspath(os.path.join(ROOT, "..", "include", "hdd.h"))
 SIMPLEX, CUBE, HEX = 0, 1, 2
 NBR_DIRICHLET, NBR_NEUMANN = -1, -2
 FN_CONST, FN_PER_ELEM, FN_SINUSOID, FN_COS_PRODUCT = 0, 1, 2, 3
+PRODUCT_L2, PRODUCT_H1_SEMI, PRODUCT_ELLIPTIC, PRODUCT_BOUNDARY_L2, PRODUCT_PENALTY = 0, 1, 2, 3, 4
 TENSOR_CONST, TENSOR_ISO_PER_ELEM, TENSOR_SYM_PER_ELEM = 0, 1, 2
 BOUNDARY_ALL_DIRICHLET, BOUNDARY_ALL_NEUMANN = 0, 1
 MAX_COMP = 8
@@ -138,6 +139,8 @@ def lib():
         "hdd_swipdg_assemble_tiles": (_I32, [_VP, C.POINTER(MeshT), C.POINTER(ScalarFn), _I32, C.POINTER(TensorFn),
                                              C.POINTER(Params), C.POINTER(CsrT), _VP, _VP, _I64, _VP]),
         "hdd_affine_lincomb": (_I32, [_VP, _I64, _VP, _I32, _VP, _I32, _VP, _I64, _VP]),
+        "hdd_product_assemble": (_I32, [_VP, C.POINTER(MeshT), _I32, _VP, _VP, C.POINTER(Params), C.POINTER(CsrT),
+                                        _VP, _VP]),
         "hdd_swipdg_rhs": (_I32, [_VP, C.POINTER(MeshT), _VP, _VP, _VP, _VP, _VP, C.POINTER(Params), _VP, _VP]),
         "hdd_block_operator_map": (_I32, [_VP, _I32, _I32, _VP, _VP, _VP, _VP, _VP, C.POINTER(_I64)]),
         "hdd_gather_values": (_I32, [_VP, _VP, _VP, _I64, _VP, _VP]),
@@ -316,16 +319,18 @@ class LocalMesh:
             plan.append(dict(peer=int(peers[i]), send=ids, recv_offset=int(ro[i]), recv_count=int(rc[i])))
         return plan
 
-    def pattern(self):
-        """Host CSR pattern of the owned rows (global columns): row_ptr, col, elem_ptr."""
+    def pattern(self, volume=False):
+        """Host CSR pattern of the owned rows (global columns): row_ptr, col, elem_ptr.  volume=True: the
+        element-local pattern of the l2 / h1_semi / elliptic / boundary_l2 products."""
         nnz = C.c_int64()
         nbrs = np.ascontiguousarray(self.neighbors)
-        _check(lib().hdd_dg_pattern_count(self.nf, self.nb, self.n_local, self.own_begin, self.own_end, _p(nbrs),
+        nf = 0 if volume else self.nf
+        _check(lib().hdd_dg_pattern_count(nf, self.nb, self.n_local, self.own_begin, self.own_end, _p(nbrs),
                                           C.byref(nnz)), "hdd_dg_pattern_count")
         row_ptr = np.empty(self.nb * self.n_own + 1, np.int64)
         col = np.empty(nnz.value, np.int32)
         elem_ptr = np.empty(self.n_own + 1, np.int64)
-        _check(lib().hdd_dg_pattern_fill(self.nf, self.nb, self.n_local, self.own_begin, self.own_end, _p(nbrs),
+        _check(lib().hdd_dg_pattern_fill(nf, self.nb, self.n_local, self.own_begin, self.own_end, _p(nbrs),
                                          _p(self.global_id), _p(row_ptr), _p(col), _p(elem_ptr)),
                "hdd_dg_pattern_fill")
         return row_ptr, col, elem_ptr
@@ -405,7 +410,7 @@ class DevicePattern:
     """CSR pattern of the owned rows in HBM.  on_device=True builds it with the HIP pattern kernels
     (hdd_pattern_elem_ptr_device / hdd_pattern_fill_device) instead of on the host."""
 
-    def __init__(self, local, device=0, host=None, ctx=None, dmesh=None, on_device=False):
+    def __init__(self, local, device=0, host=None, ctx=None, dmesh=None, on_device=False, volume=False):
         torch = _torch()
         dev = torch.device("cuda", device)
         if on_device:
@@ -429,7 +434,7 @@ class DevicePattern:
             self.t = CsrT(local.nb * local.n_own, n_cols, self.nnz, self.row_ptr.data_ptr(), self.col.data_ptr(),
                           self.elem_ptr.data_ptr())
             return
-        row_ptr, col, elem_ptr = host if host is not None else local.pattern()
+        row_ptr, col, elem_ptr = host if host is not None else local.pattern(volume=volume)
         self.host = (row_ptr, col, elem_ptr)
         self.row_ptr = torch.from_numpy(row_ptr).to(dev)
         self.col = torch.from_numpy(col).to(dev)
@@ -483,6 +488,21 @@ def halo_tiles(local):
     return np.nonzero(~bt)[0].astype(np.int32), np.nonzero(bt)[0].astype(np.int32)
 
 
+def product(ctx, dmesh, kind, dpattern, kappa=None, tensor=None, prm=None, out=None, stream=None):
+    """hdd_product_assemble: the l2 / h1_semi / elliptic / boundary_l2 / penalty products of SWIPDG::init()
+    (swipdg.hh:358-508).  Volume products need DevicePattern(..., volume=True)."""
+    torch = _torch()
+    local = dmesh.local
+    if out is None:
+        out = torch.empty(dpattern.nnz, dtype=torch.float64, device=dmesh.coords.device)
+    ref = lambda x: None if x is None else C.byref(x)
+    prm = prm or params_for(local.degree, local.dim)
+    s = stream if stream is not None else torch.cuda.current_stream(dmesh.coords.device).cuda_stream
+    _check(lib().hdd_product_assemble(ctx.h, C.byref(dmesh.t), kind, ref(kappa), ref(tensor), C.byref(prm),
+                                      C.byref(dpattern.t), out.data_ptr(), C.c_void_p(s)), "hdd_product_assemble")
+    return out
+
+
 def esv2007_force(dim=2):
     """ESV2007 Testcase1Force (problems/ESV2007.hh:78, integration order 3): 1/2 pi^2 cos(pi x/2) cos(pi y/2);
     in 3d (C5) (3/4) pi^2 prod cos(pi x_a / 2)."""
@@ -498,7 +518,7 @@ def rhs(ctx, dmesh, force=None, kappa=None, tensor=None, dirichlet=None, neumann
     local = dmesh.local
     if out is None:
         out = torch.empty(local.nb * local.n_own, dtype=torch.float64, device=dmesh.coords.device)
-    ref = lambda x: None if x is None else C.cast(C.byref(x), C.c_void_p)
+    ref = lambda x: None if x is None else C.byref(x)
     prm = prm or params_for(local.degree, local.dim)
     s = stream if stream is not None else torch.cuda.current_stream(dmesh.coords.device).cuda_stream
     _check(lib().hdd_swipdg_rhs(ctx.h, C.byref(dmesh.t), ref(force), ref(kappa), ref(tensor), ref(dirichlet),

@@ -158,7 +158,8 @@ int hdd_pattern_count(int32_t elem_type, int64_t n_local, int64_t own_begin, int
 int hdd_pattern_fill(int32_t elem_type, int64_t n_local, int64_t own_begin, int64_t own_end,
                      const int32_t* neighbors, const int64_t* global_id, int64_t* row_ptr, int32_t* col,
                      int64_t* elem_ptr);
-/* the same for any DG space: n_faces faces and nb basis functions per element (Q_p: nb = (p+1)^dim) */
+/* the same for any DG space: n_faces faces and nb basis functions per element (Q_p: nb = (p+1)^dim);
+ * n_faces = 0 gives the element-local (volume) pattern of the l2 / h1_semi / elliptic / boundary_l2 products */
 int hdd_dg_pattern_count(int32_t n_faces, int32_t nb, int64_t n_local, int64_t own_begin, int64_t own_end,
                          const int32_t* neighbors, int64_t* nnz);
 int hdd_dg_pattern_fill(int32_t n_faces, int32_t nb, int64_t n_local, int64_t own_begin, int64_t own_end,
@@ -247,6 +248,19 @@ int hdd_swipdg_assemble_tiles(hdd_ctx* ctx, const hdd_mesh* mesh, const hdd_scal
 int hdd_swipdg_rhs(hdd_ctx* ctx, const hdd_mesh* mesh, const hdd_scalar_fn* force, const hdd_scalar_fn* kappa,
                    const hdd_tensor_fn* tensor, const hdd_scalar_fn* dirichlet, const hdd_scalar_fn* neumann,
                    const hdd_swipdg_params* params, double* d_rhs, void* stream);
+
+/* Products of SWIPDG::init() (swipdg.hh:358-508; over_integrate = 2) -- BlockSWIPDG's local products
+ * (block-swipdg.hh:392-548) are the same on the subdomain's elements:
+ *   HDD_PRODUCT_L2, _H1_SEMI, _ELLIPTIC (kappa, tensor), _BOUNDARY_L2: element-local blocks; pattern =
+ *   hdd_dg_pattern_fill with n_faces = 0 (row length nb);
+ *   HDD_PRODUCT_PENALTY (kappa, tensor): the SWIPDG penalty terms sigma kappa^- kappa^+ gamma / |F|^beta on
+ *   inner faces and the boundary penalty on Dirichlet faces; pattern = the SWIPDG pattern.
+ * Writes d_vals[0..nnz) (every entry once). */
+enum { HDD_PRODUCT_L2 = 0, HDD_PRODUCT_H1_SEMI = 1, HDD_PRODUCT_ELLIPTIC = 2, HDD_PRODUCT_BOUNDARY_L2 = 3,
+       HDD_PRODUCT_PENALTY = 4 };
+int hdd_product_assemble(hdd_ctx* ctx, const hdd_mesh* mesh, int32_t product, const hdd_scalar_fn* kappa,
+                         const hdd_tensor_fn* tensor, const hdd_swipdg_params* params, const hdd_csr* pattern,
+                         double* d_vals, void* stream);
 
 /* theta-lincomb of affine components on a shared pattern -- replaces
  * AffinelyDecomposedContainer::freeze_parameter(mu) as used by ContainerBasedDefault::uncached_solve

@@ -377,7 +377,7 @@ def rhs_swipdg(grid, force=None, kappa=None, A=None, dirichlet=None, neumann=Non
     kappa = kappa or scalar()
     A = A or tensor()
     prm = prm or params()
-    ref = lambda x: None if x is None else C.cast(C.byref(x), C.c_void_p)
+    ref = lambda x: None if x is None else C.byref(x)
     L.or_rhs_swipdg(grid.h, ref(force), ref(kappa), ref(A), ref(dirichlet), ref(neumann), ref(prm), _ptr(ei),
                     _ptr(b))
     return b
@@ -392,7 +392,47 @@ def qp_rhs_swipdg(grid, force=None, kappa=None, A=None, dirichlet=None, neumann=
     kappa = kappa or scalar()
     A = A or qp_tensor(dim=grid.dim)
     prm = prm or qp_params(grid)
-    ref = lambda x: None if x is None else C.cast(C.byref(x), C.c_void_p)
-    L.or_qp_rhs_swipdg(C.cast(C.byref(grid.t), C.c_void_p), ref(force), ref(kappa), ref(A), ref(dirichlet),
+    ref = lambda x: None if x is None else C.byref(x)
+    L.or_qp_rhs_swipdg(C.byref(grid.t), ref(force), ref(kappa), ref(A), ref(dirichlet),
                        ref(neumann), ref(prm), _ptr(ei), _ptr(b))
     return b
+
+
+# ------------------------------------------------------------------------------------------------------
+# products (swipdg.hh:358-508)
+# ------------------------------------------------------------------------------------------------------
+PRODUCT_L2, PRODUCT_H1_SEMI, PRODUCT_ELLIPTIC, PRODUCT_BOUNDARY_L2, PRODUCT_PENALTY = 0, 1, 2, 3, 4
+
+
+def volume_pattern(ne, nb, elem_index=None):
+    """Block-diagonal (volume) pattern of the l2 / h1_semi / elliptic / boundary_l2 products."""
+    rp = np.arange(ne * nb + 1, dtype=np.int64) * nb
+    blk = np.arange(ne, dtype=np.int64)                     # row block k holds element k's DoFs
+    col = (blk[:, None, None] * nb + np.arange(nb)[None, None, :]).repeat(nb, axis=1).reshape(-1).astype(np.int32)
+    return rp, col
+
+
+def product(grid, kind, kappa=None, A=None, prm=None, elem_index=None):
+    L = lib()
+    L.or_product.argtypes = [C.c_void_p, C.c_int] + [C.c_void_p] * 7
+    ei = None if elem_index is None else np.ascontiguousarray(elem_index, np.int64)
+    rp, col = volume_pattern(grid.ne, grid.nb) if kind != PRODUCT_PENALTY else grid.pattern(ei)
+    val = np.empty(col.shape[0])
+    ref = lambda x: C.byref(x)
+    L.or_product(grid.h, kind, ref(kappa or scalar()), ref(A or tensor()), ref(prm or params()), _ptr(ei), _ptr(rp),
+                 _ptr(col), _ptr(val))
+    return rp, col, val
+
+
+def qp_product(grid, kind, kappa=None, A=None, prm=None, elem_index=None):
+    L = _qp_lib()
+    L.or_qp_product.restype = C.c_int
+    L.or_qp_product.argtypes = [C.c_void_p, C.c_int] + [C.c_void_p] * 7
+    ei = None if elem_index is None else np.ascontiguousarray(elem_index, np.int64)
+    rp, col = volume_pattern(grid.ne, grid.nb) if kind != PRODUCT_PENALTY else grid.pattern(ei)
+    val = np.empty(col.shape[0])
+    ref = lambda x: C.byref(x)
+    L.or_qp_product(C.byref(grid.t), kind, ref(kappa or scalar()),
+                    ref(A or qp_tensor(dim=grid.dim)), ref(prm or qp_params(grid)), _ptr(ei), _ptr(rp), _ptr(col),
+                    _ptr(val))
+    return rp, col, val

@@ -744,6 +744,113 @@ int or_rhs_swipdg(void* gp, const or_scalar_t* force, const or_scalar_t* kappa, 
   return 0;
 }
 
+/* Products (swipdg.hh:358-508): dune-gdt L2 / H1Semi / Elliptic / BoundaryL2 / SwipdgPenalty assemblables with
+ * over_integrate = 2 added to the integrand orders (test order + ansatz order [+ kappa, A orders]). */
+int or_product(void* gp, int kind, const or_scalar_t* kappa, const or_tensor_t* A, const or_params_t* prm,
+               const int64_t* elem_index, const int64_t* row_ptr, const int32_t* col, double* val)
+{
+  grid_t* g = (grid_t*)gp;
+  const int nb = g->nb;
+  ctx_t c = {g, kappa, A, prm, elem_index, row_ptr, col, val};
+  memset(val, 0, sizeof(double) * (size_t)row_ptr[g->ne * nb]);
+  const int over = 2;
+  double L[4][4], EN[4][4], NE[4][4], NN[4][4];
+  for (int64_t e = 0; e < g->ne; ++e) {
+    geom_t G; geometry(g, e, &G);
+    if (kind <= OR_PRODUCT_ELLIPTIC) {
+      int order = kind == OR_PRODUCT_L2 ? 2 + over : 0 + over;
+      if (kind == OR_PRODUCT_ELLIPTIC) order = scalar_order(kappa) + TENSOR_ORDER + over;
+      double Am[2][2];
+      if (kind == OR_PRODUCT_ELLIPTIC) eval_tensor(A, e, Am);
+      quad2_t q; volume_rule(g->type, order, &q);
+      memset(L, 0, sizeof(L));
+      for (int k = 0; k < q.n; ++k) {
+        double phi[4], gh[4][2], gpv[4][2], x[2];
+        shape(g->type, q.x[k], phi, gh);
+        global_pt(&G, q.x[k], x);
+        for (int i = 0; i < nb; ++i) map_grad(&G, gh[i], gpv[i]);
+        const double w = q.w[k] * fabs(G.det);
+        const double kap = kind == OR_PRODUCT_ELLIPTIC ? eval_scalar(kappa, e, x) : 1.0;
+        for (int i = 0; i < nb; ++i)
+          for (int j = 0; j < nb; ++j) {
+            double v;
+            if (kind == OR_PRODUCT_L2) v = phi[i] * phi[j];
+            else if (kind == OR_PRODUCT_H1_SEMI) v = gpv[i][0] * gpv[j][0] + gpv[i][1] * gpv[j][1];
+            else v = kap * ((Am[0][0] * gpv[j][0] + Am[0][1] * gpv[j][1]) * gpv[i][0] +
+                            (Am[1][0] * gpv[j][0] + Am[1][1] * gpv[j][1]) * gpv[i][1]);
+            L[i][j] += w * v;
+          }
+      }
+      scatter(&c, e, e, L);
+      continue;
+    }
+    for (int f = 0; f < g->nf; ++f) {
+      const int64_t ne = g->nbr[e * g->nf + f];
+      face_t F; face_geometry(g, &G, f, &F);
+      if (kind == OR_PRODUCT_BOUNDARY_L2) {
+        if (ne >= 0) continue;
+        quad1_t q; line_rule(2 + over, &q);
+        memset(L, 0, sizeof(L));
+        for (int k = 0; k < q.n; ++k) {
+          const double s = q.s[k];
+          double xin[2] = {F.ra[0] + s * (F.rb[0] - F.ra[0]), F.ra[1] + s * (F.rb[1] - F.ra[1])};
+          double ph[4], gh[4][2];
+          shape(g->type, xin, ph, gh);
+          for (int i = 0; i < nb; ++i)
+            for (int j = 0; j < nb; ++j) L[i][j] += q.w[k] * F.len * ph[i] * ph[j];
+        }
+        scatter(&c, e, e, L);
+        continue;
+      }
+      /* PENALTY: the penalty terms of SWIPDG::Inner / BoundaryLHS */
+      if (ne < 0 && prm->boundary_kind != OR_BOUNDARY_DIRICHLET) continue;
+      if (ne >= 0 && !(e < ne)) continue;
+      double Ai[2][2]; eval_tensor(A, e, Ai);
+      const double* n = F.n;
+      const double dm = n[0] * (Ai[0][0] * n[0] + Ai[0][1] * n[1]) + n[1] * (Ai[1][0] * n[0] + Ai[1][1] * n[1]);
+      double gamma = dm, sigma = prm->sigma_boundary;
+      geom_t Go;
+      if (ne >= 0) {
+        double Ao[2][2]; eval_tensor(A, ne, Ao);
+        geometry(g, ne, &Go);
+        const double dp = n[0] * (Ao[0][0] * n[0] + Ao[0][1] * n[1]) + n[1] * (Ao[1][0] * n[0] + Ao[1][1] * n[1]);
+        gamma = dp * dm / (dp + dm);
+        sigma = prm->sigma_inner;
+      }
+      const double hpow = pow(F.len, prm->beta);
+      quad1_t q; line_rule(scalar_order(kappa) + TENSOR_ORDER + 2 + over, &q);
+      memset(L, 0, sizeof(L)); memset(EN, 0, sizeof(EN)); memset(NE, 0, sizeof(NE)); memset(NN, 0, sizeof(NN));
+      for (int k = 0; k < q.n; ++k) {
+        const double s = q.s[k];
+        double xin[2] = {F.ra[0] + s * (F.rb[0] - F.ra[0]), F.ra[1] + s * (F.rb[1] - F.ra[1])};
+        double x[2]; global_pt(&G, xin, x);
+        double pe[4], ghe[4][2], pn[4] = {0, 0, 0, 0}, ghn[4][2];
+        shape(g->type, xin, pe, ghe);
+        const double ke = eval_scalar(kappa, e, x);
+        double pen;
+        if (ne >= 0) {
+          double xout[2]; local_pt(&Go, x, xout);
+          shape(g->type, xout, pn, ghn);
+          pen = ke * eval_scalar(kappa, ne, x) * sigma * gamma / hpow;
+        } else {
+          pen = ke * sigma * gamma / hpow;
+        }
+        const double fac = q.w[k] * F.len * pen;
+        for (int i = 0; i < nb; ++i)
+          for (int j = 0; j < nb; ++j) {
+            L[i][j] += fac * pe[j] * pe[i];
+            EN[i][j] -= fac * pn[j] * pe[i];
+            NE[i][j] -= fac * pe[j] * pn[i];
+            NN[i][j] += fac * pn[j] * pn[i];
+          }
+      }
+      scatter(&c, e, e, L);
+      if (ne >= 0) { scatter(&c, e, ne, EN); scatter(&c, ne, e, NE); scatter(&c, ne, ne, NN); }
+    }
+  }
+  return 0;
+}
+
 /* ||u - u_h||_L2 and |u - u_h|_H1 for the ESV2007 exact solution, element-wise high order quadrature */
 int or_error_norms_esv2007(void* gp, const double* u, const int64_t* elem_index, int order, double* l2,
                            double* h1)

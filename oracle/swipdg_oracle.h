@@ -70,6 +70,13 @@ int or_rhs_l2(void* g, int force_kind, int force_order, const int64_t* elem_inde
 int or_rhs_swipdg(void* g, const or_scalar_t* force, const or_scalar_t* kappa, const or_tensor_t* A,
                   const or_scalar_t* dirichlet, const or_scalar_t* neumann, const or_params_t* p,
                   const int64_t* elem_index, double* b);
+/* products of SWIPDG::init() (swipdg.hh:358-508), over_integrate = 2:
+ *   L2 / H1_SEMI / ELLIPTIC (kappa, A) / BOUNDARY_L2: element-local blocks (volume pattern)
+ *   PENALTY (kappa, A): the SWIPDG penalty terms on inner (4 blocks) and Dirichlet faces (face pattern) */
+enum { OR_PRODUCT_L2 = 0, OR_PRODUCT_H1_SEMI = 1, OR_PRODUCT_ELLIPTIC = 2, OR_PRODUCT_BOUNDARY_L2 = 3,
+       OR_PRODUCT_PENALTY = 4 };
+int or_product(void* g, int kind, const or_scalar_t* kappa, const or_tensor_t* A, const or_params_t* p,
+               const int64_t* elem_index, const int64_t* row_ptr, const int32_t* col, double* val);
 int or_error_norms_esv2007(void* g, const double* u, const int64_t* elem_index, int order, double* l2, double* h1);
 
 #ifdef __cplusplus

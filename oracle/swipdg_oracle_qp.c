@@ -554,6 +554,121 @@ int or_qp_assemble(const or_qp_grid_t* in, const or_qp_scalar_t* kappa, const or
   return 0;
 }
 
+/* products, over_integrate = 2 (kinds as OR_PRODUCT_* of swipdg_oracle.h: 0 L2, 1 H1 semi, 2 elliptic,
+ * 3 boundary L2, 4 SWIPDG penalty) */
+int or_qp_product(const or_qp_grid_t* in, int kind, const or_qp_scalar_t* kappa, const or_qp_tensor_t* A,
+                  const or_qp_params_t* prm, const int64_t* elem_index, const int64_t* row_ptr, const int32_t* col,
+                  double* val)
+{
+  qgrid_t g;
+  if (init_grid(in, &g)) return -1;
+  qctx_t c = {&g, kappa, A, prm, elem_index, row_ptr, col, val};
+  const int nb = g.nb, d = g.dim, over = 2;
+  memset(val, 0, sizeof(double) * (size_t)row_ptr[g.ne * nb]);
+  double* buf = (double*)malloc(sizeof(double) * (size_t)(4 * nb * nb));
+  double *L = buf, *EN = buf + nb * nb, *NE = buf + 2 * nb * nb, *NN = buf + 3 * nb * nb;
+  qrule_t* q = (qrule_t*)malloc(sizeof(qrule_t));
+  double phi[125], gh[125][3], gp[125][3], pn[125], ghn[125][3];
+  for (int64_t e = 0; e < g.ne; ++e) {
+    geo_t G;
+    geometry(&g, e, &G);
+    if (kind <= 2) {
+      int order = kind == 0 ? 2 * g.p + over : 2 * (g.p - 1) + over;
+      if (kind == 2) order += scalar_order(kappa);
+      double Am[3][3];
+      if (kind == 2) eval_tensor(&g, A, e, Am);
+      tensor_rule(d, order, q);
+      memset(L, 0, sizeof(double) * (size_t)(nb * nb));
+      for (int k = 0; k < q->n; ++k) {
+        double x[3], Ag[3];
+        shape(&g, q->x[k], phi, gh);
+        global_pt(&G, q->x[k], x);
+        for (int i = 0; i < nb; ++i) map_grad(&G, gh[i], gp[i]);
+        const double w = q->w[k] * fabs(G.det) * (kind == 2 ? eval_scalar(kappa, e, x) : 1.0);
+        for (int i = 0; i < nb; ++i)
+          for (int j = 0; j < nb; ++j) {
+            double v;
+            if (kind == 0) v = phi[i] * phi[j];
+            else if (kind == 1) v = dot(d, gp[i], gp[j]);
+            else { matvec(d, Am, gp[j], Ag); v = dot(d, Ag, gp[i]); }
+            L[i * nb + j] += w * v;
+          }
+      }
+      scatter(&c, e, e, L);
+      continue;
+    }
+    for (int f = 0; f < g.nf; ++f) {
+      const int64_t ne = neighbour(&g, e, f);
+      double n[3], fvol;
+      face_normal(&G, f, n, &fvol);
+      if (kind == 3) {
+        if (ne >= 0) continue;
+        tensor_rule(d - 1, 2 * g.p + over, q);
+        memset(L, 0, sizeof(double) * (size_t)(nb * nb));
+        for (int k = 0; k < q->n; ++k) {
+          double xin[3];
+          face_ref_point(d, f, q->x[k], xin);
+          shape(&g, xin, phi, gh);
+          for (int i = 0; i < nb; ++i)
+            for (int j = 0; j < nb; ++j) L[i * nb + j] += q->w[k] * fvol * phi[i] * phi[j];
+        }
+        scatter(&c, e, e, L);
+        continue;
+      }
+      if (ne < 0 && prm->boundary_kind != OR_QP_BOUNDARY_DIRICHLET) continue;
+      if (ne >= 0 && !(e < ne)) continue;
+      double Ai[3][3], An_i[3];
+      eval_tensor(&g, A, e, Ai);
+      matvec(d, Ai, n, An_i);
+      const double dm = dot(d, n, An_i);
+      double gamma = dm, sigma = prm->sigma_boundary;
+      geo_t Go;
+      if (ne >= 0) {
+        double Ao[3][3], An_o[3];
+        eval_tensor(&g, A, ne, Ao);
+        matvec(d, Ao, n, An_o);
+        geometry(&g, ne, &Go);
+        const double dp = dot(d, n, An_o);
+        gamma = dp * dm / (dp + dm);
+        sigma = prm->sigma_inner;
+      }
+      const double hpow = pow(fvol, prm->beta);
+      tensor_rule(d - 1, scalar_order(kappa) + 2 * g.p + over, q);
+      const size_t sz = sizeof(double) * (size_t)(nb * nb);
+      memset(L, 0, sz); memset(EN, 0, sz); memset(NE, 0, sz); memset(NN, 0, sz);
+      for (int k = 0; k < q->n; ++k) {
+        double xin[3], x[3], xout[3];
+        face_ref_point(d, f, q->x[k], xin);
+        global_pt(&G, xin, x);
+        shape(&g, xin, phi, gh);
+        const double ke = eval_scalar(kappa, e, x);
+        double pen;
+        if (ne >= 0) {
+          local_pt(&Go, x, xout);
+          shape(&g, xout, pn, ghn);
+          pen = ke * eval_scalar(kappa, ne, x) * sigma * gamma / hpow;
+        } else {
+          for (int i = 0; i < nb; ++i) pn[i] = 0.0;
+          pen = ke * sigma * gamma / hpow;
+        }
+        const double fac = q->w[k] * fvol * pen;
+        for (int i = 0; i < nb; ++i)
+          for (int j = 0; j < nb; ++j) {
+            L[i * nb + j] += fac * phi[j] * phi[i];
+            EN[i * nb + j] -= fac * pn[j] * phi[i];
+            NE[i * nb + j] -= fac * phi[j] * pn[i];
+            NN[i * nb + j] += fac * pn[j] * pn[i];
+          }
+      }
+      scatter(&c, e, e, L);
+      if (ne >= 0) { scatter(&c, e, ne, EN); scatter(&c, ne, e, NE); scatter(&c, ne, ne, NN); }
+    }
+  }
+  free(buf);
+  free(q);
+  return 0;
+}
+
 /* SWIPDG right-hand side (see or_rhs_swipdg in swipdg_oracle.c for the functionals and orders) */
 int or_qp_rhs_swipdg(const or_qp_grid_t* in, const or_qp_scalar_t* force, const or_qp_scalar_t* kappa,
                      const or_qp_tensor_t* A, const or_qp_scalar_t* dirichlet, const or_qp_scalar_t* neumann,

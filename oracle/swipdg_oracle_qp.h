@@ -48,6 +48,10 @@ int or_qp_assemble(const or_qp_grid_t* g, const or_qp_scalar_t* kappa, const or_
 int or_qp_rhs_swipdg(const or_qp_grid_t* g, const or_qp_scalar_t* force, const or_qp_scalar_t* kappa,
                      const or_qp_tensor_t* A, const or_qp_scalar_t* dirichlet, const or_qp_scalar_t* neumann,
                      const or_qp_params_t* p, const int64_t* elem_index, double* b);
+/* products (see or_product in swipdg_oracle.h; kinds OR_PRODUCT_*) */
+int or_qp_product(const or_qp_grid_t* g, int kind, const or_qp_scalar_t* kappa, const or_qp_tensor_t* A,
+                  const or_qp_params_t* p, const int64_t* elem_index, const int64_t* row_ptr, const int32_t* col,
+                  double* val);
 int or_qp_rhs_esv2007(const or_qp_grid_t* g, int force_order, const int64_t* elem_index, double* b);
 int or_qp_error_esv2007(const or_qp_grid_t* g, const double* u, const int64_t* elem_index, int order, double* l2,
                         double* h1);
