@@ -48,37 +48,58 @@ def parse():
     return ap.parse_args()
 
 
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(nx_full, ny, target_s):
-    """The CPU oracle (single thread: the reference's walk() runs without TBB, swipdg.hh:485) timed on a
-    bounded strip of the same workload: nxs x ny Kuhn squares over [0, 5 nxs/nx_full] x [0,1]."""
+    """The CPU oracle timed on a bounded strip of the same workload (nxs x ny Kuhn squares over
+    [0, 5 nxs/nx_full] x [0,1], checkerboard of the full domain), SURVEY.md 8(d) protocol: 1 warm-up, median
+    of 5.  `value`: the sequential element walk with per-entry CSR binary search, 1 thread -- the reference's
+    walk() runs without TBB (swipdg.hh:485).  `omp_value`: the owner-computes OpenMP variant of the same
+    integrands on the host cores this process may use (16 on the GPU box's share)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     perm = O.spe10_synthetic_permeability()
     lower = (0.0, 0.0)
+    threads = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()))
 
-    def run(nxs):
+    def run(nxs, reps=5, omp=0):
         upper = (5.0 * nxs / nx_full, 1.0)
         et, c, ev = O.kuhn_grid(nxs, ny, lower, upper)
-        # checkerboard of the FULL domain, evaluated at the strip's element centres
         k = O.checkerboard(O.element_centers(c, ev), (0.0, 0.0), (5.0, 1.0), 100, 20, perm)
         g = O.Grid(et, c, ev)
         rp, col = g.pattern()
         kap, ten, prm = O.scalar(O.FN_CONST, 1.0), O.tensor(O.TENSOR_ISO_PER_ELEM, per_elem=k), O.params()
-        O.assemble(g, kap, ten, prm, pattern=(rp, col))          # warm-up
+        fn = (lambda: O.assemble_owner(g, kap, ten, prm, pattern=(rp, col), threads=omp)) if omp else \
+             (lambda: O.assemble(g, kap, ten, prm, pattern=(rp, col)))
+        fn()                                                    # warm-up
         ts = []
-        for _ in range(3):
+        for _ in range(reps):
             t = time.perf_counter()
-            O.assemble(g, kap, ten, prm, pattern=(rp, col))
+            fn()
             ts.append(time.perf_counter() - t)
         return float(np.median(ts)), g.ne * 3
 
-    t_cal, _ = run(25)
-    nxs = int(min(nx_full, max(25, 25 * (target_s / 3.0) / max(t_cal, 1e-6))))
+    t_cal, _ = run(25, reps=1)
+    per_rep = target_s / 6.0                                   # warm-up + 5 timed runs ~ target_s
+    nxs = int(min(nx_full, max(25, 25 * per_rep / max(t_cal, 1e-6))))
     t, dofs = run(nxs)
+    t_omp, _ = run(nxs, omp=threads)
     return dict(value=dofs / t, unit="DoFs/s", cores=1, kind="port",
                 sample="CPU oracle (oracle/swipdg_oracle.c, sequential element walk + per-entry CSR binary "
-                       "search, 1 thread, median of 3 after 1 warm-up) on a %d x %d Kuhn strip = %d DoFs "
-                       "(%.2f s per assembly)" % (nxs, ny, dofs, t))
+                       "search, 1 thread, median of 5 after 1 warm-up) on a %d x %d Kuhn strip of the C2 "
+                       "workload = %d DoFs (%.3f s per assembly)" % (nxs, ny, dofs, t),
+                omp_value=dofs / t_omp, omp_cores=threads,
+                omp_sample="owner-computes OpenMP variant of the same integrands, %d threads, same strip, "
+                           "median of 5 (%.3f s per assembly)" % (threads, t_omp),
+                cpu_model=_cpu_model(), host_cpus=os.cpu_count())
 
 
 def main():

@@ -1074,7 +1074,7 @@ __device__ __forceinline__ int tile_offset(int c, bool active)
 // Persistent, software-pipelined driver (see the P1 comment above): per wave a sequence of 64-element
 // tiles, memory order [prefetch own data t+1][compute t -> LDS][gathers t+1][stores t].
 // ------------------------------------------------------------------------------------------------
-template <class P>
+template <class P, bool TL>   // TL: tiles come from a.tile_list (interior / halo split), else 0..n_tiles-1
 __global__ void __launch_bounds__(64, 1)
 swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
 {
@@ -1096,7 +1096,8 @@ swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
   double* scratch = lds + IMG + 2;
   // optional tile list (interior / halo-boundary split of a sharded assembly): position -> tile
   auto tile_at = [&](int64_t pos) -> int64_t {
-    return a.tile_list ? int64_t(__builtin_amdgcn_readfirstlane(a.tile_list[pos])) : pos;
+    if constexpr (TL) return int64_t(__builtin_amdgcn_readfirstlane(a.tile_list[pos]));
+    return pos;
   };
   auto elem_of = [&](int64_t pos) {
     const int64_t t0 = a.own_begin + tile_at(pos) * 64;
@@ -1206,7 +1207,10 @@ static hipError_t launch_persistent(const AssembleArgs& a, hipStream_t s)
     ac.n_comp = 1;
     ac.kappa[0] = a.kappa[c];
     ac.vals[0] = a.vals[c];
-    hipLaunchKernelGGL(swipdg_persistent_kernel<P>, dim3(unsigned(G)), dim3(64), lds, s, ac, tiles);
+    if (a.tile_list)
+      hipLaunchKernelGGL((swipdg_persistent_kernel<P, true>), dim3(unsigned(G)), dim3(64), lds, s, ac, tiles);
+    else
+      hipLaunchKernelGGL((swipdg_persistent_kernel<P, false>), dim3(unsigned(G)), dim3(64), lds, s, ac, tiles);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }

@@ -194,6 +194,17 @@ def assemble(grid, kappa, A, prm, elem_index=None, pattern=None):
     return row_ptr, col, val
 
 
+def assemble_owner(grid, kappa, A, prm, pattern=None, threads=1):
+    """Owner-computes OpenMP variant of assemble() (same values up to summation order)."""
+    L = lib()
+    L.or_assemble_swipdg_owner.argtypes = [C.c_void_p] * 8 + [C.c_int]
+    row_ptr, col = pattern if pattern is not None else grid.pattern()
+    val = np.empty(col.shape[0], np.float64)
+    L.or_assemble_swipdg_owner(grid.h, C.byref(kappa), C.byref(A), C.byref(prm), None, _ptr(row_ptr), _ptr(col),
+                               _ptr(val), int(threads))
+    return row_ptr, col, val
+
+
 def block_numbering(grid, subdomain, n_sub):
     sd = np.ascontiguousarray(subdomain, np.int32)
     ei = np.empty(grid.ne, np.int64)

@@ -577,6 +577,37 @@ int or_assemble_swipdg(void* gp, const or_scalar_t* kappa, const or_tensor_t* A,
   return 0;
 }
 
+/* Owner-computes parallel variant (CPU baseline on all host cores): the same local
+ * integrands, but each element assembles only ITS rows (volume, both face blocks of its row side, boundary
+ * terms) so that an OpenMP loop over elements never writes a row twice.  Same values as the sequential
+ * walk up to summation order. */
+int or_assemble_swipdg_owner(void* gp, const or_scalar_t* kappa, const or_tensor_t* A, const or_params_t* p,
+                             const int64_t* elem_index, const int64_t* row_ptr, const int32_t* col, double* val,
+                             int n_threads)
+{
+  grid_t* g = (grid_t*)gp;
+  ctx_t c = {g, kappa, A, p, elem_index, row_ptr, col, val};
+  memset(val, 0, sizeof(double) * (size_t)row_ptr[g->ne * g->nb]);
+#pragma omp parallel for schedule(static) num_threads(n_threads > 0 ? n_threads : 1)
+  for (int64_t e = 0; e < g->ne; ++e) {
+    double L[4][4], EN[4][4], NE[4][4], NN[4][4];
+    local_volume(&c, e, L);
+    scatter(&c, e, e, L);
+    for (int f = 0; f < g->nf; ++f) {
+      const int64_t ne = g->nbr[e * g->nf + f];
+      if (ne >= 0) {
+        local_inner(&c, e, f, ne, L, EN, NE, NN);
+        scatter(&c, e, e, L);
+        scatter(&c, e, ne, EN);
+      } else if (p->boundary_kind == OR_BOUNDARY_DIRICHLET) {
+        local_boundary(&c, e, f, L);
+        scatter(&c, e, e, L);
+      }
+    }
+  }
+  return 0;
+}
+
 /* ------------------------------------------------------------------------------------------------ */
 /* BlockSWIPDG (block-swipdg.hh:262-390): local all-Neumann SWIPDG per subdomain + boundary + coupling */
 /* ------------------------------------------------------------------------------------------------ */

@@ -60,6 +60,9 @@ int64_t or_pattern_nnz(void* g);
 int or_pattern(void* g, const int64_t* elem_index, int64_t* row_ptr, int32_t* col);
 int or_assemble_swipdg(void* g, const or_scalar_t* kappa, const or_tensor_t* A, const or_params_t* p,
                        const int64_t* elem_index, const int64_t* row_ptr, const int32_t* col, double* val);
+int or_assemble_swipdg_owner(void* g, const or_scalar_t* kappa, const or_tensor_t* A, const or_params_t* p,
+                             const int64_t* elem_index, const int64_t* row_ptr, const int32_t* col, double* val,
+                             int n_threads);
 int or_block_numbering(void* g, const int32_t* subdomain, int32_t n_sub, int64_t* elem_index);
 int or_assemble_block_swipdg(void* g, const int32_t* subdomain, int32_t n_sub, const or_scalar_t* kappa,
                              const or_tensor_t* A, const or_params_t* p, const int64_t* elem_index,
