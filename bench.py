@@ -236,7 +236,7 @@ def main():
                        if world > 1 else "single GPU"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "swipdg_persistent_kernel<P1PwcPolicy<1, 0>>",
+                         "kernel": "swipdg_persistent_kernel<P1PwcPolicy<1, 0>, false>",
                          "kernel_ms_avg": kernel_ms, "kernel_ms_avg_max_rank": kernel_ms_max,
                          "algorithmic_bytes_per_launch": alg_bytes},
             "cpu_baseline": cpu,

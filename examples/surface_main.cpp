@@ -27,10 +27,26 @@ int main(int argc, char** argv)
   hdd_structured_desc d{HDD_SIMPLEX, 16, 16, 2, 2, HDD_BOUNDARY_ALL_DIRICHLET, 0, {-1.0, -1.0}, {1.0, 1.0}};
   hdd_grid* g = nullptr;
   if (hdd_grid_create_structured(&d, &g) != HDD_OK) return 1;
-  Problems::Problem esv;   // kappa = 1 (affine part), A = I
+  Problems::Problem esv;   // kappa = 1 (affine part), A = I, Testcase1Force, g_D = g_N = 0
+  esv.force = Problems::ScalarFunction::cos_product(0.5 * M_PI * M_PI, 0.5 * M_PI, 0.5 * M_PI, 0.0, 3);
   {
     Discretizations::BlockSWIPDG block(g, esv);
     block.init();
+    dump(out + "/block_rhs.bin", block.rhs().affine_part());
+    std::printf("rhs components %d\n", block.rhs().num_components());
+    for (const char* id : {"l2", "penalty"}) {
+      const auto P = block.get_product(id);
+      dump(out + "/product_" + std::string(id) + "_row_ptr.bin", P.pattern->row_ptr);
+      auto pv = P.affine_part();
+      pv.resize(size_t(P.pattern->nnz));
+      dump(out + "/product_" + std::string(id) + ".bin", pv);
+    }
+    try {
+      block.get_product("h2");
+      std::printf("unknown product accepted\n");
+    } catch (const std::invalid_argument& e) {
+      std::printf("product rejected: %s\n", e.what());
+    }
     const auto& A = block.system_matrix();
     dump(out + "/block_row_ptr.bin", A.pattern->row_ptr);
     dump(out + "/block_col.bin", A.pattern->col);
@@ -93,6 +109,25 @@ int main(int argc, char** argv)
     std::printf("parametric tensor unexpectedly accepted\n");
   } catch (const std::logic_error& e) {
     std::printf("rejected: %s\n", e.what());
+  }
+  hdd_grid_destroy(g);
+
+  // 4. C5 through the same surface: ESV2007 3d, Q3 on a 3x3x3 hexahedral grid of [-1,1]^3
+  hdd_structured3_desc d3{3, 3, 3, 1, 1, 1, HDD_BOUNDARY_ALL_DIRICHLET, 3, {-1.0, -1.0, -1.0}, {1.0, 1.0, 1.0}};
+  if (hdd_grid_create_structured_3d(&d3, &g) != HDD_OK) return 1;
+  Problems::Problem esv3;
+  esv3.diffusion_tensor = Problems::TensorFunction::identity3d();
+  esv3.force = Problems::ScalarFunction::cos_product(0.75 * M_PI * M_PI, 0.5 * M_PI, 0.5 * M_PI, 0.5 * M_PI, 3);
+  {
+    Discretizations::SWIPDG sw(g, esv3);
+    sw.init();
+    const auto& A = sw.system_matrix();
+    std::printf("hex order %d dofs %lld\n", sw.polynomial_order(), (long long)sw.num_dofs());
+    auto a = A.affine_part(); a.resize(size_t(A.pattern->nnz));
+    dump(out + "/hex_row_ptr.bin", A.pattern->row_ptr);
+    dump(out + "/hex_col.bin", A.pattern->col);
+    dump(out + "/hex_affine.bin", a);
+    dump(out + "/hex_rhs.bin", sw.rhs().affine_part());
   }
   hdd_grid_destroy(g);
   std::printf("surface ok\n");

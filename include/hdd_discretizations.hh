@@ -3,9 +3,11 @@
 // Mirrors, for the assembly hot path, the reference's discretization classes (header-only C++ like the
 // reference itself) on top of the C ABI in hdd.h:
 //   Dune::HDD::LinearElliptic::Discretizations::SWIPDG       (discretizations/swipdg.hh:109-520)
-//     ctor validation (swipdg.hh:172-176), pattern() (201-204), init() (206-512, LHS part),
-//     system_matrix() (base.hh:240-248, an affinely decomposed container: affine part + components with
-//     ParameterFunctional coefficients), freeze_parameter(mu) (base.hh:338-341, 357-361)
+//     ctor validation (swipdg.hh:172-176), pattern() (201-204), init() (206-512: system matrix, right-hand
+//     side, products), system_matrix() / rhs() (base.hh:240-258, affinely decomposed containers: affine part
+//     + components with ParameterFunctional coefficients), freeze_parameter(mu) (base.hh:338-341, 357-361),
+//     available_products() / get_product(id) (base.hh:266-322; "l2", "h1_semi", "elliptic", "boundary_l2",
+//     "penalty", "energy" as registered at swipdg.hh:358-508)
 //   Dune::HDD::LinearElliptic::Discretizations::BlockSWIPDG  (discretizations/block-swipdg.hh:177-846)
 //     num_subdomains() (553), neighbouring_subdomains(ss) (558), localize_vector (567),
 //     globalize_vectors (583), get_local_operator(ss) (625), get_coupling_operator(ss, nn) (639)
@@ -104,11 +106,24 @@ struct ScalarFunction {
   {
     ScalarFunction f; f.kind = HDD_FN_SINUSOID; f.c = a; f.b = b; f.kx = kx; f.ky = ky; f.order = order; return f;
   }
+  // a cos(kx x) cos(ky y) [cos(kz z)]: ESV2007 Testcase1Force (problems/ESV2007.hh:78)
+  static ScalarFunction cos_product(double a, double kx, double ky, double kz, int order)
+  {
+    ScalarFunction f; f.kind = HDD_FN_COS_PRODUCT; f.c = a; f.b = kz; f.kx = kx; f.ky = ky; f.order = order; return f;
+  }
+  bool is_zero() const { return kind == HDD_FN_CONST && c == 0.0; }
 };
 struct TensorFunction {
   int kind = HDD_TENSOR_CONST;
-  double c[3] = {1.0, 0.0, 1.0};
-  std::vector<double> per_element;   // ISO: [ne]; SYM: [3][ne]
+  double c[6] = {1.0, 0.0, 1.0, 0.0, 0.0, 0.0};   // 2d a11 a12 a22; 3d a11 a12 a13 a22 a23 a33 (see identity3d)
+  std::vector<double> per_element;   // ISO: [ne]; SYM: [3 | 6][ne]
+  static TensorFunction identity3d()
+  {
+    TensorFunction t;
+    const double id[6] = {1.0, 0.0, 0.0, 1.0, 0.0, 1.0};
+    std::copy(id, id + 6, t.c);
+    return t;
+  }
   static TensorFunction identity() { return TensorFunction(); }
   static TensorFunction isotropic(std::vector<double> v)
   {
@@ -128,6 +143,10 @@ struct Problem {
   TensorFunction diffusion_tensor;
   bool diffusion_tensor_parametric = false;
   bool diffusion_tensor_empty = false;
+  // right-hand side data (non-parametric): force, Dirichlet and Neumann values (zero = absent)
+  ScalarFunction force = ScalarFunction::constant(0.0);
+  ScalarFunction dirichlet = ScalarFunction::constant(0.0);
+  ScalarFunction neumann = ScalarFunction::constant(0.0);
 };
 }  // namespace Problems
 
@@ -175,6 +194,36 @@ class AffinelyDecomposedMatrix {
   }
 };
 
+// AffinelyDecomposedContainer<Vector> (the right-hand side)
+class AffinelyDecomposedVector {
+ public:
+  std::shared_ptr<internal::DeviceArray<double>> affine;
+  std::vector<std::shared_ptr<internal::DeviceArray<double>>> comps;
+  std::vector<Pymor::ParameterFunctional> coefficients;
+  int64_t size = 0;
+  bool has_affine_part() const { return bool(affine); }
+  int num_components() const { return int(comps.size()); }
+  std::vector<double> affine_part() const { auto h = affine->download(); h.resize(size_t(size)); return h; }
+  std::vector<double> component(int q) const { auto h = comps.at(q)->download(); h.resize(size_t(size)); return h; }
+};
+
+namespace internal {
+inline int degree_of(const hdd_grid_info& gi)
+{
+  if (gi.elem_type != HDD_HEX) return 1;
+  int p = 1;
+  while ((p + 1) * (p + 1) * (p + 1) < gi.nb) ++p;
+  return p;
+}
+// LocalEvaluation::SWIPDG::internal::{inner,boundary}_sigma(p), default_beta(d)
+inline hdd_swipdg_params swipdg_params(int p, int dim)
+{
+  const double si = p <= 1 ? 8.0 : (p == 2 ? 20.0 : (p == 3 ? 38.0 : 50.0));
+  const double sb = p <= 1 ? 14.0 : (p == 2 ? 38.0 : (p == 3 ? 74.0 : 99.0));
+  return hdd_swipdg_params{si, sb, 1.0 / (dim - 1), -1, -1};
+}
+}  // namespace internal
+
 class SWIPDG {
  public:
   // grid: the (multiscale) grid provider; the boundary info is part of the grid (AllDirichlet /
@@ -189,6 +238,7 @@ class SWIPDG {
     internal::check(hdd_ctx_create(hip_device, &ctx_), "hdd_ctx_create");
     internal::check(hdd_local_create(grid, 0, info_.n_subdomains, &local_), "hdd_local_create");
     internal::check(hdd_local_get_info(local_, &linfo_), "hdd_local_get_info");
+    degree_ = internal::degree_of(info_);
     build_pattern();
   }
   virtual ~SWIPDG()
@@ -201,12 +251,14 @@ class SWIPDG {
 
   const Pattern& pattern() const { return *pattern_; }
 
-  // assembles the LHS (every diffusion-factor component + the affine part) on the device; idempotent
+  // assembles the system matrix (every diffusion-factor component + the affine part), the right-hand side
+  // and the requested products on the device; idempotent (container_based_initialized_, swipdg.hh:208)
   void init()
   {
     if (initialized_) return;
     const int64_t n = linfo_.n_local;
-    std::vector<double> coords(size_t(2 * info_.nvpe * n));
+    const int dim = info_.dim;
+    std::vector<double> coords(size_t(dim * info_.nvpe * n));
     std::vector<int32_t> nbrs(size_t(info_.nfaces * n));
     std::vector<uint32_t> finfo(static_cast<size_t>(n));
     internal::check(hdd_local_fill(local_, coords.data(), nbrs.data(), finfo.data(), nullptr, nullptr), "hdd_local_fill");
@@ -215,26 +267,79 @@ class SWIPDG {
     d_finfo_ = internal::DeviceArray<uint32_t>(finfo);
     const auto& T = problem_.diffusion_tensor;
     if (T.kind != HDD_TENSOR_CONST) d_tensor_ = internal::DeviceArray<double>(T.per_element);
-    hdd_mesh m{info_.elem_type, 0, n, linfo_.own_begin, linfo_.own_end, d_coords_.get(), d_nbrs_.get(), d_finfo_.get()};
-    hdd_tensor_fn A{T.kind, 0, {T.c[0], T.c[1], T.c[2]}, d_tensor_.get()};
-    hdd_swipdg_params prm{8.0, 14.0, 1.0 / (2 - 1), -1, -1};   // inner/boundary_sigma(1), default_beta(2)
+    mesh_ = hdd_mesh{info_.elem_type, degree_, n, linfo_.own_begin, linfo_.own_end, d_coords_.get(), d_nbrs_.get(),
+                     d_finfo_.get()};
+    tensor_ = hdd_tensor_fn{T.kind, 0, {T.c[0], T.c[1], T.c[2], T.c[3], T.c[4], T.c[5]}, d_tensor_.get()};
+    prm_ = internal::swipdg_params(degree_, dim);
     const hdd_csr pat = pattern_->csr();
     matrix_.pattern = pattern_;
     matrix_.ctx = ctx_;
     matrix_.coefficients = problem_.diffusion_factor.coefficients;
     auto assemble = [&](const Problems::ScalarFunction& f) {
       auto vals = std::make_shared<internal::DeviceArray<double>>(size_t(pattern_->nnz) + 1);
-      std::unique_ptr<internal::DeviceArray<double>> pe;
-      if (f.kind == HDD_FN_PER_ELEM) pe.reset(new internal::DeviceArray<double>(f.per_element));
-      hdd_scalar_fn k{f.kind, f.order, f.c, f.b, f.kx, f.ky, pe ? pe->get() : nullptr};
+      Fn k(f);
       double* v = vals->get();
-      internal::check(hdd_swipdg_assemble(ctx_, &m, &k, 1, &A, &prm, &pat, &v, nullptr), "hdd_swipdg_assemble");
+      internal::check(hdd_swipdg_assemble(ctx_, &mesh_, &k.fn, 1, &tensor_, &prm_, &pat, &v, nullptr),
+                      "hdd_swipdg_assemble");
       internal::hip_check(hipDeviceSynchronize(), "init");
       return vals;
     };
     for (const auto& c : problem_.diffusion_factor.components) matrix_.comps.push_back(assemble(c));
     if (problem_.diffusion_factor.has_affine_part) matrix_.affine = assemble(problem_.diffusion_factor.affine_part);
+    assemble_rhs();
     initialized_ = true;
+  }
+
+  const AffinelyDecomposedMatrix& system_matrix() const
+  {
+    if (!initialized_) throw std::logic_error("system_matrix(): call init() first");
+    return matrix_;
+  }
+  const AffinelyDecomposedVector& rhs() const
+  {
+    if (!initialized_) throw std::logic_error("rhs(): call init() first");
+    return rhs_;
+  }
+
+  // base.hh:266-322: "l2", "h1_semi", "elliptic", "boundary_l2", "penalty", "energy"
+  std::vector<std::string> available_products() const
+  {
+    return {"l2", "h1_semi", "elliptic", "boundary_l2", "penalty", "energy"};
+  }
+  AffinelyDecomposedMatrix get_product(const std::string& id)
+  {
+    init();
+    if (id == "energy") return matrix_;
+    int kind;
+    if (id == "l2") kind = HDD_PRODUCT_L2;
+    else if (id == "h1_semi") kind = HDD_PRODUCT_H1_SEMI;
+    else if (id == "elliptic") kind = HDD_PRODUCT_ELLIPTIC;
+    else if (id == "boundary_l2") kind = HDD_PRODUCT_BOUNDARY_L2;
+    else if (id == "penalty") kind = HDD_PRODUCT_PENALTY;
+    else throw std::invalid_argument("Product '" + id + "' not available!");
+    const bool volume = kind != HDD_PRODUCT_PENALTY;
+    std::shared_ptr<const Pattern> P = volume ? volume_pattern() : std::shared_ptr<const Pattern>(pattern_);
+    const hdd_csr pat = P->csr();
+    AffinelyDecomposedMatrix out;
+    out.pattern = P;
+    out.ctx = ctx_;
+    auto run = [&](const Problems::ScalarFunction& f) {
+      auto vals = std::make_shared<internal::DeviceArray<double>>(size_t(P->nnz) + 1);
+      Fn k(f);
+      internal::check(hdd_product_assemble(ctx_, &mesh_, kind, &k.fn, &tensor_, &prm_, &pat, vals->get(), nullptr),
+                      "hdd_product_assemble");
+      internal::hip_check(hipDeviceSynchronize(), "get_product");
+      return vals;
+    };
+    const auto& K = problem_.diffusion_factor;
+    if (kind == HDD_PRODUCT_ELLIPTIC || kind == HDD_PRODUCT_PENALTY) {   // affinely decomposed like kappa
+      out.coefficients = K.coefficients;
+      for (const auto& c : K.components) out.comps.push_back(run(c));
+      if (K.has_affine_part) out.affine = run(K.affine_part);
+    } else {
+      out.affine = run(Problems::ScalarFunction::constant(1.0));
+    }
+    return out;
   }
 
   const AffinelyDecomposedMatrix& system_matrix() const
@@ -245,24 +350,89 @@ class SWIPDG {
   int64_t num_dofs() const { return pattern_->rows; }
   hdd_ctx* context() const { return ctx_; }
   const hdd_grid* grid() const { return grid_; }
+  int polynomial_order() const { return degree_; }
 
  protected:
+  // a scalar function bound to the device (per-element values uploaded, kept alive with the descriptor)
+  struct Fn {
+    hdd_scalar_fn fn;
+    std::unique_ptr<internal::DeviceArray<double>> pe;
+    explicit Fn(const Problems::ScalarFunction& f)
+    {
+      if (f.kind == HDD_FN_PER_ELEM) pe.reset(new internal::DeviceArray<double>(f.per_element));
+      fn = hdd_scalar_fn{f.kind, f.order, f.c, f.b, f.kx, f.ky, pe ? pe->get() : nullptr};
+    }
+  };
+
+  // swipdg.hh:251-347: affine part = L2Volume(f) + DirichletBoundarySWIPDG(kappa_aff, A, g_D) + L2Face(g_N);
+  // component q = DirichletBoundarySWIPDG(kappa_q, A, g_D) with kappa's coefficient theta_q
+  void assemble_rhs()
+  {
+    const auto& P = problem_;
+    const int64_t size = pattern_->rows;
+    rhs_.size = size;
+    rhs_.coefficients.clear();
+    auto run = [&](const Problems::ScalarFunction* force, const Problems::ScalarFunction* kappa) {
+      auto b = std::make_shared<internal::DeviceArray<double>>(size_t(size) + 1);
+      std::unique_ptr<Fn> f, k, d, nm;
+      if (force && !force->is_zero()) f.reset(new Fn(*force));
+      if (kappa && !P.dirichlet.is_zero()) { k.reset(new Fn(*kappa)); d.reset(new Fn(P.dirichlet)); }
+      if (force && !P.neumann.is_zero()) nm.reset(new Fn(P.neumann));
+      internal::check(hdd_swipdg_rhs(ctx_, &mesh_, f ? &f->fn : nullptr, k ? &k->fn : nullptr, &tensor_,
+                                     d ? &d->fn : nullptr, nm ? &nm->fn : nullptr, &prm_, b->get(), nullptr),
+                      "hdd_swipdg_rhs");
+      internal::hip_check(hipDeviceSynchronize(), "rhs");
+      return b;
+    };
+    const auto& K = P.diffusion_factor;
+    rhs_.affine = run(&P.force, K.has_affine_part ? &K.affine_part : nullptr);
+    if (!P.dirichlet.is_zero())
+      for (int q = 0; q < K.num_components(); ++q) {
+        rhs_.comps.push_back(run(nullptr, &K.components[q]));
+        rhs_.coefficients.push_back(K.coefficients[q]);
+      }
+  }
+
+  std::shared_ptr<const Pattern> volume_pattern()
+  {
+    if (volume_pattern_) return volume_pattern_;
+    auto P = std::make_shared<Pattern>();
+    const int64_t n = linfo_.n_local, own = linfo_.own_end - linfo_.own_begin;
+    std::vector<int32_t> nbrs(size_t(info_.nfaces * n));
+    internal::check(hdd_local_fill(local_, nullptr, nbrs.data(), nullptr, nullptr, nullptr), "hdd_local_fill");
+    internal::check(hdd_dg_pattern_count(0, info_.nb, n, linfo_.own_begin, linfo_.own_end, nbrs.data(), &P->nnz),
+                    "hdd_dg_pattern_count");
+    P->rows = own * info_.nb;
+    P->cols = info_.n_elements * info_.nb;
+    P->row_ptr.resize(size_t(P->rows + 1));
+    P->col.resize(size_t(P->nnz));
+    P->elem_ptr.resize(size_t(own + 1));
+    internal::check(hdd_dg_pattern_fill(0, info_.nb, n, linfo_.own_begin, linfo_.own_end, nbrs.data(), nullptr,
+                                        P->row_ptr.data(), P->col.data(), P->elem_ptr.data()), "hdd_dg_pattern_fill");
+    P->d_row_ptr = internal::DeviceArray<int64_t>(P->row_ptr);
+    P->d_col = internal::DeviceArray<int32_t>(P->col);
+    P->d_elem_ptr = internal::DeviceArray<int64_t>(P->elem_ptr);
+    volume_pattern_ = P;
+    return P;
+  }
+
   void build_pattern()
   {
     auto P = std::make_shared<Pattern>();
     const int64_t n = linfo_.n_local;
     std::vector<int32_t> nbrs(size_t(info_.nfaces * n));
     internal::check(hdd_local_fill(local_, nullptr, nbrs.data(), nullptr, nullptr, nullptr), "hdd_local_fill");
-    internal::check(hdd_pattern_count(info_.elem_type, n, linfo_.own_begin, linfo_.own_end, nbrs.data(), &P->nnz),
-                    "hdd_pattern_count");
+    internal::check(hdd_dg_pattern_count(info_.nfaces, info_.nb, n, linfo_.own_begin, linfo_.own_end, nbrs.data(),
+                                         &P->nnz), "hdd_dg_pattern_count");
     const int64_t own = linfo_.own_end - linfo_.own_begin;
     P->rows = own * info_.nb;
     P->cols = info_.n_elements * info_.nb;
     P->row_ptr.resize(size_t(P->rows + 1));
     P->col.resize(size_t(P->nnz));
     P->elem_ptr.resize(size_t(own + 1));
-    internal::check(hdd_pattern_fill(info_.elem_type, n, linfo_.own_begin, linfo_.own_end, nbrs.data(), nullptr,
-                                     P->row_ptr.data(), P->col.data(), P->elem_ptr.data()), "hdd_pattern_fill");
+    internal::check(hdd_dg_pattern_fill(info_.nfaces, info_.nb, n, linfo_.own_begin, linfo_.own_end, nbrs.data(),
+                                        nullptr, P->row_ptr.data(), P->col.data(), P->elem_ptr.data()),
+                    "hdd_dg_pattern_fill");
     P->d_row_ptr = internal::DeviceArray<int64_t>(P->row_ptr);
     P->d_col = internal::DeviceArray<int32_t>(P->col);
     P->d_elem_ptr = internal::DeviceArray<int64_t>(P->elem_ptr);
@@ -276,10 +446,16 @@ class SWIPDG {
   hdd_ctx* ctx_ = nullptr;
   hdd_local* local_ = nullptr;
   std::shared_ptr<Pattern> pattern_;
+  std::shared_ptr<const Pattern> volume_pattern_;
   internal::DeviceArray<double> d_coords_, d_tensor_;
   internal::DeviceArray<int32_t> d_nbrs_;
   internal::DeviceArray<uint32_t> d_finfo_;
+  hdd_mesh mesh_{};
+  hdd_tensor_fn tensor_{};
+  hdd_swipdg_params prm_{};
+  int degree_ = 1;
   AffinelyDecomposedMatrix matrix_;
+  AffinelyDecomposedVector rhs_;
   bool initialized_ = false;
 };
 

@@ -37,6 +37,13 @@ def test_cpp_surface_against_oracle():
         lrp, lcol, lval = ld("local0_row_ptr", np.int64), ld("local0_col", np.int32), ld("local0_affine", np.float64)
         crp, ccol, cval = ld("coupling0_row_ptr", np.int64), ld("coupling0_col", np.int32), ld("coupling0_affine", np.float64)
         osa, osc, osf = ld("os_affine", np.float64), ld("os_comp0", np.float64), ld("os_frozen_0.3", np.float64)
+        brhs = ld("block_rhs", np.float64)
+        pl2_rp, pl2 = ld("product_l2_row_ptr", np.int64), ld("product_l2", np.float64)
+        ppen_rp, ppen = ld("product_penalty_row_ptr", np.int64), ld("product_penalty", np.float64)
+        hrp, hcol, hval = ld("hex_row_ptr", np.int64), ld("hex_col", np.int32), ld("hex_affine", np.float64)
+        hrhs = ld("hex_rhs", np.float64)
+        assert "rhs components 0" in r.stdout and "product rejected: Product 'h2' not available!" in r.stdout
+        assert "hex order 3 dofs 1728" in r.stdout
     # oracle: block-SWIPDG on the same multiscale grid
     g = H.Grid.structured(H.SIMPLEX, 16, 16, (-1, -1), (1, 1), px=2, py=2)
     pc, pev, psd = g.connectivity()
@@ -49,6 +56,13 @@ def test_cpp_surface_against_oracle():
     ei, rp, col, val = O.assemble_block(og, sub, 4, O.scalar(), O.tensor(), O.params())
     assert np.array_equal(brp, rp) and np.array_equal(bcol, col)
     assert compare_rows(rp, bval, val, 1e-12)[1]
+    # right-hand side and products through the surface (block numbering = elem_index ei)
+    b = O.rhs_swipdg(og, force=O.esv2007_force(), elem_index=ei)
+    assert np.max(np.abs(brhs - b)) <= 1e-12 * np.max(np.abs(b))
+    for prod_rp, prod, kind in [(pl2_rp, pl2, O.PRODUCT_L2), (ppen_rp, ppen, O.PRODUCT_PENALTY)]:
+        orp, _, oval = O.product(og, kind, elem_index=ei)
+        assert np.array_equal(prod_rp, orp)
+        assert compare_rows(orp, prod, oval, 1e-12)[1]
     A = O.to_scipy(rp, col, val).tocsr()
     a0, b0 = g.subdomain_range(0, 1)
     n0 = int(nbs[0])
@@ -69,3 +83,10 @@ def test_cpp_surface_against_oracle():
     _, _, vc = O.assemble(g2, O.scalar(O.FN_SINUSOID, 0.0, -0.75, kx, ky, order=3), O.tensor(), O.params())
     assert compare_rows(rp2, osa, va, 1e-12)[1] and compare_rows(rp2, osc, vc, 1e-12)[1]
     assert compare_rows(rp2, osf, va + 0.3 * vc, 1e-12)[1]
+    # C5 through the surface: Q3 hexahedra, matrix and right-hand side vs the Q_p oracle
+    q = O.QpGrid(3, 3, (3, 3, 3), (-1, -1, -1), (1, 1, 1))
+    orp, ocol, oval = O.qp_assemble(q, O.scalar(), O.qp_tensor(), O.qp_params(q))
+    assert np.array_equal(hrp, orp) and np.array_equal(hcol, ocol)
+    assert compare_rows(orp, hval, oval, 1e-12)[1]
+    ob = O.qp_rhs_swipdg(q, force=O.esv2007_force(3))
+    assert np.max(np.abs(hrhs - ob)) <= 1e-12 * np.max(np.abs(ob))
