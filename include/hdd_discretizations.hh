@@ -207,7 +207,7 @@ class AffinelyDecomposedVector {
   std::vector<double> component(int q) const { auto h = comps.at(q)->download(); h.resize(size_t(size)); return h; }
 };
 
-namespace internal {
+namespace detail {
 inline int degree_of(const hdd_grid_info& gi)
 {
   if (gi.elem_type != HDD_HEX) return 1;
@@ -222,7 +222,7 @@ inline hdd_swipdg_params swipdg_params(int p, int dim)
   const double sb = p <= 1 ? 14.0 : (p == 2 ? 38.0 : (p == 3 ? 74.0 : 99.0));
   return hdd_swipdg_params{si, sb, 1.0 / (dim - 1), -1, -1};
 }
-}  // namespace internal
+}  // namespace detail
 
 class SWIPDG {
  public:
@@ -238,7 +238,7 @@ class SWIPDG {
     internal::check(hdd_ctx_create(hip_device, &ctx_), "hdd_ctx_create");
     internal::check(hdd_local_create(grid, 0, info_.n_subdomains, &local_), "hdd_local_create");
     internal::check(hdd_local_get_info(local_, &linfo_), "hdd_local_get_info");
-    degree_ = internal::degree_of(info_);
+    degree_ = detail::degree_of(info_);
     build_pattern();
   }
   virtual ~SWIPDG()
@@ -270,7 +270,7 @@ class SWIPDG {
     mesh_ = hdd_mesh{info_.elem_type, degree_, n, linfo_.own_begin, linfo_.own_end, d_coords_.get(), d_nbrs_.get(),
                      d_finfo_.get()};
     tensor_ = hdd_tensor_fn{T.kind, 0, {T.c[0], T.c[1], T.c[2], T.c[3], T.c[4], T.c[5]}, d_tensor_.get()};
-    prm_ = internal::swipdg_params(degree_, dim);
+    prm_ = detail::swipdg_params(degree_, dim);
     const hdd_csr pat = pattern_->csr();
     matrix_.pattern = pattern_;
     matrix_.ctx = ctx_;
@@ -342,11 +342,6 @@ class SWIPDG {
     return out;
   }
 
-  const AffinelyDecomposedMatrix& system_matrix() const
-  {
-    if (!initialized_) throw std::logic_error("system_matrix(): call init() first");
-    return matrix_;
-  }
   int64_t num_dofs() const { return pattern_->rows; }
   hdd_ctx* context() const { return ctx_; }
   const hdd_grid* grid() const { return grid_; }

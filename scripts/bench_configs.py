@@ -11,6 +11,10 @@
       16.8 M DoFs, 7.4 G nnz, 59 GB of values resident in HBM), DG Q3 (64 basis functions), kappa = 1, A = I,
       AllDirichlet; f64 MFMA kernel (hex_qp.hip).  The device pattern build is timed separately (the
       reference builds its pattern outside init(), swipdg.hh:169).
+  c5s ESV2007 3d 256^3 (16.8 M hexahedra, 1.07 G DoFs, 4.8e11 nnz = 3.8 TB of values: larger than HBM), Q3,
+      streamed-slab mode: the grid is cut into x-slabs (rank-local meshes with face ghosts)
+      whose row blocks are assembled in turn into one rotating value buffer; the time is one pass over all
+      slabs (values of earlier slabs are overwritten -- a throughput measurement, nothing is skipped).
 Prints one JSON line per config."""
 import argparse
 import json
@@ -128,6 +132,53 @@ def c5(args):
                 fp64_peak_TF=78.6, mfma_frac=mfma_flops / t / 78.6e12)
 
 
+def c5s(args):
+    import torch
+    import hdd_amd as H
+    n, deg, slabs = (args.n or 256), args.degree, args.slabs
+    grid = H.Grid.structured3d((n, n, n), (-1, -1, -1), (1, 1, 1), p=(slabs, 1, 1), degree=deg)
+    ctx = H.Context(0)
+    prm = H.params_for(deg, 3)
+    t0 = time.perf_counter()
+    parts = []
+    for sl in range(slabs):
+        loc = grid.local(sl, sl + 1)
+        dm = H.DeviceMesh(loc)
+        ep = torch.empty(loc.n_own + 1, dtype=torch.int64, device="cuda")
+        nnz = H.C.c_int64()
+        H._check(H.lib().hdd_pattern_elem_ptr_device(ctx.h, H.C.byref(dm.t), grid.nb, ep.data_ptr(),
+                                                    H.C.byref(nnz), None), "hdd_pattern_elem_ptr_device")
+        csr = H.CsrT(grid.nb * loc.n_own, grid.ne * grid.nb, nnz.value, None, None, ep.data_ptr())
+        nbr = loc.neighbors[:, loc.own_begin:loc.own_end]
+        parts.append(dict(dm=dm, ep=ep, csr=csr, nnz=nnz.value, n_own=loc.n_own,
+                          inner=int((nbr >= 0).sum()), dirichlet=int((nbr == H.NBR_DIRICHLET).sum())))
+        loc.coords = loc.neighbors = None   # host copies no longer needed
+    t_setup = time.perf_counter() - t0
+    vals = torch.empty(max(p["nnz"] for p in parts), dtype=torch.float64, device="cuda")
+    kap = H.ScalarFn(H.FN_CONST, 0, 1.0, 0.0, 0.0, 0.0, None)
+    ten = H.tensor_fn(dim=3)
+    ptrs = (H.C.c_void_p * 1)(vals.data_ptr())
+    s = torch.cuda.current_stream().cuda_stream
+
+    def sweep():
+        for p in parts:
+            H._check(H.lib().hdd_swipdg_assemble(ctx.h, H.C.byref(p["dm"].t), H.C.byref(kap), 1, H.C.byref(ten),
+                                                 H.C.byref(prm), H.C.byref(p["csr"]), ptrs, H.C.c_void_p(s)),
+                     "hdd_swipdg_assemble")
+    t = timed(sweep, max(1, args.steps // 5), 1)
+    nnz = sum(p["nnz"] for p in parts)
+    dofs = grid.ne * grid.nb
+    n_own = sum(p["n_own"] for p in parts)
+    inner = sum(p["inner"] for p in parts)
+    nif, nbf = inner // 2, sum(p["dirichlet"] for p in parts)
+    nq, nqf, nb = deg ** 3, (deg + 1) ** 2, grid.nb
+    alg_flops = n_own * 2 * nb * nb * nq * 3 + nif * 24 * nb * nb * nqf + nbf * 6 * nb * nb * nqf
+    return dict(config="c5s_esv2007_3d_q%d_%d^3_streamed_%d_slabs" % (deg, n, slabs), dofs=dofs, nnz=nnz,
+                values_TB=8 * nnz / 1e12, rotating_buffer_GB=8 * vals.numel() / 1e9, setup_s=t_setup,
+                assembly_s=t, assembled_dofs_per_s=dofs / t, values_written_GBps=8 * nnz / t / 1e9,
+                alg_TFLOPs=alg_flops / t / 1e12, fp64_peak_TF=78.6)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("configs", nargs="*", default=["c3", "c4"])
@@ -136,11 +187,12 @@ def main():
     ap.add_argument("--samples", type=int, default=128)
     ap.add_argument("--n", type=int, default=0)
     ap.add_argument("--degree", type=int, default=3)
+    ap.add_argument("--slabs", type=int, default=64)
     args = ap.parse_args()
     import torch
     torch.cuda.set_device(0)
     for c in args.configs:
-        print(json.dumps(dict(c3=c3, c4=c4, c5=c5)[c](args)), flush=True)
+        print(json.dumps(dict(c3=c3, c4=c4, c5=c5, c5s=c5s)[c](args)), flush=True)
 
 
 if __name__ == "__main__":
