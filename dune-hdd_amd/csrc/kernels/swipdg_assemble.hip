@@ -33,6 +33,13 @@
 #ifndef HDD_MIN_WAVES_PER_EU
 #define HDD_MIN_WAVES_PER_EU 4
 #endif
+// profiling ablations (HDD_DEBUG_FLAGS at run time) exist only in a library built with -DHDD_ABLATION
+// (scripts/ablate.py): 1 = skip compute, 2 = drop the value stores, 4 = skip the neighbour gathers
+#ifdef HDD_ABLATION
+#define HDD_ABL(a, bit) (((a).debug_flags & (bit)) != 0)
+#else
+#define HDD_ABL(a, bit) false
+#endif
 
 namespace hdd {
 namespace dev {
@@ -850,6 +857,13 @@ template <class E, int NQV, int NQF, int TK, int KK>
 struct GenericPolicy {
   static constexpr int NB = E::NB, NF = E::NF, NV = E::NV;
   static constexpr int RB = (NF + 1) * NB * NB;
+  // workgroups (single-wave tiles) per CU and the register cap: simplices (18 KB tiles) run 8 per CU at
+  // <= 256 registers (2 waves / SIMD hide the sinusoid's VALU latency: C3 0.278 -> 0.241 ms per component,
+  // profiles/r01/s2/ab1.log); quads are LDS-bound at 3 per CU and keep the full register file (capping them
+  // at 256 spills: 0.84 -> 1.30 ms)
+  static constexpr int WGCU = NB == 4 ? 3 : 8;
+  static constexpr int MINW = NB == 4 ? 1 : 2;
+  static constexpr bool PAD = NB == 4;   // padded LDS image for uniform tiles (see the persistent kernel)
   using Own = GOwn<E>;
   using Gat = GGat<E>;
 
@@ -1039,11 +1053,164 @@ struct GenericPolicy {
   }
 };
 
+// ------------------------------------------------------------------------------------------------
+// Q1 on parallelograms, piecewise-constant coefficients: closed-form face integrals.
+//
+// On an affine quadrilateral the trace of a Q1 function on a face is linear in the face parameter s and
+// so is (A grad phi) . n, so every face integrand of SWIPDG::Inner / BoundaryLHS is a quadratic in s: the
+// reference's 2-point Gauss rule integrates it exactly, and so does the closed form used here,
+//   int (A grad phi_j . n) phi_i = |F| (p_i alpha_j + q_i beta_j),  int phi_i phi_j = |F| M_ij,
+// with alpha_j / beta_j the values at the face's first / second vertex, (p, q) = (1/3, 1/6) for the first
+// face vertex and (1/6, 1/3) for the second, M = [[1/3, 1/6], [1/6, 1/3]] on the face vertices.  The
+// vertex values are ghat_j(v) . m with m = J^{-1} A n (one 2-vector per face and side) and the reference
+// gradients ghat_j(v) compile-time constants in {0, +-1}.  The volume term keeps the reference's 1-point
+// rule (integrand order 0 for piecewise-constant data): S_ij = |det J| kappa ghat_i(c)^T J^{-1} A J^{-T}
+// ghat_j(c).  Results equal the quadrature form up to rounding (GPU parity tolerance 1e-12 of the row
+// maximum).  Neighbour quantities are in role coordinates (A = my face vertex a, B = b, C = the
+// neighbour vertex next to A), as in GenericPolicy.
+// ------------------------------------------------------------------------------------------------
+template <int TK, int KK>
+struct Q1PwcPolicy : GenericPolicy<Cube, 1, 2, TK, KK> {
+  using Base = GenericPolicy<Cube, 1, 2, TK, KK>;
+  using E = Cube;
+  static constexpr int NB = 4, NF = 4;
+  using Own = typename Base::Own;
+  using Gat = typename Base::Gat;
+
+  // reference Q1 gradient of basis k at the reference point (x, y): component d
+  __host__ __device__ static constexpr double gh(int k, int d, double x, double y)
+  {
+    return d == 0 ? ((k & 1) ? 1.0 : -1.0) * ((k & 2) ? y : 1.0 - y)
+                  : ((k & 2) ? 1.0 : -1.0) * ((k & 1) ? x : 1.0 - x);
+  }
+
+  __device__ static void compute(const AssembleArgs& a, int64_t e, const Own& o, const Gat& gt, double* img)
+  {
+    const double j00 = o.X[1] - o.X[0], j01 = o.X[2] - o.X[0], j10 = o.Y[1] - o.Y[0], j11 = o.Y[2] - o.Y[0];
+    const double det = j00 * j11 - j01 * j10;
+    const double id = rcp_nr(det);
+    const double i00 = j11 * id, i01 = -j01 * id, i10 = -j10 * id, i11 = j00 * id;   // J^{-1}
+    const double adet = fabs(det);
+    const double osgn = det > 0.0 ? 1.0 : -1.0;
+    int pos_self = 0, pos[NF];
+#pragma unroll
+    for (int f = 0; f < NF; ++f) pos_self += (o.nbr[f] >= 0 && o.nbr[f] < e);
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+      int p = (e < o.nbr[f]) ? 1 : 0;
+#pragma unroll
+      for (int q = 0; q < NF; ++q) p += (o.nbr[q] >= 0 && o.nbr[q] < o.nbr[f]);
+      pos[f] = p;
+    }
+    const int rowlen = (Base::n_interior(o) + 1) * NB;
+    const Tensor A = o.A;
+    const double ke = o.ke;
+    double S[NB][NB];
+    {   // LocalEvaluation::Elliptic, 1-point rule: K = J^{-1} A J^{-T}
+      const double p00 = i00 * A.a00 + i01 * A.a01, p01 = i00 * A.a01 + i01 * A.a11;
+      const double p10 = i10 * A.a00 + i11 * A.a01, p11 = i10 * A.a01 + i11 * A.a11;
+      const double k00 = p00 * i00 + p01 * i01, k01 = p00 * i10 + p01 * i11, k11 = p10 * i10 + p11 * i11;
+      const double fac = adet * ke;
+#pragma unroll
+      for (int i = 0; i < NB; ++i)
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+          const double gix = gh(i, 0, 0.5, 0.5), giy = gh(i, 1, 0.5, 0.5);
+          const double gjx = gh(j, 0, 0.5, 0.5), gjy = gh(j, 1, 0.5, 0.5);
+          S[i][j] = fac * (gix * (k00 * gjx + k01 * gjy) + giy * (k01 * gjx + k11 * gjy));
+        }
+    }
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+      const int32_t n = o.nbr[f];
+      if (n <= HDD_NBR_NEUMANN) continue;
+      const int fa = E::fv(f, 0), fb = E::fv(f, 1);
+      const double ax = E::rv(fa, 0), ay = E::rv(fa, 1), bx = E::rv(fb, 0), by = E::rv(fb, 1);
+      const double Ax = o.X[fa], Ay = o.Y[fa], Bx = o.X[fb], By = o.Y[fb];
+      const double tx = Bx - Ax, ty = By - Ay;
+      const double il = rsq_nr(tx * tx + ty * ty);
+      const double len = (tx * tx + ty * ty) * il;
+      const double nsc = E::face_sign(f) * osgn * il;
+      const double nx = ty * nsc, ny = -tx * nsc;
+      const double anx = A.a00 * nx + A.a01 * ny, any = A.a01 * nx + A.a11 * ny;
+      const double dm = anx * nx + any * ny;
+      const double ihp = a.beta == 1.0 ? il : rcp_nr(pow(len, a.beta));
+      const double mx = i00 * anx + i01 * any, my = i10 * anx + i11 * any;   // J^{-1} A n
+      double al[NB], be[NB];   // (A grad phi_k . n) at my face vertices a, b
+#pragma unroll
+      for (int k = 0; k < NB; ++k) {
+        al[k] = gh(k, 0, ax, ay) * mx + gh(k, 1, ax, ay) * my;
+        be[k] = gh(k, 0, bx, by) * mx + gh(k, 1, bx, by) * my;
+      }
+      const double L3 = len * (1.0 / 3.0), L6 = len * (1.0 / 6.0);
+      // int (A grad phi_j . n) phi_i  and  int phi_i phi_j
+      auto I1 = [&](int j, int i) { return i == fa ? L3 * al[j] + L6 * be[j] : (i == fb ? L6 * al[j] + L3 * be[j] : 0.0); };
+      auto MM = [&](int i, int j) {
+        return (i == fa || i == fb) && (j == fa || j == fb) ? (i == j ? L3 : L6) : 0.0;
+      };
+      if (n >= 0) {
+        const double Cx = gt.Cx[f], Cy = gt.Cy[f];
+        const Tensor Ap = gt.Ap[f];
+        const double kn = gt.kn[f];
+        // neighbour in role coordinates: A = (0,0), B = (1,0), C = (0,1)
+        const double h00 = Bx - Ax, h01 = Cx - Ax, h10 = By - Ay, h11 = Cy - Ay;
+        const double hid = rcp_nr(h00 * h11 - h01 * h10);
+        const double anpx = Ap.a00 * nx + Ap.a01 * ny, anpy = Ap.a01 * nx + Ap.a11 * ny;
+        const double dp = anpx * nx + anpy * ny;
+        const double mpx = (h11 * anpx - h01 * anpy) * hid, mpy = (-h10 * anpx + h00 * anpy) * hid;
+        double alp[NB], bep[NB];   // (A+ grad phi+_r . n) at A (0,0) and B (1,0)
+#pragma unroll
+        for (int r = 0; r < NB; ++r) {
+          alp[r] = gh(r, 0, 0.0, 0.0) * mpx + gh(r, 1, 0.0, 0.0) * mpy;
+          bep[r] = gh(r, 0, 1.0, 0.0) * mpx + gh(r, 1, 1.0, 0.0) * mpy;
+        }
+        const double rs = rcp_nr(dp + dm);
+        const double gamma = (dp * dm) * rs;
+        const double w_plus = dm * rs, w_minus = dp * rs;
+        const double pen = (ke * kn * a.sigma_inner * gamma) * ihp;
+        const double cs = -w_minus * ke, cp = -w_plus * kn, cm = w_minus * ke;
+#pragma unroll
+        for (int i = 0; i < NB; ++i)
+#pragma unroll
+          for (int j = 0; j < NB; ++j) S[i][j] += cs * (I1(j, i) + I1(i, j)) + pen * MM(i, j);
+        int slot[NB];
+#pragma unroll
+        for (int r = 0; r < NB; ++r) slot[r] = role_slot<E>(o.finfo, f, r);
+#pragma unroll
+        for (int i = 0; i < NB; ++i) {
+          // int phi+_r phi_i: phi+_A = 1 - s, phi+_B = s (roles 0, 1); int phi+_r (A grad phi_i . n) likewise
+          const double pi = i == fa ? L3 : (i == fb ? L6 : 0.0), qi = i == fa ? L6 : (i == fb ? L3 : 0.0);
+          double* row = img + i * rowlen + pos[f] * NB;
+#pragma unroll
+          for (int r = 0; r < NB; ++r) {
+            const double anr = pi * alp[r] + qi * bep[r];
+            const double ai = r == 0 ? L3 * al[i] + L6 * be[i] : (r == 1 ? L6 * al[i] + L3 * be[i] : 0.0);
+            const double mr = r == 0 ? pi : (r == 1 ? qi : 0.0);
+            row[slot[r]] = cp * anr + cm * ai - pen * mr;
+          }
+        }
+      } else {   // Dirichlet: SWIPDG::BoundaryLHS
+        const double pen = (a.sigma_boundary * ke * dm) * ihp;
+#pragma unroll
+        for (int i = 0; i < NB; ++i)
+#pragma unroll
+          for (int j = 0; j < NB; ++j) S[i][j] += -ke * (I1(j, i) + I1(i, j)) + pen * MM(i, j);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+#pragma unroll
+      for (int j = 0; j < NB; ++j) img[i * rowlen + pos_self * NB + j] = S[i][j];
+  }
+};
+
 // P1 simplex, piecewise-constant coefficients: the closed-form policy (p1_compute above)
 template <int TK, int KK>
 struct P1PwcPolicy {
   static constexpr int NB = 3, NF = 3;
   static constexpr int RB = 36;
+  static constexpr int WGCU = 4, MINW = 1;   // store-bound: 4 tiles per CU (sweep 1..8)
+  static constexpr bool PAD = false;          // store-bound: its 4-way write conflicts stay hidden
   using Own = P1Own;
   using Gat = P1Gat;
   __device__ static void load_own(const AssembleArgs& a, int64_t e, Own& o) { p1_load_own<TK, KK>(a, e, o); }
@@ -1074,12 +1241,21 @@ __device__ __forceinline__ int tile_offset(int c, bool active)
 // Persistent, software-pipelined driver (see the P1 comment above): per wave a sequence of 64-element
 // tiles, memory order [prefetch own data t+1][compute t -> LDS][gathers t+1][stores t].
 // ------------------------------------------------------------------------------------------------
+//
+// LDS image.  Contiguous (element i at its CSR offset inside the tile, streamed with aligned 16-byte reads)
+// puts the lanes' row blocks RB doubles apart: for Q1 (RB = 80 = 160 dwords) a ds_write_b64 meets only
+// two bank pairs per 32 lanes, a 16-way conflict (80 such writes per tile).  Policies with P::PAD stage
+// *uniform* tiles (every element with all NF faces interior: tile length = nact * RB, the bulk of a mesh)
+// padded instead: lane i at lds[i * (RB + 1) + j], conflict-free ((RB + 1) odd), and the reader maps the
+// tile's CSR value d to lds[d + d / RB].  Other tiles use the contiguous image.
 template <class P, bool TL>   // TL: tiles come from a.tile_list (interior / halo split), else 0..n_tiles-1
-__global__ void __launch_bounds__(64, 1)
+__global__ void __launch_bounds__(64, P::MINW)
 swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
 {
-  constexpr int IMG = 64 * P::RB;
+  constexpr int RB = P::RB;
+  constexpr int IMG = 64 * RB;
   constexpr int STORES = (IMG / 2 + 63) / 64;
+  static_assert(!P::PAD || 64 * (RB + 1) <= IMG + 2 + RB, "padded image fits the LDS allocation");
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const int lane = threadIdx.x;
   const int64_t G = gridDim.x, b = blockIdx.x;
@@ -1127,32 +1303,66 @@ swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
     int64_t base_n, tile_end_n;
     bounds(tn, base_n, tile_end_n);
 
-    const bool active = a.own_begin + tile_at(t) * 64 + lane < a.own_end;
+    const int64_t t0 = a.own_begin + tile_at(t) * 64;
+    const bool active = t0 + lane < a.own_end;
     const int64_t base_al = base & ~int64_t(1);
     const int off = tile_offset<P::NB>(P::n_interior(own), active) + int(base - base_al);
-    P::compute(a, e, own, gat, active ? lds + off : scratch);
+    const int tlen = int(tile_end - base);
+    const bool uni = P::PAD && tlen == RB * int(a.own_end - t0 < 64 ? a.own_end - t0 : 64);   // wave-uniform
+    double* img = uni ? lds + lane * (RB + 1) : (active ? lds + off : scratch);
+    if (!HDD_ABL(a, 1)) P::compute(a, e, own, gat, img);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
     typename P::Gat gat_n;
-    P::load_gat(a, en, own_n, gat_n);
+    if (!HDD_ABL(a, 4)) P::load_gat(a, en, own_n, gat_n);
 
     const int64_t start = (base + 1) & ~int64_t(1);
     const int64_t stop = tile_end & ~int64_t(1);
-    const double head = lds[base - base_al];
-    const double tail = lds[tile_end - 1 - base_al];
-    out[base] = head;
-    out[tile_end - 1] = tail;
-    const int nbytes = stop > start ? int(stop - start) * 8 : 0;
+    const int nbytes = stop > start && !HDD_ABL(a, 2) ? int(stop - start) * 8 : 0;
     __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(out + start, (short)0, nbytes, 0x00020000);
-    const double* src = lds + (start - base_al);
+    if (P::PAD && uni) {
+      auto at = [](int d) { return d + d / RB; };   // padded slot of the tile's CSR value d
+      const double head = lds[0];
+      const double tail = lds[at(tlen - 1)];
+      out[base] = head;
+      out[tile_end - 1] = tail;
+      const int d0 = int(start - base), dmax = tlen - 2;
+      if (d0 == 0) {   // element blocks start on even d: no 16-byte chunk straddles two elements
 #pragma unroll
-    for (int k = 0; k < STORES; ++k) {
-      const int idx = 2 * (lane + 64 * k);
-      const int li = idx < IMG ? idx : 0;
-      const dvec2 v = *reinterpret_cast<const dvec2*>(src + li);
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ivec4, v), rsrc, idx * 8, 0, 0);
+        for (int k = 0; k < STORES; ++k) {
+          const int d = 2 * (lane + 64 * k);
+          const int a0 = at(d <= dmax ? d : 0);
+          dvec2 v;
+          v.x = lds[a0];
+          v.y = lds[a0 + 1];
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ivec4, v), rsrc, d * 8, 0, 0);
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < STORES; ++k) {
+          const int m2 = 2 * (lane + 64 * k);
+          const int d = m2 + 1 <= dmax ? m2 + 1 : 0;
+          dvec2 v;
+          v.x = lds[at(d)];
+          v.y = lds[at(d + 1)];
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ivec4, v), rsrc, m2 * 8, 0, 0);
+        }
+      }
+    } else {
+      const double head = lds[base - base_al];
+      const double tail = lds[tile_end - 1 - base_al];
+      out[base] = head;
+      out[tile_end - 1] = tail;
+      const double* src = lds + (start - base_al);
+#pragma unroll
+      for (int k = 0; k < STORES; ++k) {
+        const int idx = 2 * (lane + 64 * k);
+        const int li = idx < IMG ? idx : 0;
+        const dvec2 v = *reinterpret_cast<const dvec2*>(src + li);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ivec4, v), rsrc, idx * 8, 0, 0);
+      }
     }
     if (!has_next) break;
     t = tn;
@@ -1198,7 +1408,7 @@ static hipError_t launch_persistent(const AssembleArgs& a, hipStream_t s)
   int dev = 0, cus = 256;
   (void)hipGetDevice(&dev);
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  int wgcu = 4;   // measured best on MI355X for P1 (sweep 1..8: profiles/r01/sweep_wg_per_cu.log)
+  int wgcu = P::WGCU;   // measured per policy (profiles/r01/sweep_wg_per_cu.log, profiles/r01/s2/)
   if (const char* w = getenv("HDD_P1_WGCU")) wgcu = atoi(w);   // profiling sweeps only
   wgcu = std::max(1, std::min<int>(wgcu, int((160 * 1024) / lds)));   // resident by LDS (Q1 tiles: 3 per CU)
   const int64_t G = std::min<int64_t>(tiles, int64_t(cus) * wgcu);
@@ -1236,7 +1446,7 @@ static hipError_t dispatch_kinds(const AssembleArgs& a, hipStream_t s, bool smoo
 }
 
 template <int TK, int KK> using P1Pwc = P1PwcPolicy<TK, KK>;
-template <int TK, int KK> using Q1Pwc = GenericPolicy<Cube, 1, 2, TK, KK>;
+template <int TK, int KK> using Q1Pwc = Q1PwcPolicy<TK, KK>;
 template <int TK, int KK> using Q1Smooth3 = GenericPolicy<Cube, 4, 3, TK, KK>;
 template <int TK, int KK> using P1Smooth3 = GenericPolicy<Simplex, 6, 3, TK, KK>;
 

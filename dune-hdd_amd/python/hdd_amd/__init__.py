@@ -12,7 +12,7 @@ import numpy as np
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.abspath(os.path.join(_PKG, "..", ".."))          # dune-hdd_amd/
-LIB_PATH = os.path.join(ROOT, "lib", "libhdd_amd.so")
+LIB_PATH = os.environ.get("HDD_AMD_LIB") or os.path.join(ROOT, "lib", "libhdd_amd.so")   # override: A/B runs
 HEADER = os.path.abspath(os.path.join(ROOT, "..", "include", "hdd.h"))
 
 SIMPLEX, CUBE, HEX = 0, 1, 2

@@ -1,37 +1,63 @@
-"""A/B timing of kernel ablations (HDD_DEBUG_FLAGS) in ONE process, interleaved rounds (guide 5.4 rule 24)."""
-import os, sys, json
+"""A/B timing of kernel ablations (HDD_DEBUG_FLAGS) in ONE process, interleaved rounds, several workloads
+side by side (one of them unchanged serves as the control for box-to-box clock differences).
+Flags (swipdg_persistent_kernel): 1 = skip compute, 2 = drop the value stores (range 0), 4 = skip the
+neighbour gathers, 8 = interleave the waves' store chunks, 16 = one wave per tile (RS = 1).
+usage: python scripts/ablate.py c2:0,1 c4:0,8,16 c3:0"""
+import os, sys, math
 import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "dune-hdd_amd", "python"))
 import torch
 import hdd_amd as H
 
-flags = [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "0,1,2,4,3,5,6,7").split(",")]
-nx, ny = 3200, 640
-grid = H.Grid.structured(H.SIMPLEX, nx, ny, (0, 0), (5, 1))
-local = grid.local()
-rng = np.random.default_rng(10)
-perm = 10.0 ** rng.uniform(-3, 3, 2000)
-k = torch.from_numpy(local.checkerboard((0, 0), (5, 1), 100, 20, perm)).cuda()
-ctx = H.Context(0)
-dm = H.DeviceMesh(local)
-dp = H.DevicePattern(local)
-kap = [H.scalar_fn(H.FN_CONST, 1.0)]
-ten = H.tensor_fn(H.TENSOR_ISO_PER_ELEM, per_elem=k)
-vals = [torch.empty(dp.nnz, dtype=torch.float64, device="cuda")]
-res = {f: [] for f in flags}
-for rnd in range(6):
-    for f in flags:
-        os.environ["HDD_DEBUG_FLAGS"] = str(f)
-        for _ in range(3):
-            H.assemble(ctx, dm, dp, kap, ten, vals=vals)
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-        ev[0].record()
-        for _ in range(10):
-            H.assemble(ctx, dm, dp, kap, ten, vals=vals)
-        ev[1].record()
-        torch.cuda.synchronize()
-        res[f].append(ev[0].elapsed_time(ev[1]) / 10)
-os.environ["HDD_DEBUG_FLAGS"] = "0"
-for f in flags:
-    print("flags=%d  median %.4f ms  min %.4f ms" % (f, np.median(res[f]), np.min(res[f])))
+
+def workload(cfg, ctx):
+    rng = np.random.default_rng(10)
+    perm = 10.0 ** rng.uniform(-3, 3, 2000)
+    if cfg == "c3":
+        grid = H.Grid.structured(H.SIMPLEX, 1024, 1024, (-1, -1), (1, 1))
+        local = grid.local()
+        kap = [H.scalar_fn(H.FN_SINUSOID, 1.0, 0.75, 4 * math.pi, 2 * math.pi, order=3)]
+        ten = H.tensor_fn()
+    else:
+        et, nx, ny, p = (H.SIMPLEX, 3200, 640, 1) if cfg == "c2" else (H.CUBE, 3520, 1200, 8)
+        grid = H.Grid.structured(et, nx, ny, (0, 0), (5, 1), px=p, py=p)
+        local = grid.local()
+        k = torch.from_numpy(local.checkerboard((0, 0), (5, 1), 100, 20, perm)).cuda()
+        kap = [H.scalar_fn(H.FN_CONST, 1.0)]
+        ten = H.tensor_fn(H.TENSOR_ISO_PER_ELEM, per_elem=k)
+    dm = H.DeviceMesh(local)
+    dp = H.DevicePattern(local)
+    vals = [torch.empty(dp.nnz, dtype=torch.float64, device="cuda")]
+    return lambda: H.assemble(ctx, dm, dp, kap, ten, vals=vals)
+
+
+def main():
+    groups = sys.argv[1:] or ["c2:0", "c4:0"]
+    ctx = H.Context(0)
+    runs = []
+    for g in groups:
+        cfg, fl = g.split(":")
+        fn = workload(cfg, ctx)
+        runs += [(cfg, int(f), fn) for f in fl.split(",")]
+    res = {(c, f): [] for c, f, _ in runs}
+    for rnd in range(6):
+        for cfg, f, fn in runs:
+            os.environ["HDD_DEBUG_FLAGS"] = str(f)
+            for _ in range(3):
+                fn()
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+            ev[0].record()
+            for _ in range(10):
+                fn()
+            ev[1].record()
+            torch.cuda.synchronize()
+            res[(cfg, f)].append(ev[0].elapsed_time(ev[1]) / 10)
+    os.environ["HDD_DEBUG_FLAGS"] = "0"
+    for cfg, f, _ in runs:
+        r = res[(cfg, f)]
+        print("%s flags=%-3d median %.4f ms  min %.4f ms" % (cfg, f, np.median(r), np.min(r)), flush=True)
+
+
+if __name__ == "__main__":
+    main()
