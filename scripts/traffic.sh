@@ -6,6 +6,8 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 ROOT=$(pwd)
 OUT=$ROOT/gpurun_out/traffic_${1:-r01}
 mkdir -p "$OUT"
+MB=$ROOT/scripts/microbench
+[ -x "$MB/stream" ] || /opt/rocm/bin/hipcc -O3 -Wno-unused-result -Wno-unused-value --offload-arch=gfx950 "$MB/stream.hip" -o "$MB/stream" || exit 1
 export TMPDIR=/tmp
 cd /tmp
 for c in FETCH_SIZE WRITE_SIZE; do
