@@ -258,3 +258,57 @@ def test_bench_size_properties(ctx):
     interior_rows = interior_elem.repeat_interleave(3)
     rel = rs[interior_rows].abs().max() / scale
     assert rel < 1e-12, float(rel)
+
+
+@pytest.mark.parametrize("et,nx,ny", [(H.SIMPLEX, 1, 1), (H.CUBE, 1, 1), (H.CUBE, 1, 9), (H.SIMPLEX, 9, 1),
+                                      (H.CUBE, 65, 2), (H.SIMPLEX, 33, 1), (H.CUBE, 64, 1)])
+def test_edge_meshes(ctx, et, nx, ny):
+    """Degenerate and ragged sizes: a single element (every face Dirichlet), one-element-wide strips, and
+    owned ranges one past / exactly a multiple of the 64-element tile."""
+    grid = H.Grid.structured(et, nx, ny, (0, 0), (1, 1))
+    _, (rp, col, _), (val,) = _run_product(ctx, grid, [H.scalar_fn(H.FN_CONST, 1.0)], H.tensor_fn())
+    og = O.Grid(*_oracle_mesh(et, nx, ny, (0, 0), (1, 1)))
+    orp, ocol, oval = O.assemble(og, O.scalar(O.FN_CONST, 1.0), O.tensor(O.TENSOR_CONST), O.params())
+    assert np.array_equal(rp, orp) and np.array_equal(col, ocol)
+    worst, ok = compare_rows(rp, val, oval, RTOL)
+    assert ok, worst
+
+
+def _affine_quad_mesh(nx, ny, M, c):
+    """Structured quads pushed through x -> M x + c: every element a general parallelogram (non-diagonal
+    Jacobian), Dune vertex order kept."""
+    et, coords, ev = O.cube_grid(nx, ny, (0, 0), (1, 1))
+    return et, coords @ np.asarray(M, float).T + np.asarray(c, float), ev
+
+
+@pytest.mark.parametrize("smooth", [False, True])
+def test_parallelogram_mesh_uniform_tiles(ctx, smooth):
+    """Q1 on sheared/rotated parallelograms, large enough for tiles of 64 interior elements (the padded
+    LDS image path) next to boundary tiles (the contiguous path); piecewise-constant SPD tensors, or the
+    OS2014 sinusoid (quadrature policy)."""
+    torch = _torch()
+    M = [[1.3, 0.45], [-0.2, 0.9]]
+    et, coords, ev = _affine_quad_mesh(200, 40, M, (0.3, -0.1))
+    grid = H.Grid.from_connectivity(et, coords, ev)
+    rng = np.random.default_rng(7)
+    ne = ev.shape[0]
+    a = rng.uniform(0.5, 2.0, ne); c = rng.uniform(0.5, 2.0, ne); b = rng.uniform(-0.3, 0.3, ne)
+    sym = np.stack([a, b, c], 0)
+    if smooth:
+        fns = [H.scalar_fn(H.FN_SINUSOID, 1.0, 0.75, 4 * np.pi, 2 * np.pi, order=3)]
+        ofn = O.scalar(O.FN_SINUSOID, 1.0, 0.75, 4 * np.pi, 2 * np.pi, order=3)
+    else:
+        kap = rng.uniform(0.1, 10.0, ne)
+        fns = [H.scalar_fn(H.FN_PER_ELEM, per_elem=torch.from_numpy(kap).cuda())]
+        ofn = O.scalar(O.FN_PER_ELEM, per_elem=kap)
+    tsym = torch.from_numpy(np.ascontiguousarray(sym)).cuda()
+    local, (rp, col, _), (val,) = _run_product(ctx, grid, fns, H.tensor_fn(H.TENSOR_SYM_PER_ELEM, per_elem=tsym))
+    nb = local.neighbors[:, local.own_begin:local.own_end]
+    full = (nb >= 0).all(axis=0)[: (local.n_own // 64) * 64].reshape(-1, 64).all(axis=1)
+    assert full.any() and not full.all(), "expected both uniform and boundary tiles"
+    og = O.Grid(et, coords, ev)
+    orp, ocol, oval = O.assemble(og, ofn, O.tensor(O.TENSOR_SYM_PER_ELEM, per_elem=np.ascontiguousarray(sym.T)),
+                                 O.params())
+    assert np.array_equal(col, ocol)
+    worst, ok = compare_rows(rp, val, oval, RTOL)
+    assert ok, worst

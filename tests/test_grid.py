@@ -133,3 +133,13 @@ def test_bench_size_counts():
     g1 = H.Grid.structured(H.CUBE, 16, 16, (-1, -1), (1, 1))
     rp, col, _ = g1.local().pattern()
     assert col.shape[0] == 19456                                  # C1
+
+
+def test_subdomain_range_errors():
+    """An empty or out-of-range owned subdomain range is rejected with HDD_ERR_RANGE (the reference's
+    Stuff::Exceptions::index_out_of_range, block-swipdg.hh:560-562), not silently assembled."""
+    g = H.Grid.structured(H.CUBE, 8, 8, (0, 0), (1, 1), px=2, py=1)
+    for s0, s1 in ((1, 1), (2, 1), (0, 3), (-1, 1)):
+        with pytest.raises(H.HddError, match="status 5"):
+            g.local(s0, s1)
+    assert g.local(1, 2).n_own == 32
