@@ -15,6 +15,10 @@ partition -- rank r owns the r-th 3200 x 640 strip of a (3200 N) x 640 grid over
 checkerboard widened to 100N x 20 cells) and assembles its own rows (owner-computes, no reduction); the
 face-halo records (vertex coordinates + tensor of the ghost elements) are exchanged with RCCL send/recv
 inside every step.
+
+--workload c4 (BASELINE.json configs[3], not the metric's line): SPE10 3520 x 1200 Q1 quads on [0,5]x[0,1]
+with 8 x 8 subdomains (block numbering), strong scaling -- rank r of N owns subdomains [64 r / N, 64 (r+1) / N)
+(columns of the 8 x 8 layout) and assembles its rows; same halo exchange.
 """
 import argparse
 import json
@@ -35,8 +39,12 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--nx", type=int, default=3200, help="squares per strip in x (per rank)")
-    ap.add_argument("--ny", type=int, default=640)
+    ap.add_argument("--workload", default="c2", choices=["c2", "c4"],
+                    help="c2 (default, the metric's line): SPE10 P1 Kuhn strips, weak scaling; c4: SPE10 "
+                         "3520x1200 Q1 with 8x8 subdomains sharded over the ranks in subdomain columns "
+                         "(BASELINE.json configs[3]), strong scaling")
+    ap.add_argument("--nx", type=int, default=0, help="c2: squares per strip in x per rank (3200); c4: 3520")
+    ap.add_argument("--ny", type=int, default=0, help="c2: 640; c4: 1200")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU work of the baseline sample")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
@@ -58,7 +66,7 @@ def _cpu_model():
     return "unknown"
 
 
-def cpu_baseline(nx_full, ny, target_s):
+def cpu_baseline(nx_full, ny, target_s, cube=False):
     """The CPU oracle timed on a bounded strip of the same workload (nxs x ny Kuhn squares over
     [0, 5 nxs/nx_full] x [0,1], checkerboard of the full domain), SURVEY.md 8(d) protocol: 1 warm-up, median
     of 5.  `value`: the sequential element walk with per-entry CSR binary search, 1 thread -- the reference's
@@ -72,7 +80,7 @@ def cpu_baseline(nx_full, ny, target_s):
 
     def run(nxs, reps=5, omp=0):
         upper = (5.0 * nxs / nx_full, 1.0)
-        et, c, ev = O.kuhn_grid(nxs, ny, lower, upper)
+        et, c, ev = (O.cube_grid if cube else O.kuhn_grid)(nxs, ny, lower, upper)
         k = O.checkerboard(O.element_centers(c, ev), (0.0, 0.0), (5.0, 1.0), 100, 20, perm)
         g = O.Grid(et, c, ev)
         rp, col = g.pattern()
@@ -85,7 +93,7 @@ def cpu_baseline(nx_full, ny, target_s):
             t = time.perf_counter()
             fn()
             ts.append(time.perf_counter() - t)
-        return float(np.median(ts)), g.ne * 3
+        return float(np.median(ts)), g.ne * (4 if cube else 3)
 
     t_cal, _ = run(25, reps=1)
     per_rep = target_s / 6.0                                   # warm-up + 5 timed runs ~ target_s
@@ -94,8 +102,9 @@ def cpu_baseline(nx_full, ny, target_s):
     t_omp, _ = run(nxs, omp=threads)
     return dict(value=dofs / t, unit="DoFs/s", cores=1, kind="port",
                 sample="CPU oracle (oracle/swipdg_oracle.c, sequential element walk + per-entry CSR binary "
-                       "search, 1 thread, median of 5 after 1 warm-up) on a %d x %d Kuhn strip of the C2 "
-                       "workload = %d DoFs (%.3f s per assembly)" % (nxs, ny, dofs, t),
+                       "search, 1 thread, median of 5 after 1 warm-up) on a %d x %d %s strip of the %s "
+                       "workload = %d DoFs (%.3f s per assembly)"
+                       % (nxs, ny, "Q1 quad" if cube else "Kuhn", "C4" if cube else "C2", dofs, t),
                 omp_value=dofs / t_omp, omp_cores=threads,
                 omp_sample="owner-computes OpenMP variant of the same integrands, %d threads, same strip, "
                            "median of 5 (%.3f s per assembly)" % (threads, t_omp),
@@ -123,13 +132,25 @@ def main():
         else:
             dist.init_process_group("gloo")
 
-    nx, ny = args.nx * world, args.ny
-    lower, upper = (0.0, 0.0), (5.0 * world, 1.0)
-    grid = H.Grid.structured(H.SIMPLEX, nx, ny, lower, upper, px=world, py=1)
-    local = grid.local(rank, rank + 1)
-    rng = np.random.default_rng(10)
-    perm = 10.0 ** rng.uniform(-3.0, 3.0, size=100 * world * 20)     # == oracle synthetic field at world=1
-    kcell = local.checkerboard(lower, upper, 100 * world, 20, perm)
+    c4 = args.workload == "c4"
+    if c4:   # strong scaling: one 3520 x 1200 Q1 mesh, 8 x 8 subdomains, rank r owns a subdomain-column range
+        nx, ny = (args.nx or 3520), (args.ny or 1200)
+        lower, upper = (0.0, 0.0), (5.0, 1.0)
+        grid = H.Grid.structured(H.CUBE, nx, ny, lower, upper, px=8, py=8)
+        if world > grid.n_sub:
+            raise SystemExit("c4 shards 64 subdomains: at most 64 ranks")
+        s0, s1 = (rank * grid.n_sub) // world, ((rank + 1) * grid.n_sub) // world
+        local = grid.local(s0, s1)
+        ncx = 100
+        perm = 10.0 ** np.random.default_rng(10).uniform(-3.0, 3.0, size=2000)
+    else:    # weak scaling: rank r owns the r-th (nx x ny) Kuhn strip of a (nx N) x ny grid
+        nx, ny = (args.nx or 3200) * world, (args.ny or 640)
+        lower, upper = (0.0, 0.0), (5.0 * world, 1.0)
+        grid = H.Grid.structured(H.SIMPLEX, nx, ny, lower, upper, px=world, py=1)
+        local = grid.local(rank, rank + 1)
+        ncx = 100 * world
+        perm = 10.0 ** np.random.default_rng(10).uniform(-3.0, 3.0, size=100 * world * 20)   # == oracle field at N=1
+    kcell = local.checkerboard(lower, upper, ncx, 20, perm)
     ctx = H.Context(local_rank)
     dmesh = H.DeviceMesh(local, local_rank, zero_ghosts=world > 1)
     tens = torch.from_numpy(kcell).cuda()
@@ -146,13 +167,15 @@ def main():
                             strip_owner(grid.n_sub, world), rank, host_staging=args.backend == "gloo")
 
     n_own = local.n_own
-    dofs_rank = 3 * n_own
+    nbf = 4 if c4 else 3
+    dofs_rank = nbf * n_own
     nbr = local.neighbors[:, local.own_begin:local.own_end]
     interior = nbr >= 0
     owned_pair = interior & (nbr >= local.own_begin) & (nbr < local.own_end)
     nif = int(owned_pair.sum()) // 2 + int((interior & ~owned_pair).sum())
     qp1 = 1
-    alg_bytes = 8 * dpat.nnz * qp1 + n_own * (84 + 8 * qp1) + 12 * nif     # SURVEY.md 8(d) formula
+    b_elem = (104 if c4 else 84) + 8 * qp1                                  # quad / triangle record
+    alg_bytes = 8 * dpat.nnz * qp1 + n_own * b_elem + 12 * nif             # SURVEY.md 8(d) formula
 
     stream = torch.cuda.current_stream()
     overlap = halo is not None and not args.no_overlap
@@ -199,7 +222,7 @@ def main():
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, kernel_ms_max = float(t[0]), float(t[1])
-    total_dofs = dofs_rank * world
+    total_dofs = nbf * grid.ne if c4 else dofs_rank * world
     value = total_dofs * args.steps / elapsed
 
     if rank == 0:
@@ -208,13 +231,17 @@ def main():
         if os.path.exists(args.traffic_json):
             try:
                 tj = json.load(open(args.traffic_json))
-                if tj.get("workload") == "spe10_swipdg_p1_kuhn_%dx%d" % (args.nx, args.ny):
+                if not c4 and world == 1 and tj.get("workload") == "spe10_swipdg_p1_kuhn_%dx%d" % (nx // world, ny):
                     traffic = tj.get("hbm_bytes_per_launch")
             except (OSError, ValueError):
                 traffic = None
+        halo_desc = ""
+        if world > 1:
+            halo_desc = ", %s face halo%s" % ("RCCL" if args.backend == "nccl" else "gloo host-staged (rehearsal)",
+                                              " overlapped with interior tiles" if overlap else "")
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(args.nx, args.ny, args.cpu_seconds)
+            cpu = cpu_baseline(nx // world, ny, args.cpu_seconds, cube=c4)
         out = {
             "metric": "assembled DoFs/sec (global stiffness), SPE10 SWIPDG p=1",
             "value": value,
@@ -224,19 +251,24 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": 1e3 * elapsed / args.steps,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if c4 else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (SPE10 Model1 stand-in permeability: perm_case1.dat absent)",
-            "config": {"workload": "spe10_swipdg_p1_kuhn_%dx%d_per_gpu" % (args.nx, args.ny),
-                       "elements_per_gpu": n_own, "dofs_per_gpu": dofs_rank, "nnz_per_gpu": dpat.nnz,
-                       "total_dofs": total_dofs, "components": qp1,
-                       "parallelism": "block-swipdg strips x%d, owner-computes, RCCL face halo%s"
-                       % (world, " overlapped with interior tiles" if overlap else "")
-                       if world > 1 else "single GPU"},
+            "config": ({"workload": "spe10_block_swipdg_q1_%dx%d_8x8_subdomains" % (nx, ny),
+                        "elements": grid.ne, "elements_rank0": n_own, "total_dofs": total_dofs,
+                        "nnz_rank0": dpat.nnz, "components": qp1,
+                        "parallelism": "subdomain columns x%d, owner-computes%s" % (world, halo_desc)}
+                       if c4 else
+                       {"workload": "spe10_swipdg_p1_kuhn_%dx%d_per_gpu" % (nx // world, ny),
+                        "elements_per_gpu": n_own, "dofs_per_gpu": dofs_rank, "nnz_per_gpu": dpat.nnz,
+                        "total_dofs": total_dofs, "components": qp1,
+                        "parallelism": "block-swipdg strips x%d, owner-computes%s" % (world, halo_desc)
+                        if world > 1 else "single GPU"}),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "swipdg_persistent_kernel<P1PwcPolicy<1, 0>, false>",
+                         "kernel": "swipdg_persistent_kernel<%s<1, 0>, %s>"
+                                   % ("Q1PwcPolicy" if c4 else "P1PwcPolicy", "true" if overlap else "false"),
                          "kernel_ms_avg": kernel_ms, "kernel_ms_avg_max_rank": kernel_ms_max,
                          "algorithmic_bytes_per_launch": alg_bytes},
             "cpu_baseline": cpu,
