@@ -774,6 +774,32 @@ extern "C" int hdd_product_assemble(hdd_ctx* ctx, const hdd_mesh* m, int32_t pro
   }
   hipError_t e = hipSetDevice(ctx->device);
   if (e != hipSuccess) return hip_fail(e, "hdd_product_assemble: hipSetDevice");
+  if (m->elem_type != HDD_HEX && m->face_info) {
+    // P1 / Q1 with piecewise-constant data: closed forms on the persistent tile driver
+    AssembleArgs f{};
+    f.elem_type = m->elem_type;
+    f.n_comp = 1;
+    f.n_local = m->n_local;
+    f.own_begin = m->own_begin;
+    f.own_end = m->own_end;
+    f.coords = m->coords;
+    f.nbrs = m->neighbors;
+    f.finfo = m->face_info;
+    f.elem_ptr = pattern->elem_ptr;
+    f.tkind = a.tkind;
+    f.tc0 = a.tc[0];
+    f.tc1 = a.tc[1];
+    f.tc2 = a.tc[2];
+    f.tper = a.tper;
+    f.sigma_inner = p->sigma_inner;
+    f.sigma_boundary = p->sigma_boundary;
+    f.beta = p->beta;
+    f.kappa[0] = a.kappa;
+    f.vals[0] = d_vals;
+    bool fast = false;
+    e = launch_product_fast(f, product, static_cast<hipStream_t>(stream), &fast);
+    if (fast) return e == hipSuccess ? HDD_OK : hip_fail(e, "hdd_product_assemble: launch");
+  }
   e = launch_product(a, static_cast<hipStream_t>(stream));
   return e == hipSuccess ? HDD_OK : hip_fail(e, "hdd_product_assemble: launch");
 }

@@ -699,7 +699,10 @@ __device__ __forceinline__ void p1_load_gat(const AssembleArgs& a, int64_t e, co
   }
 }
 
-// P1 closed-form per-element math on preloaded data (role form, see above); writes the row block into `img`
+// P1 closed-form per-element math on preloaded data (role form, see above); writes the row block into `img`.
+// PEN: only the interior-penalty terms (the SWIPDG penalty product, swipdg.hh:462-508), no volume and no
+// consistency / symmetry terms.
+template <bool PEN = false>
 __device__ __forceinline__ void p1_compute(const AssembleArgs& a, int64_t e, const P1Own& o, const P1Gat& gt,
                                            double* img)
 {
@@ -737,12 +740,13 @@ __device__ __forceinline__ void p1_compute(const AssembleArgs& a, int64_t e, con
   const double ke = o.ke;
   double S[3][3];
   {
-    const double fac = 0.5 * adet * ke;
+    const double fac = PEN ? 0.0 : 0.5 * adet * ke;
 #pragma unroll
     for (int i = 0; i < 3; ++i)
 #pragma unroll
       for (int j = 0; j < 3; ++j) S[i][j] = fac * (Ag[j][0] * g[i][0] + Ag[j][1] * g[i][1]);
   }
+  constexpr double CS = PEN ? 0.0 : 1.0;   // consistency / symmetry terms on (stiffness) or off (penalty)
 #pragma unroll
   for (int f = 0; f < 3; ++f) {
     const int32_t n = o.nbr[f];
@@ -779,8 +783,8 @@ __device__ __forceinline__ void p1_compute(const AssembleArgs& a, int64_t e, con
       const double AnB = ((Oy - Ay) * mx + (Ax - Ox) * my) * iD;
       const double AnO = ((Ay - By) * mx + (Bx - Ax) * my) * iD;
       const int jA = rev ? tb : ta, jB = rev ? ta : tb;
-      const double cpl = -w_plus * kn;
-      const double sym = w_minus * ke;
+      const double cpl = -w_plus * kn * CS;
+      const double sym = w_minus * ke * CS;
 #pragma unroll
       for (int i = 0; i < 3; ++i) {
         double* row = img + i * rowlen + pos[f] * 3;
@@ -795,7 +799,7 @@ __device__ __forceinline__ void p1_compute(const AssembleArgs& a, int64_t e, con
         for (int j = 0; j < 3; ++j) {
           const double m1i = i == fc ? 0.0 : half, m1j = j == fc ? 0.0 : half;
           const double mm = (i == fc || j == fc) ? 0.0 : (i == j ? third : sixth);
-          S[i][j] += -w_minus * ke * (Ae[j] * m1i + Ae[i] * m1j) + pen * mm;
+          S[i][j] += -w_minus * ke * CS * (Ae[j] * m1i + Ae[i] * m1j) + pen * mm;
         }
     } else {
       const double pen = (a.sigma_boundary * ke * dm) * ihp;
@@ -805,7 +809,7 @@ __device__ __forceinline__ void p1_compute(const AssembleArgs& a, int64_t e, con
         for (int j = 0; j < 3; ++j) {
           const double m1i = i == fc ? 0.0 : half, m1j = j == fc ? 0.0 : half;
           const double mm = (i == fc || j == fc) ? 0.0 : (i == j ? third : sixth);
-          S[i][j] += -ke * (Ae[j] * m1i + Ae[i] * m1j) + pen * mm;
+          S[i][j] += -ke * CS * (Ae[j] * m1i + Ae[i] * m1j) + pen * mm;
         }
     }
   }
@@ -1069,7 +1073,7 @@ struct GenericPolicy {
 // maximum).  Neighbour quantities are in role coordinates (A = my face vertex a, B = b, C = the
 // neighbour vertex next to A), as in GenericPolicy.
 // ------------------------------------------------------------------------------------------------
-template <int TK, int KK>
+template <int TK, int KK, bool PEN = false>   // PEN: penalty terms only (the SWIPDG penalty product)
 struct Q1PwcPolicy : GenericPolicy<Cube, 1, 2, TK, KK> {
   using Base = GenericPolicy<Cube, 1, 2, TK, KK>;
   using E = Cube;
@@ -1110,7 +1114,7 @@ struct Q1PwcPolicy : GenericPolicy<Cube, 1, 2, TK, KK> {
       const double p00 = i00 * A.a00 + i01 * A.a01, p01 = i00 * A.a01 + i01 * A.a11;
       const double p10 = i10 * A.a00 + i11 * A.a01, p11 = i10 * A.a01 + i11 * A.a11;
       const double k00 = p00 * i00 + p01 * i01, k01 = p00 * i10 + p01 * i11, k11 = p10 * i10 + p11 * i11;
-      const double fac = adet * ke;
+      const double fac = PEN ? 0.0 : adet * ke;
 #pragma unroll
       for (int i = 0; i < NB; ++i)
 #pragma unroll
@@ -1168,7 +1172,8 @@ struct Q1PwcPolicy : GenericPolicy<Cube, 1, 2, TK, KK> {
         const double gamma = (dp * dm) * rs;
         const double w_plus = dm * rs, w_minus = dp * rs;
         const double pen = (ke * kn * a.sigma_inner * gamma) * ihp;
-        const double cs = -w_minus * ke, cp = -w_plus * kn, cm = w_minus * ke;
+        constexpr double CS = PEN ? 0.0 : 1.0;
+        const double cs = -w_minus * ke * CS, cp = -w_plus * kn * CS, cm = w_minus * ke * CS;
 #pragma unroll
         for (int i = 0; i < NB; ++i)
 #pragma unroll
@@ -1194,7 +1199,7 @@ struct Q1PwcPolicy : GenericPolicy<Cube, 1, 2, TK, KK> {
 #pragma unroll
         for (int i = 0; i < NB; ++i)
 #pragma unroll
-          for (int j = 0; j < NB; ++j) S[i][j] += -ke * (I1(j, i) + I1(i, j)) + pen * MM(i, j);
+          for (int j = 0; j < NB; ++j) S[i][j] += -ke * (PEN ? 0.0 : 1.0) * (I1(j, i) + I1(i, j)) + pen * MM(i, j);
       }
     }
 #pragma unroll
@@ -1205,7 +1210,7 @@ struct Q1PwcPolicy : GenericPolicy<Cube, 1, 2, TK, KK> {
 };
 
 // P1 simplex, piecewise-constant coefficients: the closed-form policy (p1_compute above)
-template <int TK, int KK>
+template <int TK, int KK, bool PEN = false>
 struct P1PwcPolicy {
   static constexpr int NB = 3, NF = 3;
   static constexpr int RB = 36;
@@ -1218,7 +1223,124 @@ struct P1PwcPolicy {
   __device__ static int n_interior(const Own& o) { return int(o.nbr[0] >= 0) + int(o.nbr[1] >= 0) + int(o.nbr[2] >= 0); }
   __device__ static void compute(const AssembleArgs& a, int64_t e, const Own& o, const Gat& g, double* img)
   {
-    p1_compute(a, e, o, g, img);
+    p1_compute<PEN>(a, e, o, g, img);
+  }
+};
+
+// ------------------------------------------------------------------------------------------------
+// Element-local products on the element-diagonal (volume) pattern (swipdg.hh:358-461: L2, H1Semi,
+// Elliptic, BoundaryL2 with over_integrate = 2), P1 triangles / Q1 parallelograms, piecewise-constant
+// data.  The reference's rules (orders 2p + 2, 2(p-1) + 2 [+ ord kappa]) integrate these polynomial
+// integrands exactly, so the closed forms below equal them up to rounding:
+//   P1:  l2 |det| (1 + d_ij) / 24;  h1 / elliptic  (|det| / 2) ghat_i^T K ghat_j
+//   Q1:  l2 |det| M(i0,j0) M(i1,j1);  h1 / elliptic  sum_ab K_ab F^ab(i,j) with the 1D integrals
+//        M = int L_i L_j, D = int L_i' L_j', C = int L_i' L_j (F^00 = D x M, F^01 = C x C^T, F^10 = C^T x C,
+//        F^11 = M x D);  K = |det J| kappa J^-1 A J^-T (A = I for h1)
+//   boundary l2: sum over boundary faces of |F| (1/3, 1/6) on the face vertices.
+// Row block = nb x nb (no neighbour blocks), so tiles are 64 nb^2 doubles and no gathers are needed.
+// ------------------------------------------------------------------------------------------------
+template <class E, int KIND, int TK, int KK>
+struct VolProductPolicy {
+  static constexpr int NB = E::NB, NF = E::NF, NV = E::NV;
+  static constexpr int RB = NB * NB;
+  static constexpr int WGCU = 4, MINW = 1;
+  static constexpr bool PAD = false;
+  struct Own {
+    double X[NV], Y[NV];
+    int32_t nbr[NF];
+    Tensor A;
+    double ke;
+  };
+  struct Gat {};
+  __device__ static void load_own(const AssembleArgs& a, int64_t e, Own& o)
+  {
+    const int64_t ne = a.n_local;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {   // vertices 0, 1, 2 span the affine map
+      o.X[k] = a.coords[(2 * k) * ne + e];
+      o.Y[k] = a.coords[(2 * k + 1) * ne + e];
+    }
+    if constexpr (KIND == HDD_PRODUCT_BOUNDARY_L2) {
+#pragma unroll
+      for (int k = 3; k < NV; ++k) {
+        o.X[k] = a.coords[(2 * k) * ne + e];
+        o.Y[k] = a.coords[(2 * k + 1) * ne + e];
+      }
+#pragma unroll
+      for (int f = 0; f < NF; ++f) o.nbr[f] = a.nbrs[f * ne + e];
+    }
+    if constexpr (KIND == HDD_PRODUCT_ELLIPTIC) {
+      o.A = tensor_k<TK>(a, e);
+      o.ke = kappa_k<KK>(a, e);
+    }
+  }
+  __device__ static void load_gat(const AssembleArgs&, int64_t, const Own&, Gat&) {}
+  __device__ static int n_interior(const Own&) { return 0; }
+
+  __host__ __device__ static constexpr double m1(int i, int j) { return i == j ? 1.0 / 3.0 : 1.0 / 6.0; }
+  __host__ __device__ static constexpr double d1(int i, int j) { return i == j ? 1.0 : -1.0; }
+  __host__ __device__ static constexpr double c1(int i, int) { return i ? 0.5 : -0.5; }   // int L_i' L_j
+
+  __device__ static void compute(const AssembleArgs&, int64_t, const Own& o, const Gat&, double* img)
+  {
+    const double j00 = o.X[1] - o.X[0], j01 = o.X[2] - o.X[0], j10 = o.Y[1] - o.Y[0], j11 = o.Y[2] - o.Y[0];
+    const double det = j00 * j11 - j01 * j10;
+    const double adet = fabs(det);
+    double S[NB][NB];
+    if constexpr (KIND == HDD_PRODUCT_L2) {
+#pragma unroll
+      for (int i = 0; i < NB; ++i)
+#pragma unroll
+        for (int j = 0; j < NB; ++j)
+          S[i][j] = std::is_same<E, Simplex>::value ? adet * (i == j ? 1.0 / 12.0 : 1.0 / 24.0)
+                                                     : adet * (m1(i & 1, j & 1) * m1(i >> 1, j >> 1));
+    } else if constexpr (KIND == HDD_PRODUCT_BOUNDARY_L2) {
+#pragma unroll
+      for (int i = 0; i < NB; ++i)
+#pragma unroll
+        for (int j = 0; j < NB; ++j) S[i][j] = 0.0;
+#pragma unroll
+      for (int f = 0; f < NF; ++f) {
+        if (o.nbr[f] >= 0) continue;
+        const int fa = E::fv(f, 0), fb = E::fv(f, 1);
+        const double tx = o.X[fb] - o.X[fa], ty = o.Y[fb] - o.Y[fa];
+        const double len = sqrt(tx * tx + ty * ty);
+        S[fa][fa] += len * (1.0 / 3.0);
+        S[fb][fb] += len * (1.0 / 3.0);
+        S[fa][fb] += len * (1.0 / 6.0);
+        S[fb][fa] += len * (1.0 / 6.0);
+      }
+    } else {   // H1_SEMI / ELLIPTIC: K = |det| kappa J^-1 A J^-T
+      const double id = rcp_nr(det);
+      const double i00 = j11 * id, i01 = -j01 * id, i10 = -j10 * id, i11 = j00 * id;
+      double a00 = 1.0, a01 = 0.0, a11 = 1.0, fac = adet;
+      if constexpr (KIND == HDD_PRODUCT_ELLIPTIC) {
+        a00 = o.A.a00; a01 = o.A.a01; a11 = o.A.a11;
+        fac *= o.ke;
+      }
+      const double p00 = i00 * a00 + i01 * a01, p01 = i00 * a01 + i01 * a11;
+      const double p10 = i10 * a00 + i11 * a01, p11 = i10 * a01 + i11 * a11;
+      const double k00 = fac * (p00 * i00 + p01 * i01), k01 = fac * (p00 * i10 + p01 * i11);
+      const double k11 = fac * (p10 * i10 + p11 * i11);
+#pragma unroll
+      for (int i = 0; i < NB; ++i)
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+          if constexpr (std::is_same<E, Simplex>::value) {
+            const double gix = i == 1 ? 1.0 : (i == 0 ? -1.0 : 0.0), giy = i == 2 ? 1.0 : (i == 0 ? -1.0 : 0.0);
+            const double gjx = j == 1 ? 1.0 : (j == 0 ? -1.0 : 0.0), gjy = j == 2 ? 1.0 : (j == 0 ? -1.0 : 0.0);
+            S[i][j] = 0.5 * (gix * (k00 * gjx + k01 * gjy) + giy * (k01 * gjx + k11 * gjy));
+          } else {
+            const int i0 = i & 1, i1 = i >> 1, jj0 = j & 1, jj1 = j >> 1;
+            S[i][j] = k00 * d1(i0, jj0) * m1(i1, jj1) + k01 * c1(i0, jj0) * c1(jj1, i1) +
+                      k01 * c1(jj0, i0) * c1(i1, jj1) + k11 * m1(i0, jj0) * d1(i1, jj1);
+          }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+#pragma unroll
+      for (int j = 0; j < NB; ++j) img[i * NB + j] = S[i][j];
   }
 };
 
@@ -1427,6 +1549,19 @@ static hipError_t launch_persistent(const AssembleArgs& a, hipStream_t s)
   return hipSuccess;
 }
 
+// instantiate a policy for the runtime (tensor kind, piecewise-constant kappa kind) pair
+template <template <int, int> class PT>
+static hipError_t dispatch_pwc(const AssembleArgs& a, hipStream_t s)
+{
+  const int tk = a.tkind;
+  const bool pe = a.kappa[0].kind == HDD_FN_PER_ELEM;
+  if (tk == HDD_TENSOR_CONST)
+    return pe ? launch_persistent<PT<HDD_TENSOR_CONST, HDD_FN_PER_ELEM>>(a, s) : launch_persistent<PT<HDD_TENSOR_CONST, HDD_FN_CONST>>(a, s);
+  if (tk == HDD_TENSOR_ISO_PER_ELEM)
+    return pe ? launch_persistent<PT<HDD_TENSOR_ISO_PER_ELEM, HDD_FN_PER_ELEM>>(a, s) : launch_persistent<PT<HDD_TENSOR_ISO_PER_ELEM, HDD_FN_CONST>>(a, s);
+  return pe ? launch_persistent<PT<HDD_TENSOR_SYM_PER_ELEM, HDD_FN_PER_ELEM>>(a, s) : launch_persistent<PT<HDD_TENSOR_SYM_PER_ELEM, HDD_FN_CONST>>(a, s);
+}
+
 // instantiate a policy for the runtime (tensor kind, kappa kind) pair
 template <template <int, int> class PT>
 static hipError_t dispatch_kinds(const AssembleArgs& a, hipStream_t s, bool smooth)
@@ -1472,6 +1607,59 @@ static hipError_t launch_components(const AssembleArgs& a, int nqv, int nqf, hip
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
+}
+
+// ------------------------------------------------------------------------------------------------
+// products (hdd_product_assemble) on the persistent driver: P1 / Q1 with piecewise-constant kappa; the
+// caller falls back to the generic product kernel (rhs.hip) for smooth kappa and hexahedra
+// ------------------------------------------------------------------------------------------------
+template <class E, int KIND>
+static hipError_t launch_vol_product(const AssembleArgs& a, hipStream_t s)
+{
+  if constexpr (KIND != HDD_PRODUCT_ELLIPTIC) {
+    return launch_persistent<VolProductPolicy<E, KIND, HDD_TENSOR_CONST, HDD_FN_CONST>>(a, s);
+  } else {
+    const bool pe = a.kappa[0].kind == HDD_FN_PER_ELEM;
+    if (a.tkind == HDD_TENSOR_CONST)
+      return pe ? launch_persistent<VolProductPolicy<E, KIND, HDD_TENSOR_CONST, HDD_FN_PER_ELEM>>(a, s)
+                : launch_persistent<VolProductPolicy<E, KIND, HDD_TENSOR_CONST, HDD_FN_CONST>>(a, s);
+    if (a.tkind == HDD_TENSOR_ISO_PER_ELEM)
+      return pe ? launch_persistent<VolProductPolicy<E, KIND, HDD_TENSOR_ISO_PER_ELEM, HDD_FN_PER_ELEM>>(a, s)
+                : launch_persistent<VolProductPolicy<E, KIND, HDD_TENSOR_ISO_PER_ELEM, HDD_FN_CONST>>(a, s);
+    return pe ? launch_persistent<VolProductPolicy<E, KIND, HDD_TENSOR_SYM_PER_ELEM, HDD_FN_PER_ELEM>>(a, s)
+              : launch_persistent<VolProductPolicy<E, KIND, HDD_TENSOR_SYM_PER_ELEM, HDD_FN_CONST>>(a, s);
+  }
+}
+
+template <int TK, int KK> using P1Pen = P1PwcPolicy<TK, KK, true>;
+template <int TK, int KK> using Q1Pen = Q1PwcPolicy<TK, KK, true>;
+
+hipError_t launch_product_fast(const AssembleArgs& a, int product, hipStream_t s, bool* supported)
+{
+  *supported = true;
+  const int kk = a.kappa[0].kind;
+  const bool uses_kappa = product == HDD_PRODUCT_ELLIPTIC || product == HDD_PRODUCT_PENALTY;
+  if ((uses_kappa && kk != HDD_FN_CONST && kk != HDD_FN_PER_ELEM) ||
+      (a.elem_type != HDD_SIMPLEX && a.elem_type != HDD_CUBE)) {
+    *supported = false;
+    return hipSuccess;
+  }
+  const bool tri = a.elem_type == HDD_SIMPLEX;
+  switch (product) {
+    case HDD_PRODUCT_L2:
+      return tri ? launch_vol_product<Simplex, HDD_PRODUCT_L2>(a, s) : launch_vol_product<Cube, HDD_PRODUCT_L2>(a, s);
+    case HDD_PRODUCT_H1_SEMI:
+      return tri ? launch_vol_product<Simplex, HDD_PRODUCT_H1_SEMI>(a, s)
+                 : launch_vol_product<Cube, HDD_PRODUCT_H1_SEMI>(a, s);
+    case HDD_PRODUCT_ELLIPTIC:
+      return tri ? launch_vol_product<Simplex, HDD_PRODUCT_ELLIPTIC>(a, s)
+                 : launch_vol_product<Cube, HDD_PRODUCT_ELLIPTIC>(a, s);
+    case HDD_PRODUCT_BOUNDARY_L2:
+      return tri ? launch_vol_product<Simplex, HDD_PRODUCT_BOUNDARY_L2>(a, s)
+                 : launch_vol_product<Cube, HDD_PRODUCT_BOUNDARY_L2>(a, s);
+    default:
+      return tri ? dispatch_pwc<P1Pen>(a, s) : dispatch_pwc<Q1Pen>(a, s);
+  }
 }
 
 int volume_points(int elem_type, int order)

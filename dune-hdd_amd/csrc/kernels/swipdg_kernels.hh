@@ -115,6 +115,9 @@ hipError_t launch_product(const ProductArgs& a, hipStream_t s);
 int volume_points(int elem_type, int order);
 int face_points(int order);
 hipError_t launch_assemble(const AssembleArgs& a, int nqv, int nqf, hipStream_t s, bool* supported);
+// products of P1 / Q1 meshes with piecewise-constant kappa on the persistent tile driver (closed forms);
+// *supported = false: use launch_product
+hipError_t launch_product_fast(const AssembleArgs& a, int product, hipStream_t s, bool* supported);
 
 }  // namespace dev
 }  // namespace hdd

@@ -15,6 +15,11 @@
       streamed-slab mode: the grid is cut into x-slabs (rank-local meshes with face ghosts)
       whose row blocks are assembled in turn into one rotating value buffer; the time is one pass over all
       slabs (values of earlier slabs are overwritten -- a throughput measurement, nothing is skipped).
+  f   the SURVEY.md 8(f) rows on the C2 mesh (3200 x 640 Kuhn P1, synthetic SPE10 tensor): device pattern
+      build (hdd_pattern_elem_ptr_device + hdd_pattern_fill_device), the SWIPDG right-hand side
+      (L2Volume(ESV2007 force, order 3) + DirichletBoundarySWIPDG(g_D = 1)), and the products l2 / h1_semi /
+      elliptic (element-diagonal volume pattern) and the SWIPDG penalty (full pattern).  Bytes per call are
+      the algorithmic ones: outputs written once + the element records read.
 Prints one JSON line per config."""
 import argparse
 import json
@@ -87,6 +92,56 @@ def c4(args):
     dofs = 4 * loc.n_own
     return dict(config="c4_spe10_q1_%dx%d_block8x8" % (nx, ny), dofs=dofs, nnz=dp.nnz, assembly_ms=t * 1e3,
                 assembled_dofs_per_s=dofs / t, alg_GBps=alg / t / 1e9, roofline_frac=alg / t / 8e12)
+
+
+def f(args):
+    import torch
+    import hdd_amd as H
+    nx, ny = (args.n or 3200), (args.n and args.n // 5) or 640
+    grid = H.Grid.structured(H.SIMPLEX, nx, ny, (0, 0), (5, 1))
+    loc = grid.local()
+    rng = np.random.default_rng(10)
+    k = torch.from_numpy(loc.checkerboard((0, 0), (5, 1), 100, 20, 10.0 ** rng.uniform(-3, 3, 2000))).cuda()
+    ctx = H.Context(0)
+    dm = H.DeviceMesh(loc)
+    ne, N = loc.n_own, 3 * loc.n_own
+    res = dict(config="f_rows_spe10_kuhn%dx%d" % (nx, ny), dofs=N)
+    # device pattern (timed by wall clock around the synchronising builder)
+    gid = torch.from_numpy(loc.global_id).cuda()
+    ep = torch.empty(ne + 1, dtype=torch.int64, device="cuda")
+    nnz = H.C.c_int64()
+    s = torch.cuda.current_stream().cuda_stream
+
+    def pattern():
+        H._check(H.lib().hdd_pattern_elem_ptr_device(ctx.h, H.C.byref(dm.t), 3, ep.data_ptr(), H.C.byref(nnz),
+                                                    H.C.c_void_p(s)))
+        H._check(H.lib().hdd_pattern_fill_device(ctx.h, H.C.byref(dm.t), 3, gid.data_ptr(), ep.data_ptr(),
+                                                 rp.data_ptr(), col.data_ptr(), H.C.c_void_p(s)))
+    pattern_probe = H.DevicePattern(loc, ctx=ctx, dmesh=dm, on_device=True)
+    rp = torch.empty(N + 1, dtype=torch.int64, device="cuda")
+    col = torch.empty(pattern_probe.nnz, dtype=torch.int32, device="cuda")
+    t = timed(pattern, args.steps, args.warmup)
+    pb = 8 * (N + 1) + 4 * pattern_probe.nnz + 8 * (ne + 1) + ne * (12 + 8)
+    res.update(pattern_ms=t * 1e3, pattern_GBps=pb / t / 1e9, pattern_nnz=pattern_probe.nnz)
+    # right-hand side
+    ten = H.tensor_fn(H.TENSOR_ISO_PER_ELEM, per_elem=k)
+    out = torch.empty(N, dtype=torch.float64, device="cuda")
+    fn = lambda: H.rhs(ctx, dm, force=H.esv2007_force(), kappa=H.scalar_fn(H.FN_CONST, 1.0), tensor=ten,
+                       dirichlet=H.scalar_fn(H.FN_CONST, 1.0), out=out)
+    t = timed(fn, args.steps, args.warmup)
+    rb = 8 * N + ne * (48 + 12 + 8)
+    res.update(rhs_ms=t * 1e3, rhs_GBps=rb / t / 1e9)
+    # products
+    dpv = H.DevicePattern(loc, volume=True)
+    dpf = H.DevicePattern(loc)
+    for name, kind, dp in (("l2", H.PRODUCT_L2, dpv), ("h1_semi", H.PRODUCT_H1_SEMI, dpv),
+                           ("elliptic", H.PRODUCT_ELLIPTIC, dpv), ("penalty", H.PRODUCT_PENALTY, dpf)):
+        o = torch.empty(dp.nnz, dtype=torch.float64, device="cuda")
+        fn = lambda: H.product(ctx, dm, kind, dp, kappa=H.scalar_fn(H.FN_CONST, 1.0), tensor=ten, out=o)
+        t = timed(fn, args.steps, args.warmup)
+        b = 8 * dp.nnz + ne * (48 + 12 + 8)
+        res.update({name + "_ms": t * 1e3, name + "_GBps": b / t / 1e9, name + "_nnz": dp.nnz})
+    return res
 
 
 def c5(args):
@@ -192,7 +247,7 @@ def main():
     import torch
     torch.cuda.set_device(0)
     for c in args.configs:
-        print(json.dumps(dict(c3=c3, c4=c4, c5=c5, c5s=c5s)[c](args)), flush=True)
+        print(json.dumps(dict(c3=c3, c4=c4, c5=c5, c5s=c5s, f=f)[c](args)), flush=True)
 
 
 if __name__ == "__main__":

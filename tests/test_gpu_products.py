@@ -61,3 +61,35 @@ def test_products_hex(ctx, deg):
         assert np.array_equal(dp.host[0], rp) and np.array_equal(dp.host[1], col), kind
         worst, ok = compare_rows(rp, val.cpu().numpy(), oval, 1e-12)
         assert ok, (kind, worst)
+
+
+@pytest.mark.parametrize("et", [H.SIMPLEX, H.CUBE])
+def test_products_pwc_fast_path(ctx, et):
+    """The closed-form products on the persistent tile driver (piecewise-constant kappa and tensor): Kuhn
+    triangles / sheared parallelograms large enough for full 64-element tiles, a per-element diffusion
+    factor and an anisotropic SPD tensor per element, against the oracle's quadrature."""
+    torch = _torch()
+    nx, ny = 70, 30
+    et_, coords, ev = (O.kuhn_grid if et == H.SIMPLEX else O.cube_grid)(nx, ny, (0, 0), (1, 1))
+    coords = coords @ np.array([[1.3, 0.45], [-0.2, 0.9]]).T + np.array([0.3, -0.1])
+    grid = H.Grid.from_connectivity(et, coords, ev)
+    loc = grid.local()
+    dm = H.DeviceMesh(loc)
+    og = O.Grid(et_, coords, ev)
+    rng = np.random.default_rng(11)
+    ne = ev.shape[0]
+    a = rng.uniform(0.5, 2.0, ne); c = rng.uniform(0.5, 2.0, ne); b = rng.uniform(-0.3, 0.3, ne)
+    sym = np.stack([a, b, c], 0)
+    kap = rng.uniform(0.1, 10.0, ne)
+    hk = H.scalar_fn(H.FN_PER_ELEM, per_elem=torch.from_numpy(kap).cuda())
+    ht = H.tensor_fn(H.TENSOR_SYM_PER_ELEM, per_elem=torch.from_numpy(np.ascontiguousarray(sym)).cuda())
+    ok_ = O.scalar(O.FN_PER_ELEM, per_elem=kap)
+    ot = O.tensor(O.TENSOR_SYM_PER_ELEM, per_elem=np.ascontiguousarray(sym.T))
+    for kind in KINDS:
+        dp = H.DevicePattern(loc, volume=kind != H.PRODUCT_PENALTY)
+        val = H.product(ctx, dm, kind, dp, kappa=hk, tensor=ht, prm=H.params())
+        torch.cuda.synchronize()
+        rp, col, oval = O.product(og, kind, kappa=ok_, A=ot, prm=O.params())
+        assert np.array_equal(dp.host[0], rp) and np.array_equal(dp.host[1], col), kind
+        worst, ok = compare_rows(rp, val.cpu().numpy(), oval, 1e-12)
+        assert ok, (kind, worst)
