@@ -756,6 +756,93 @@ __global__ void pattern_fill_kernel(const int32_t* __restrict__ nbrs, int32_t nf
   }
 }
 
+// P1 / Q1 (nb = nf = 3 or 4): one wave per 64-element tile, lane = element.  The lane sorts its <= nf + 1
+// column blocks in registers, stages its row block of column ids in an LDS image of the tile (offsets from
+// ballots, the elem_ptr rule) and the wave streams the tile's contiguous column range out with 16-byte
+// stores: no 64-bit divisions, no per-entry block search (the wave-per-element kernel above keeps hexahedra).
+__device__ __forceinline__ int lanes_below(uint64_t m)
+{
+  return int(__builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u)));
+}
+
+template <int NB, int NF>
+__global__ void __launch_bounds__(64) pattern_fill_tile_kernel(const int32_t* __restrict__ nbrs, int64_t n_local,
+                                                               int64_t own_begin, int64_t n_own,
+                                                               const int64_t* __restrict__ gid,
+                                                               const int64_t* __restrict__ elem_ptr,
+                                                               int64_t* __restrict__ row_ptr, int32_t* __restrict__ col,
+                                                               int64_t n_tiles)
+{
+  constexpr int RB = (NF + 1) * NB * NB;
+  __shared__ __attribute__((aligned(16))) int32_t img[64 * RB + 8 + RB];
+  typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+  const int lane = threadIdx.x;
+  for (int64_t t = blockIdx.x; t < n_tiles; t += gridDim.x) {
+    const int64_t k0 = t * 64, k = k0 + lane;
+    const bool active = k < n_own;
+    const int64_t e = own_begin + (active ? k : k0);
+    int64_t key[NF + 1];
+    key[0] = gid ? gid[e] : e;
+    int nblk = 1;
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+      const int32_t nf = nbrs[f * n_local + e];
+      key[f + 1] = nf >= 0 ? (gid ? gid[nf] : int64_t(nf)) : INT64_MAX;
+      nblk += nf >= 0;
+    }
+#pragma unroll
+    for (int i = 0; i < NF; ++i)   // sorting network (bubble, compile-time)
+#pragma unroll
+      for (int j = 0; j < NF - i; ++j) {
+        const int64_t lo = key[j] < key[j + 1] ? key[j] : key[j + 1];
+        const int64_t hi = key[j] < key[j + 1] ? key[j + 1] : key[j];
+        key[j] = lo;
+        key[j + 1] = hi;
+      }
+    const int64_t kend = k0 + 64 < n_own ? k0 + 64 : n_own;
+    const int64_t base = __builtin_amdgcn_readfirstlane(elem_ptr[k0]);
+    const int64_t tend = __builtin_amdgcn_readfirstlane(elem_ptr[kend]);
+    const int64_t al = base & ~int64_t(3);
+    const int c = nblk - 1;
+    int sum = lanes_below(__ballot(active));
+    sum += lanes_below(__ballot(active && (c & 1)));
+    sum += 2 * lanes_below(__ballot(active && (c & 2)));
+    sum += 4 * lanes_below(__ballot(active && (c & 4)));
+    const int off = NB * NB * sum;
+    const int rl = NB * nblk;
+    if (active) {
+#pragma unroll
+      for (int i = 0; i < NB; ++i) row_ptr[k * NB + i] = base + off + i * rl;
+      if (k == n_own - 1) row_ptr[n_own * NB] = base + off + NB * rl;
+    }
+    int32_t* my = active ? img + (base - al) + off : img + 64 * RB + 8;
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+#pragma unroll
+      for (int b = 0; b <= NF; ++b)
+        if (b < nblk)
+#pragma unroll
+          for (int j = 0; j < NB; ++j) my[i * rl + b * NB + j] = int32_t(key[b] * NB + j);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int64_t n16 = (tend - al + 3) >> 2;
+    for (int64_t q = lane; q < n16; q += 64) {
+      const int64_t g0 = al + 4 * q;
+      if (g0 >= base && g0 + 4 <= tend) {
+        *reinterpret_cast<i32x4*>(col + g0) = *reinterpret_cast<const i32x4*>(img + 4 * q);
+      } else {
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (g0 + u >= base && g0 + u < tend) col[g0 + u] = img[4 * q + u];
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+}
+
 hipError_t launch_pattern_counts(const int32_t* nbrs, int32_t nf, int64_t n_local, int64_t own_begin, int64_t own_end,
                                  int64_t nb2, int64_t* d_counts, hipStream_t s)
 {
@@ -772,6 +859,20 @@ hipError_t launch_pattern_fill(const int32_t* nbrs, int32_t nf, int32_t nb, int6
 {
   const int64_t n_own = own_end - own_begin;
   if (n_own <= 0) return hipSuccess;
+  if ((nb == 3 && nf == 3) || (nb == 4 && nf == 4)) {
+    int dev = 0, cus = 256;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const int64_t tiles = (n_own + 63) / 64;
+    const unsigned grid = unsigned(std::min<int64_t>(tiles, int64_t(cus) * 8));
+    if (nb == 3)
+      hipLaunchKernelGGL((pattern_fill_tile_kernel<3, 3>), dim3(grid), dim3(64), 0, s, nbrs, n_local, own_begin, n_own,
+                         gid, elem_ptr, row_ptr, col, tiles);
+    else
+      hipLaunchKernelGGL((pattern_fill_tile_kernel<4, 4>), dim3(grid), dim3(64), 0, s, nbrs, n_local, own_begin, n_own,
+                         gid, elem_ptr, row_ptr, col, tiles);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(pattern_fill_kernel, dim3(unsigned((n_own + 3) / 4)), dim3(256), 0, s, nbrs, nf, nb, n_local,
                      own_begin, n_own, gid, elem_ptr, row_ptr, col);
   return hipGetLastError();

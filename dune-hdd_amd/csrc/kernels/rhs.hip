@@ -10,6 +10,7 @@
 // the kernel is written for generality, not for a roofline.  Quadrature rules come from the host.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 
 #include "swipdg_kernels.hh"
@@ -210,6 +211,123 @@ __global__ __launch_bounds__(256) void rhs_kernel(RhsArgs a)
       }
     }
     a.out[t] = acc;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------
+// P1 / Q1 right-hand side, one thread per element: the geometry, the functions' values at the quadrature
+// points and the face data are evaluated once per element (rhs_kernel above repeats them per basis
+// function), the nb values of the element are accumulated in registers.  Same rules and formulas.
+// ---------------------------------------------------------------------------------------------------
+template <bool TRI>
+__device__ __forceinline__ void rhs2d_shape(double x, double y, double* v, double* gx, double* gy)
+{
+  if constexpr (TRI) {
+    v[0] = 1.0 - x - y; v[1] = x; v[2] = y;
+    gx[0] = -1.0; gy[0] = -1.0; gx[1] = 1.0; gy[1] = 0.0; gx[2] = 0.0; gy[2] = 1.0;
+  } else {
+    v[0] = (1 - x) * (1 - y); v[1] = x * (1 - y); v[2] = (1 - x) * y; v[3] = x * y;
+    gx[0] = -(1 - y); gy[0] = -(1 - x); gx[1] = 1 - y; gy[1] = -x; gx[2] = -y; gy[2] = 1 - x; gx[3] = y; gy[3] = x;
+  }
+}
+
+template <bool TRI>
+__global__ __launch_bounds__(256) void rhs2d_kernel(RhsArgs a)
+{
+  constexpr int NB = TRI ? 3 : 4, NF = TRI ? 3 : 4;
+  const int64_t n_own = a.own_end - a.own_begin;
+  const int64_t n = a.n_local;
+  for (int64_t k = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; k < n_own; k += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t e = a.own_begin + k;
+    const double x0 = a.coords[e], y0 = a.coords[n + e];
+    const double j00 = a.coords[2 * n + e] - x0, j10 = a.coords[3 * n + e] - y0;   // vertex 1 - vertex 0
+    const double j01 = a.coords[4 * n + e] - x0, j11 = a.coords[5 * n + e] - y0;   // vertex 2 - vertex 0
+    const double det = j00 * j11 - j01 * j10, adet = fabs(det);
+    double acc[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) acc[i] = 0.0;
+    double v[NB], gx[NB], gy[NB], xq[2];
+    if (a.has_force) {
+      for (int q = 0; q < a.nqv; ++q) {
+        const double xh = a.qv[q][0], yh = a.qv[q][1];
+        xq[0] = x0 + j00 * xh + j01 * yh;
+        xq[1] = y0 + j10 * xh + j11 * yh;
+        rhs2d_shape<TRI>(xh, yh, v, gx, gy);
+        const double fv = a.qv[q][3] * adet * rhs_fn(a.force, e, xq, 2);
+#pragma unroll
+        for (int i = 0; i < NB; ++i) acc[i] += fv * v[i];
+      }
+    }
+    if (a.has_dirichlet || a.has_neumann) {
+      const double i00 = j11 / det, i01 = -j01 / det, i10 = -j10 / det, i11 = j00 / det;
+#pragma unroll
+      for (int f = 0; f < NF; ++f) {
+        const int32_t nbr = a.nbrs[f * n + e];
+        const bool dir = nbr == HDD_NBR_DIRICHLET && a.has_dirichlet;
+        const bool neu = nbr == HDD_NBR_NEUMANN && a.has_neumann;
+        if (!dir && !neu) continue;
+        double r0[2] = {0, 0}, t1[2] = {0, 0}, nr[2] = {0, 0};
+        if constexpr (TRI) {
+          const double P[3][2] = {{0, 0}, {1, 0}, {0, 1}};
+          const int fv[3][2] = {{0, 1}, {0, 2}, {1, 2}};
+          const double N[3][2] = {{0, -1}, {-1, 0}, {1, 1}};
+          for (int c = 0; c < 2; ++c) {
+            r0[c] = P[fv[f][0]][c];
+            t1[c] = P[fv[f][1]][c] - P[fv[f][0]][c];
+            nr[c] = N[f][c];
+          }
+        } else {
+          const int af = f >> 1, sd = f & 1;
+          r0[af] = sd;
+          nr[af] = sd ? 1.0 : -1.0;
+          t1[1 - af] = 1.0;
+        }
+        double nvx = i00 * nr[0] + i10 * nr[1], nvy = i01 * nr[0] + i11 * nr[1];
+        const double nn = sqrt(nvx * nvx + nvy * nvy);
+        nvx /= nn;
+        nvy /= nn;
+        const double dx = j00 * t1[0] + j01 * t1[1], dy = j10 * t1[0] + j11 * t1[1];
+        const double fvol = sqrt(dx * dx + dy * dy);
+        const double* qs = dir ? &a.qd[0][0] : &a.qn[0][0];
+        const int nq = dir ? a.nqd : a.nqn;
+        double cr0 = 0.0, cr1 = 0.0, gamma = 0.0, hpow = 1.0;
+        if (dir) {
+          double A00, A01, A11;
+          if (a.tkind == HDD_TENSOR_ISO_PER_ELEM) {
+            A00 = A11 = a.tper[e];
+            A01 = 0.0;
+          } else if (a.tkind == HDD_TENSOR_SYM_PER_ELEM) {
+            A00 = a.tper[e]; A01 = a.tper[n + e]; A11 = a.tper[2 * n + e];
+          } else {
+            A00 = a.tc[0]; A01 = a.tc[1]; A11 = a.tc[2];
+          }
+          const double Anx = A00 * nvx + A01 * nvy, Any = A01 * nvx + A11 * nvy;
+          gamma = nvx * Anx + nvy * Any;
+          cr0 = i00 * Anx + i01 * Any;   // (A grad phi_i) . n = (J^{-1} A n) . grad_ref phi_i
+          cr1 = i10 * Anx + i11 * Any;
+          hpow = pow(fvol, a.beta);
+        }
+        for (int q = 0; q < nq; ++q) {
+          const double s0 = qs[3 * q], w = qs[3 * q + 2];
+          const double xh = r0[0] + s0 * t1[0], yh = r0[1] + s0 * t1[1];
+          xq[0] = x0 + j00 * xh + j01 * yh;
+          xq[1] = y0 + j10 * xh + j11 * yh;
+          rhs2d_shape<TRI>(xh, yh, v, gx, gy);
+          const double gv = w * fvol * rhs_fn(dir ? a.dirichlet : a.neumann, e, xq, 2);
+          if (dir) {
+            const double kap = rhs_fn(a.kappa, e, xq, 2);
+            const double pen = a.sigma_boundary * kap * gamma / hpow;
+#pragma unroll
+            for (int i = 0; i < NB; ++i) acc[i] += gv * (-kap * (cr0 * gx[i] + cr1 * gy[i]) + pen * v[i]);
+          } else {
+#pragma unroll
+            for (int i = 0; i < NB; ++i) acc[i] += gv * v[i];
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) a.out[k * NB + i] = acc[i];
   }
 }
 
@@ -468,7 +586,19 @@ hipError_t launch_product(const ProductArgs& a, hipStream_t s)
 
 hipError_t launch_rhs(const RhsArgs& a, hipStream_t s)
 {
-  const int64_t total = (a.own_end - a.own_begin) * a.nb;
+  const int64_t n_own = a.own_end - a.own_begin;
+  if (a.elem_type != HDD_HEX && n_own > 0) {
+    int dev = 0, cus = 256;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const int64_t blocks = std::min<int64_t>((n_own + 255) / 256, int64_t(cus) * 8);
+    if (a.elem_type == HDD_SIMPLEX)
+      hipLaunchKernelGGL(rhs2d_kernel<true>, dim3(unsigned(blocks)), dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL(rhs2d_kernel<false>, dim3(unsigned(blocks)), dim3(256), 0, s, a);
+    return hipGetLastError();
+  }
+  const int64_t total = n_own * a.nb;
   if (total <= 0) return hipSuccess;
   const int64_t blocks = (total + 255) / 256;
   hipLaunchKernelGGL(rhs_kernel, dim3(unsigned(blocks < (1 << 20) ? blocks : (1 << 20))), dim3(256), 0, s, a);

@@ -133,3 +133,20 @@ def test_device_pattern_equals_host(ctx, kind):
     assert np.array_equal(dpat.row_ptr.cpu().numpy(), host[0])
     assert np.array_equal(dpat.col.cpu().numpy(), host[1])
     assert np.array_equal(dpat.elem_ptr.cpu().numpy(), host[2])
+
+
+@pytest.mark.parametrize("et", [H.SIMPLEX, H.CUBE])
+def test_device_pattern_tiles_equal_host(ctx, et):
+    """The tiled P1/Q1 device pattern builder over many 64-element tiles (ragged last tile, ghosts,
+    block numbering through global ids) equals the host pattern."""
+    torch = _torch()
+    g = H.Grid.structured(et, 203, 41, px=4, py=3)
+    loc = g.local(2, 9)
+    host = loc.pattern()
+    dpat = H.DevicePattern(loc, ctx=ctx, on_device=True)
+    torch.cuda.synchronize()
+    assert loc.n_own % 64 != 0
+    assert dpat.nnz == host[1].shape[0]
+    assert np.array_equal(dpat.row_ptr.cpu().numpy(), host[0])
+    assert np.array_equal(dpat.col.cpu().numpy(), host[1])
+    assert np.array_equal(dpat.elem_ptr.cpu().numpy(), host[2])
