@@ -20,6 +20,10 @@
       (L2Volume(ESV2007 force, order 3) + DirichletBoundarySWIPDG(g_D = 1)), and the products l2 / h1_semi /
       elliptic (element-diagonal volume pattern) and the SWIPDG penalty (full pattern).  Bytes per call are
       the algorithmic ones: outputs written once + the element records read.
+  ops BlockSWIPDG operator extraction (get_local_operator / get_coupling_operator, block-swipdg.hh:612-690)
+      on the C4 layout (Q1, 8 x 8 subdomains; --n sets nx, default 3520): every local and every coupling
+      operator's values gathered from the assembled global matrix in one hdd_gather_values pass (maps
+      built once on the host by hdd_block_operator_map); bytes = 8 read + 8 index + 8 written per value.
 Prints one JSON line per config."""
 import argparse
 import json
@@ -144,6 +148,47 @@ def f(args):
     return res
 
 
+def ops(args):
+    import torch
+    import hdd_amd as H
+    nx = args.n or 3520
+    ny = nx * 1200 // 3520
+    grid = H.Grid.structured(H.CUBE, nx, ny, (0, 0), (5, 1), px=8, py=8)
+    loc = grid.local()
+    rp, col, _ = loc.pattern()
+    t0 = time.perf_counter()
+    srcs, n_ops = [], 0
+    for ss in range(64):
+        sx, sy = divmod(ss, 8)
+        for nn in [ss] + [(sx + dx) * 8 + sy + dy for dx, dy in ((-1, 0), (1, 0), (0, -1), (0, 1))
+                          if 0 <= sx + dx < 8 and 0 <= sy + dy < 8]:
+            nnz = H.C.c_int64()
+            H._check(H.lib().hdd_block_operator_map(grid.h, ss, nn, H._p(rp), H._p(col), None, None, None,
+                                                    H.C.byref(nnz)))
+            src = np.empty(nnz.value, np.int64)
+            ocol = np.empty(nnz.value, np.int32)
+            orp = np.empty(4 * grid.ne + 1, np.int64)   # upper bound of the operator's rows + 1
+            H._check(H.lib().hdd_block_operator_map(grid.h, ss, nn, H._p(rp), H._p(col), H._p(orp), H._p(ocol),
+                                                    H._p(src), H.C.byref(nnz)))
+            srcs.append(src)
+            n_ops += 1
+    t_map = time.perf_counter() - t0
+    src = torch.from_numpy(np.concatenate(srcs)).cuda()
+    ctx = H.Context(0)
+    dm, dp = H.DeviceMesh(loc), H.DevicePattern(loc)
+    rng = np.random.default_rng(10)
+    k = torch.from_numpy(loc.checkerboard((0, 0), (5, 1), 100, 20, 10.0 ** rng.uniform(-3, 3, 2000))).cuda()
+    (vals,) = H.assemble(ctx, dm, dp, [H.scalar_fn(H.FN_CONST, 1.0)], H.tensor_fn(H.TENSOR_ISO_PER_ELEM, per_elem=k))
+    out = torch.empty(src.numel(), dtype=torch.float64, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    fn = lambda: H._check(H.lib().hdd_gather_values(ctx.h, H.C.c_void_p(vals.data_ptr()), H.C.c_void_p(src.data_ptr()),
+                                                    src.numel(), H.C.c_void_p(out.data_ptr()), H.C.c_void_p(s)))
+    t = timed(fn, args.steps, args.warmup)
+    n = src.numel()
+    return dict(config="ops_block_swipdg_q1_%dx%d_8x8" % (nx, ny), operators=n_ops, values=n, global_nnz=dp.nnz,
+                host_map_s=t_map, gather_ms=t * 1e3, gather_GBps=24 * n / t / 1e9)
+
+
 def c5(args):
     import torch
     import hdd_amd as H
@@ -247,7 +292,7 @@ def main():
     import torch
     torch.cuda.set_device(0)
     for c in args.configs:
-        print(json.dumps(dict(c3=c3, c4=c4, c5=c5, c5s=c5s, f=f)[c](args)), flush=True)
+        print(json.dumps(dict(c3=c3, c4=c4, c5=c5, c5s=c5s, f=f, ops=ops)[c](args)), flush=True)
 
 
 if __name__ == "__main__":
