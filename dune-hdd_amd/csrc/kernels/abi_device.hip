@@ -173,6 +173,10 @@ static int assemble_hex(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_fn* ka
     a.sigma_inner = p->sigma_inner;
     a.sigma_boundary = p->sigma_boundary;
     a.beta = p->beta;
+    {
+      const char* df = getenv("HDD_DEBUG_FLAGS");   // profiling ablations (HDD_ABLATION builds only)
+      a.debug_flags = df ? atoi(df) : 0;
+    }
     gauss_legendre01(nq1v, a.tab.sv, a.tab.wv);
     gauss_legendre01(nq1f, a.tab.sf, a.tab.wf);
     for (int r = 0; r <= deg; ++r) {

@@ -36,6 +36,12 @@ namespace dev {
 
 typedef double dbl4 __attribute__((ext_vector_type(4)));
 
+#ifdef HDD_ABLATION   // profiling ablations (HDD_DEBUG_FLAGS): 2 = drop the value stores
+#define HDD_HEX_ABL(a, bit) (((a).debug_flags & (bit)) != 0)
+#else
+#define HDD_HEX_ABL(a, bit) false
+#endif
+
 template <int P, int SM>
 struct HexCfg {
   static constexpr int NP = P + 1;
@@ -646,13 +652,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
         for (int I = 0; I < 4; ++I)
 #pragma unroll
-          for (int rr = 0; rr < 4; ++rr) out[(I * 16 + g + 4 * rr) * rl + cofs + col] = E[I][rr];
+          for (int rr = 0; rr < 4; ++rr)
+            if (!HDD_HEX_ABL(a, 2)) out[(I * 16 + g + 4 * rr) * rl + cofs + col] = E[I][rr];
       }
     }
 #pragma unroll
     for (int I = 0; I < 4; ++I)
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) out[(I * 16 + g + 4 * rr) * rl + sofs + col] = S[I][rr];
+      for (int rr = 0; rr < 4; ++rr)
+        if (!HDD_HEX_ABL(a, 2)) out[(I * 16 + g + 4 * rr) * rl + sofs + col] = S[I][rr];
   }
 }
 

@@ -58,6 +58,7 @@ struct HexArgs {
   double* vals;
   double sigma_inner, sigma_boundary, beta;
   double* ws;                   // p=3 register kernel: per-element coefficient records [n_own][HEX_REC]
+  int32_t debug_flags, pad;     // ablations (HDD_ABLATION builds only)
   HexTables tab;
 };
 
