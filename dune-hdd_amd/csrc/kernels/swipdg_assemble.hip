@@ -1228,6 +1228,160 @@ struct P1PwcPolicy {
 };
 
 // ------------------------------------------------------------------------------------------------
+// P1 with a smooth diffusion factor (OS2014 sinusoid, C3): kappa moments.
+//
+// P1 gradients, and hence (A grad phi) . n, are constant on an element, so every integrand is kappa (or
+// kappa^2 in the interior penalty, kappa^- kappa^+ with one smooth kappa) times a polynomial of the trace:
+//   volume   int kappa grad phi_j . A grad phi_i  = |det J| (sum_q w_q kappa(x_q)) g_i . A g_j      (Dunavant 6)
+//   face     int kappa phi_i        = |F| sum_q w_q kappa(x_q) phi_i(s_q)                         (Gauss 3)
+//            int kappa^m phi_i phi_j = |F| sum_q w_q kappa(x_q)^m phi_i(s_q) phi_j(s_q)  (m = 2 inner, 1 Dirichlet)
+// The moments use the reference's points and weights (the same rules as GenericPolicy: integrand orders
+// ord kappa + 0 / ord kappa + 2 with ord kappa = 3), so the entries equal the quadrature form up to
+// rounding, at 15 kappa evaluations and the P1 closed-form entry count per element.
+// ------------------------------------------------------------------------------------------------
+template <int TK>
+struct P1SmoothPolicy {
+  static constexpr int NB = 3, NF = 3;
+  static constexpr int RB = 36;
+  // 8 tiles per CU at <= 256 registers: 0.201 ms per C3 component vs 0.231 at 4 (and 0.230 for the
+  // quadrature policy at 8; profiles/r01/s2/ab_p1s.log)
+  static constexpr int WGCU = 8, MINW = 2;
+  static constexpr bool PAD = false;
+  using Own = P1Own;
+  using Gat = P1Gat;
+  __device__ static void load_own(const AssembleArgs& a, int64_t e, Own& o) { p1_load_own<TK, HDD_FN_CONST>(a, e, o); }
+  __device__ static void load_gat(const AssembleArgs& a, int64_t e, const Own& o, Gat& g)
+  {
+    p1_load_gat<TK, HDD_FN_CONST>(a, e, o, g);
+  }
+  __device__ static int n_interior(const Own& o) { return int(o.nbr[0] >= 0) + int(o.nbr[1] >= 0) + int(o.nbr[2] >= 0); }
+
+  __device__ static void compute(const AssembleArgs& a, int64_t e, const Own& o, const Gat& gt, double* img)
+  {
+    using E = Simplex;
+    const KappaArg& K = a.kappa[0];
+    auto kap = [&](double x, double y) { return K.c + K.b * sin(K.kx * x + K.ky * y); };
+    const double j00 = o.X[1] - o.X[0], j01 = o.X[2] - o.X[0], j10 = o.Y[1] - o.Y[0], j11 = o.Y[2] - o.Y[0];
+    const double det = j00 * j11 - j01 * j10;
+    const double id = rcp_nr(det);
+    const double i00 = j11 * id, i01 = -j01 * id, i10 = -j10 * id, i11 = j00 * id;
+    double g[3][2];
+    g[1][0] = i00; g[1][1] = i01;
+    g[2][0] = i10; g[2][1] = i11;
+    g[0][0] = -i00 - i10; g[0][1] = -i01 - i11;
+    double Ag[3][2];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      Ag[k][0] = o.A.a00 * g[k][0] + o.A.a01 * g[k][1];
+      Ag[k][1] = o.A.a01 * g[k][0] + o.A.a11 * g[k][1];
+    }
+    const double adet = fabs(det);
+    const double osgn = det > 0.0 ? 1.0 : -1.0;
+    int nblk = 1, pos_self = 0, pos[3];
+#pragma unroll
+    for (int f = 0; f < 3; ++f) {
+      nblk += o.nbr[f] >= 0;
+      pos_self += (o.nbr[f] >= 0 && o.nbr[f] < e);
+    }
+#pragma unroll
+    for (int f = 0; f < 3; ++f) {
+      int p = (e < o.nbr[f]) ? 1 : 0;
+#pragma unroll
+      for (int q = 0; q < 3; ++q) p += (o.nbr[q] >= 0 && o.nbr[q] < o.nbr[f]);
+      pos[f] = p;
+    }
+    const int rowlen = nblk * 3;
+    double kv = 0.0;   // sum_q w_q kappa(x_q), Dunavant 6
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+      const double xh = VolRule<Simplex, 6>::x(q), yh = VolRule<Simplex, 6>::y(q);
+      kv += VolRule<Simplex, 6>::w(q) * kap(o.X[0] + j00 * xh + j01 * yh, o.Y[0] + j10 * xh + j11 * yh);
+    }
+    double S[3][3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) S[i][j] = adet * kv * (Ag[j][0] * g[i][0] + Ag[j][1] * g[i][1]);
+#pragma unroll
+    for (int f = 0; f < 3; ++f) {
+      const int32_t n = o.nbr[f];
+      if (n <= HDD_NBR_NEUMANN) continue;
+      const int fa = E::fv(f, 0), fb = E::fv(f, 1), fc = 3 - fa - fb;
+      const double Ax = o.X[fa], Ay = o.Y[fa], Bx = o.X[fb], By = o.Y[fb];
+      const double tx = Bx - Ax, ty = By - Ay;
+      const double il = rsq_nr(tx * tx + ty * ty);
+      const double len = (tx * tx + ty * ty) * il;
+      const double nsc = E::face_sign(f) * osgn * il;
+      const double nx = ty * nsc, ny = -tx * nsc;
+      double Ae[3];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) Ae[k] = Ag[k][0] * nx + Ag[k][1] * ny;
+      const double dm = agn(o.A, nx, ny, nx, ny);
+      const double ihp = a.beta == 1.0 ? il : rcp_nr(pow(len, a.beta));
+      const bool inner = n >= 0;
+      // moments over the face's Gauss 3 points (s from vertex a to vertex b)
+      double k1a = 0.0, k1b = 0.0, qaa = 0.0, qab = 0.0, qbb = 0.0;
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const double sq = Gauss01<3>::s(q), wq = Gauss01<3>::w(q) * len;
+        const double k = kap(Ax + sq * tx, Ay + sq * ty);
+        const double kk = inner ? k * k : k;
+        k1a += wq * k * (1.0 - sq);
+        k1b += wq * k * sq;
+        qaa += wq * kk * (1.0 - sq) * (1.0 - sq);
+        qab += wq * kk * sq * (1.0 - sq);
+        qbb += wq * kk * sq * sq;
+      }
+      auto M1 = [&](int i) { return i == fa ? k1a : (i == fb ? k1b : 0.0); };
+      auto MM = [&](int i, int j) {
+        return (i == fc || j == fc) ? 0.0 : (i != j ? qab : (i == fa ? qaa : qbb));
+      };
+      if (inner) {
+        const uint32_t inf = (o.finfo >> (4 * f)) & 15u;
+        const int tw = int(inf & 7u);
+        const bool rev = (inf & 8u) != 0u;
+        const int ta = E::fv(tw, 0), tb = E::fv(tw, 1), to = 3 - ta - tb;
+        const double Ox = gt.Ox[f], Oy = gt.Oy[f];
+        const Tensor Ap = gt.Ap[f];
+        const double dp = agn(Ap, nx, ny, nx, ny);
+        const double rs = rcp_nr(dp + dm);
+        const double gamma = (dp * dm) * rs;
+        const double w_plus = dm * rs, w_minus = dp * rs;
+        const double pc = (a.sigma_inner * gamma) * ihp;
+        const double iD = rcp_nr((Bx - Ax) * (Oy - Ay) - (By - Ay) * (Ox - Ax));
+        const double mx = Ap.a00 * nx + Ap.a01 * ny, my = Ap.a01 * nx + Ap.a11 * ny;
+        const double AnA = ((By - Oy) * mx + (Ox - Bx) * my) * iD;
+        const double AnB = ((Oy - Ay) * mx + (Ax - Ox) * my) * iD;
+        const double AnO = ((Ay - By) * mx + (Bx - Ax) * my) * iD;
+        const int jA = rev ? tb : ta, jB = rev ? ta : tb;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          double* row = img + i * rowlen + pos[f] * 3;
+          const double m1i = M1(i);
+          row[jA] = -w_plus * AnA * m1i + w_minus * Ae[i] * k1a - pc * MM(i, fa);
+          row[jB] = -w_plus * AnB * m1i + w_minus * Ae[i] * k1b - pc * MM(i, fb);
+          row[to] = -w_plus * AnO * m1i;
+        }
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+          for (int j = 0; j < 3; ++j) S[i][j] += -w_minus * (Ae[j] * M1(i) + Ae[i] * M1(j)) + pc * MM(i, j);
+      } else {   // Dirichlet: SWIPDG::BoundaryLHS, penalty sigma_b kappa (n.An) / |F|^beta
+        const double pc = (a.sigma_boundary * dm) * ihp;
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+          for (int j = 0; j < 3; ++j) S[i][j] += -(Ae[j] * M1(i) + Ae[i] * M1(j)) + pc * MM(i, j);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) img[i * rowlen + pos_self * 3 + j] = S[i][j];
+  }
+};
+
+// ------------------------------------------------------------------------------------------------
 // Element-local products on the element-diagonal (volume) pattern (swipdg.hh:358-461: L2, H1Semi,
 // Elliptic, BoundaryL2 with over_integrate = 2), P1 triangles / Q1 parallelograms, piecewise-constant
 // data.  The reference's rules (orders 2p + 2, 2(p-1) + 2 [+ ord kappa]) integrate these polynomial
@@ -1585,6 +1739,14 @@ template <int TK, int KK> using Q1Pwc = Q1PwcPolicy<TK, KK>;
 template <int TK, int KK> using Q1Smooth3 = GenericPolicy<Cube, 4, 3, TK, KK>;
 template <int TK, int KK> using P1Smooth3 = GenericPolicy<Simplex, 6, 3, TK, KK>;
 
+static hipError_t dispatch_smooth_p1(const AssembleArgs& a, hipStream_t s)
+{
+  if (a.debug_flags & 256) return dispatch_kinds<P1Smooth3>(a, s, true);   // A/B: the quadrature policy
+  if (a.tkind == HDD_TENSOR_CONST) return launch_persistent<P1SmoothPolicy<HDD_TENSOR_CONST>>(a, s);
+  if (a.tkind == HDD_TENSOR_ISO_PER_ELEM) return launch_persistent<P1SmoothPolicy<HDD_TENSOR_ISO_PER_ELEM>>(a, s);
+  return launch_persistent<P1SmoothPolicy<HDD_TENSOR_SYM_PER_ELEM>>(a, s);
+}
+
 // one launch per component: components of one call may differ in kind (affine part const, component
 // per-element, ...) -- the kinds are compile-time inside the kernels
 static hipError_t launch_components(const AssembleArgs& a, int nqv, int nqf, hipStream_t s, bool* supported)
@@ -1597,7 +1759,7 @@ static hipError_t launch_components(const AssembleArgs& a, int nqv, int nqf, hip
     const bool smooth = ac.kappa[0].kind == HDD_FN_SINUSOID;
     hipError_t e = hipSuccess;
     if (ac.elem_type == HDD_SIMPLEX && nqv == 1 && nqf == 2 && !smooth) e = dispatch_kinds<P1Pwc>(ac, s, false);
-    else if (ac.elem_type == HDD_SIMPLEX && nqv == 6 && nqf == 3 && smooth) e = dispatch_kinds<P1Smooth3>(ac, s, true);
+    else if (ac.elem_type == HDD_SIMPLEX && nqv == 6 && nqf == 3 && smooth) e = dispatch_smooth_p1(ac, s);
     else if (ac.elem_type == HDD_CUBE && nqv == 1 && nqf == 2 && !smooth) e = dispatch_kinds<Q1Pwc>(ac, s, false);
     else if (ac.elem_type == HDD_CUBE && nqv == 4 && nqf == 3 && smooth) e = dispatch_kinds<Q1Smooth3>(ac, s, true);
     else {
