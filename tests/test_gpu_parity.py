@@ -312,3 +312,46 @@ def test_parallelogram_mesh_uniform_tiles(ctx, smooth):
     assert np.array_equal(col, ocol)
     worst, ok = compare_rows(rp, val, oval, RTOL)
     assert ok, worst
+
+
+def _scrambled_quad_mesh(nx, ny, seed):
+    """Structured quads whose elements are renumbered by random symmetries of the reference square (Dune
+    cube vertex order kept valid: rotations and reflections), so neighbouring elements see each other's
+    faces under every twin-face id and orientation; then a shear."""
+    et, coords, ev = O.cube_grid(nx, ny, (0, 0), (1, 1))
+    rng = np.random.default_rng(seed)
+    # the 8 symmetries of the square as permutations of the lexicographic vertices (00, 10, 01, 11)
+    syms = [(0, 1, 2, 3), (1, 3, 0, 2), (3, 2, 1, 0), (2, 0, 3, 1),     # rotations
+            (1, 0, 3, 2), (2, 3, 0, 1), (0, 2, 1, 3), (3, 1, 2, 0)]     # reflections
+    pick = rng.integers(0, 8, ev.shape[0])
+    ev = np.stack([ev[k, list(syms[p])] for k, p in enumerate(pick)]).astype(np.int32)
+    coords = coords @ np.array([[1.1, 0.3], [0.0, 0.8]]).T
+    return et, coords, ev
+
+
+@pytest.mark.parametrize("smooth", [False, True])
+def test_scrambled_quad_orientations(ctx, smooth):
+    """Q1 closed-form / quadrature policies against the oracle when faces meet under all twin-face ids and
+    reversals (the role-slot mapping), with full tiles (padded image) present."""
+    torch = _torch()
+    et, coords, ev = _scrambled_quad_mesh(130, 20, 5)
+    grid = H.Grid.from_connectivity(et, coords, ev)
+    local = grid.local()
+    assert np.any((local.face_info & 0x8888) != 0), "expected reversed faces"
+    ne = ev.shape[0]
+    rng = np.random.default_rng(9)
+    t = rng.uniform(0.5, 3.0, ne)
+    if smooth:
+        fns = [H.scalar_fn(H.FN_SINUSOID, 1.0, 0.5, 3.0, 2.0, order=3)]
+        ofn = O.scalar(O.FN_SINUSOID, 1.0, 0.5, 3.0, 2.0, order=3)
+    else:
+        kap = rng.uniform(0.2, 5.0, ne)
+        fns = [H.scalar_fn(H.FN_PER_ELEM, per_elem=torch.from_numpy(kap).cuda())]
+        ofn = O.scalar(O.FN_PER_ELEM, per_elem=kap)
+    local, (rp, col, _), (val,) = _run_product(ctx, grid, fns,
+                                               H.tensor_fn(H.TENSOR_ISO_PER_ELEM, per_elem=torch.from_numpy(t).cuda()))
+    og = O.Grid(et, coords, ev)
+    orp, ocol, oval = O.assemble(og, ofn, O.tensor(O.TENSOR_ISO_PER_ELEM, per_elem=t), O.params())
+    assert np.array_equal(col, ocol)
+    worst, ok = compare_rows(rp, val, oval, RTOL)
+    assert ok, worst
