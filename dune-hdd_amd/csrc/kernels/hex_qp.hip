@@ -517,8 +517,9 @@ typedef const double __attribute__((address_space(4)))* cdptr;   // constant AS:
 
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void hex_q3_kernel(HexArgs a)
 {
-  constexpr int NB = 64;
+  constexpr int NB = 64, XLD = 17;   // per-wave transpose buffer: 64 rows x 16 columns, padded rows
   __shared__ HexTables T;
+  __shared__ double XT[4][NB * XLD];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   {   // flat parallel copy of the by-value tables
@@ -557,32 +558,68 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const int64_t sofs = (hdr >> 32) * NB;
     const double M[3][3] = {{R[2], R[3], R[4]}, {R[3], R[5], R[6]}, {R[4], R[6], R[7]}};
 
-    // ---- volume ----
     dbl4 S[4];
 #pragma unroll
     for (int I = 0; I < 4; ++I) S[I] = dbl4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll 1
-    for (int q2 = 0; q2 < 3; ++q2) {
-      const double lw = T.Lv[wc][q2], dw = T.Dv[wc][q2];
-      const double lI[4] = {T.Lv[0][q2], T.Lv[1][q2], T.Lv[2][q2], T.Lv[3][q2]};
-      const double dI[4] = {T.Dv[0][q2], T.Dv[1][q2], T.Dv[2][q2], T.Dv[3][q2]};
-      const double w2 = T.wv[q2];
-#pragma unroll
-      for (int q1 = 0; q1 < 3; ++q1) {
-        const double wq = wvg * T.wv[q1] * w2;
-        const double D0 = P01[0][q1] * lw, D1 = P01[1][q1] * lw, D2 = P01[2][q1] * dw;
-#pragma unroll
-        for (int ax = 0; ax < 3; ++ax) {
-          const double b = wq * (M[ax][0] * D0 + M[ax][1] * D1 + M[ax][2] * D2);
-#pragma unroll
-          for (int I = 0; I < 4; ++I) S[I] = mfma(P01[ax][q1] * (ax == 2 ? dI[I] : lI[I]), b, S[I]);
-        }
-      }
-    }
 
-    // ---- faces ----
+    // ---- faces, rows rotated to the face normal ----
+    // A-operand rows of a face with normal axis n run in the layout (row tile = basis index along n, lane
+    // r & 3 / r >> 2 = the basis indices along the face's qs / qt axes): the [V] rows (nonzero trace) then
+    // sit on row tile 3 sd for every face, so the [V] part takes one MFMA per k-step instead of four.
+    // Columns stay natural (coalesced 128-byte row stores).  S follows the faces' layouts: x faces ->
+    // (LDS transpose, per wave) natural -> (register transpose, same lane) y layout -> y faces -> natural
+    // -> volume and z faces.  x layout: row n = I + 4 g + 16 rr; y layout: n = g + 4 I + 16 rr.
+    double* xt = XT[w];
+    auto reg_transpose = [&]() __attribute__((always_inline)) {   // (tile, comp) -> (comp, tile), same lane
+      dbl4 Tm[4];
+#pragma unroll
+      for (int I = 0; I < 4; ++I)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) Tm[rr][I] = S[I][rr];
+#pragma unroll
+      for (int I = 0; I < 4; ++I) S[I] = Tm[I];
+    };
 #pragma unroll 1
     for (int f = 0; f < 6; ++f) {
+      if (f == 2) {   // x layout -> natural (cross-lane: via this wave's LDS buffer) -> y layout
+#pragma unroll
+        for (int I = 0; I < 4; ++I)
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr) xt[(I + 4 * g + 16 * rr) * XLD + r] = S[I][rr];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+        for (int I = 0; I < 4; ++I)
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr) S[I][rr] = xt[(16 * I + g + 4 * rr) * XLD + r];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        reg_transpose();   // natural (tile i2, comp i1) -> y layout (tile i1, comp i2)
+      }
+      if (f == 4) {
+        reg_transpose();   // y layout -> natural
+        // ---- volume (natural layout) ----
+#pragma unroll 1
+        for (int q2 = 0; q2 < 3; ++q2) {
+          const double lw = T.Lv[wc][q2], dw = T.Dv[wc][q2];
+          const double lI[4] = {T.Lv[0][q2], T.Lv[1][q2], T.Lv[2][q2], T.Lv[3][q2]};
+          const double dI[4] = {T.Dv[0][q2], T.Dv[1][q2], T.Dv[2][q2], T.Dv[3][q2]};
+          const double w2 = T.wv[q2];
+#pragma unroll
+          for (int q1 = 0; q1 < 3; ++q1) {
+            const double wq = wvg * T.wv[q1] * w2;
+            const double D0 = P01[0][q1] * lw, D1 = P01[1][q1] * lw, D2 = P01[2][q1] * dw;
+#pragma unroll
+            for (int ax = 0; ax < 3; ++ax) {
+              const double b = wq * (M[ax][0] * D0 + M[ax][1] * D1 + M[ax][2] * D2);
+#pragma unroll
+              for (int I = 0; I < 4; ++I) S[I] = mfma(P01[ax][q1] * (ax == 2 ? dI[I] : lI[I]), b, S[I]);
+            }
+          }
+        }
+      }
       const cdptr F = R + 8 + 10 * f;
       const int64_t fk = d2i(F[9]);
       const int kind = int32_t(fk & 0xffffffff);
@@ -590,6 +627,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       const bool inner = kind > 0;
       const int af = f >> 1, sd = f & 1;
       const double cm[3] = {F[0], F[1], F[2]}, cp[3] = {F[3], F[4], F[5]};
+      // coefficients of the rotated row operands: (qs axis, qt axis, normal)
+      const double cr0 = af == 1 ? cm[0] : (af == 0 ? cm[1] : cm[0]);
+      const double cr1 = af == 2 ? cm[1] : cm[2];
+      const double cr2 = cm[af];
       const double ca = F[6], cb = F[7], ce = F[8];
       const double Le0o = sd ? Le0[1] : Le0[0], De0o = sd ? De0[1] : De0[0];
       const double Le1o = sd ? Le1[1] : Le1[0], De1o = sd ? De1[1] : De1[0];
@@ -618,19 +659,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
                              cp[1], cp[2], Vn, Nn);
           const double bEv = et * Vo - al * No, bNv = -be * Nn - et * Vn;   // [V] rows of K
           const double bEn = -al * Vo, bNn = al * Vn;                       // [N] rows of K
-          double Va[4], Na[4];
+          double Va[4], Na[4];   // rotated rows: tile I = normal index, lane (r & 3, r >> 2) = (qs, qt) axes
 #pragma unroll
           for (int I = 0; I < 4; ++I)
-            q3_face_eval<AF>(Le0o, De0o, Le1o, De1o, Lfg0, Dfg0, Lfg1, Dfg1, lf1, df1, T.Lf[I][qt], T.Df[I][qt],
-                             T.Le[I][sd], T.De[I][sd], cm[0], cm[1], cm[2], Va[I], Na[I]);
-          // independent accumulators back to back (S[I] / E[I] reuse is 4-8 MFMAs apart)
-#pragma unroll
-          for (int I = 0; I < 4; ++I)
-            if (AF != 2 || I == 3 * sd) S[I] = mfma(Va[I], bEv, S[I]);   // z faces: [V] rows live on tile 3 sd
-          if (inner) {
-#pragma unroll
-            for (int I = 0; I < 4; ++I)
-              if (AF != 2 || I == 3 * sd) E[I] = mfma(Va[I], bNv, E[I]);
+            q3_face_eval<2>(0.0, 0.0, 0.0, 0.0, Lfg0, Dfg0, Lfg1, Dfg1, lf1, df1, 0.0, 0.0, T.Le[I][sd], T.De[I][sd],
+                            cr0, cr1, cr2, Va[I], Na[I]);
+          // [V] rows live on row tile 3 sd (uniform branch: no runtime-indexed accumulator)
+          if (sd) {
+            S[3] = mfma(Va[3], bEv, S[3]);
+            if (inner) E[3] = mfma(Va[3], bNv, E[3]);
+          } else {
+            S[0] = mfma(Va[0], bEv, S[0]);
+            if (inner) E[0] = mfma(Va[0], bNv, E[0]);
           }
           // [N] rows of K: B = -alpha V- / alpha V+ at the columns; on z faces V vanishes off the face plane,
           // i.e. outside column tile 3 sd (own side) / 3 (1 - sd) (neighbour side): wave-uniform skips
@@ -652,8 +692,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
         for (int I = 0; I < 4; ++I)
 #pragma unroll
-          for (int rr = 0; rr < 4; ++rr)
-            if (!HDD_HEX_ABL(a, 2)) out[(I * 16 + g + 4 * rr) * rl + cofs + col] = E[I][rr];
+          for (int rr = 0; rr < 4; ++rr) {
+            const int row = af == 0 ? I + 4 * g + 16 * rr : (af == 1 ? g + 4 * I + 16 * rr : 16 * I + g + 4 * rr);
+            if (!HDD_HEX_ABL(a, 2)) out[int64_t(row) * rl + cofs + col] = E[I][rr];
+          }
       }
     }
 #pragma unroll

@@ -215,12 +215,14 @@ def c5(args):
     # F = ne 2 nb^2 nq d + nif 24 nb^2 nqf + nbf 6 nb^2 nqf (reference quadrature)
     alg_flops = loc.n_own * 2 * nb * nb * nq * 3 + nif * 24 * nb * nb * nqf + nbf * 6 * nb * nb * nqf
     # executed MFMA work of hex_q3_kernel (v_mfma_f64_16x16x4: 2048 flop), whole element = 4 waves:
-    # volume 27 k-steps x 4 row tiles per wave; x/y faces 32 (S) + 32 (E, inner) per wave; z faces: [V] part
-    # on one row tile and [N] part in one wave only -> 32 (S) + 32 (E) over the 4 waves
+    # volume 27 k-steps x 4 row tiles per wave; every face runs its rows in the layout rotated to its normal,
+    # so the [V] part takes 1 row tile (4 k-steps) per wave; the [N] part 4 tiles x 4 k-steps in every wave
+    # on x / y faces and in one wave only on z faces (column skip) -> x/y: 80 (S) + 80 (E, inner) per face,
+    # z: 32 (S) + 32 (E)
     nbr_own = nbr[:, loc.own_begin:loc.own_end]
     xy_inner = int((nbr_own[:4] >= 0).sum()); xy_dir = int((nbr_own[:4] == H.NBR_DIRICHLET).sum())
     z_inner = int((nbr_own[4:] >= 0).sum()); z_dir = int((nbr_own[4:] == H.NBR_DIRICHLET).sum())
-    n_mfma = (loc.n_own * 4 * 108 + (xy_inner + xy_dir) * 128 + xy_inner * 128 + (z_inner + z_dir) * 32
+    n_mfma = (loc.n_own * 4 * 108 + (xy_inner + xy_dir) * 80 + xy_inner * 80 + (z_inner + z_dir) * 32
               + z_inner * 32) if deg == 3 else 0
     mfma_flops = 2048 * n_mfma
     alg_bytes = 8 * dp.nnz + loc.n_own * (24 * 8 + 8 + 6 * 4)
