@@ -47,7 +47,7 @@ def parse():
     ap.add_argument("--ny", type=int, default=0, help="c2: 640; c4: 1200")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU work of the baseline sample")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01s2.json"))
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo = rehearsal of the N-rank path on one GPU (host-staged halo)")
     ap.add_argument("--no-overlap", action="store_true",
@@ -276,7 +276,7 @@ def main():
                         if world > 1 else "single GPU"}),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "swipdg_persistent_kernel<%s<1, 0>, %s>"
+                         "kernel": "swipdg_persistent_kernel<%s<1, 0, false>, %s>"
                                    % ("Q1PwcPolicy" if c4 else "P1PwcPolicy", "true" if overlap else "false"),
                          "kernel_ms_avg": kernel_ms, "kernel_ms_avg_max_rank": kernel_ms_max,
                          "algorithmic_bytes_per_launch": alg_bytes},
