@@ -228,8 +228,7 @@ def test_golden_fixtures(ctx):
 def test_bench_size_properties(ctx):
     """Full C2 size (3200 x 640 Kuhn, 4.1 M triangles, 147 M nnz): size-independent properties checked on
     the device -- symmetry a_ij = a_ji, zero row sums on rows without Dirichlet faces, positive
-    diagonal -- plus entry-wise parity of sampled tiles against the oracle on sub-grids would need the
-    same coefficients; the full-size oracle comparison runs in test_gpu_large.py."""
+    diagonal.  The entry-wise full-size comparison with the oracle is tests/test_gpu_large.py."""
     torch = _torch()
     perm = O.spe10_synthetic_permeability()
     grid = H.Grid.structured(H.SIMPLEX, 3200, 640, SPE10_LOWER, SPE10_UPPER)
