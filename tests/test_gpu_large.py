@@ -48,3 +48,26 @@ def test_full_size_against_oracle(ctx, cfg):
     assert col.shape[0] == (147386880 if cfg == "c2" else 337768960)
     worst, ok = compare_rows_fast(rp, got, ref, 1e-12)
     assert ok, worst
+
+
+def test_full_size_os2014_components(ctx):
+    """C3 at its quoted size (1024^2 Kuhn triangles, 75.5 M nnz per component): the affine part and the
+    mu-component (sinusoid kappa, integration order 3) in one call, entry-wise against the oracle."""
+    import torch
+    from cases import os2014_components
+    grid = H.Grid.structured(H.SIMPLEX, 1024, 1024, (-1, -1), (1, 1))
+    local = grid.local()
+    comps = os2014_components()
+    dm, dp = H.DeviceMesh(local), H.DevicePattern(local)
+    vals = H.assemble(ctx, dm, dp, [H.scalar_fn(H.FN_SINUSOID, c, b, kx, ky, order=3) for c, b, kx, ky in comps],
+                      H.tensor_fn())
+    torch.cuda.synchronize()
+    rp, col, _ = dp.host
+    assert col.shape[0] == 75460608
+    coords, ev, _ = grid.connectivity()
+    og = O.Grid(H.SIMPLEX, coords, ev)
+    for (c, b, kx, ky), v in zip(comps, vals):
+        _, _, ref = O.assemble_owner(og, O.scalar(O.FN_SINUSOID, c, b, kx, ky, order=3), O.tensor(O.TENSOR_CONST),
+                                     O.params(), pattern=(rp, col), threads=THREADS)
+        worst, ok = compare_rows_fast(rp, v.cpu().numpy(), ref, 1e-12)
+        assert ok, worst
