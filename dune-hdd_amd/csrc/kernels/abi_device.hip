@@ -307,10 +307,12 @@ extern "C" int hdd_swipdg_assemble_tiles(hdd_ctx* ctx, const hdd_mesh* m, const 
 }
 
 // ------------------------------------------------------------------------------------------------
-// theta-lincomb: out[s][k] = sum_q theta[s][q] v_q[k]; up to LC_S samples per launch, 2 values per lane
+// theta-lincomb: out[s][k] = sum_q theta[s][q] v_q[k]; up to LC_S samples per launch (the components are
+// read once per LC_S samples), 2 values per lane written as one 16-byte non-temporal store per sample
 // ------------------------------------------------------------------------------------------------
 namespace {
-constexpr int LC_S = 16;
+constexpr int LC_S = 32;
+typedef double lc_dvec2 __attribute__((ext_vector_type(2)));
 struct LincombArgs {
   const double* v[HDD_MAX_COMP];
   double theta[LC_S][HDD_MAX_COMP];
@@ -328,7 +330,7 @@ __global__ void __launch_bounds__(256) lincomb_kernel(const LincombArgs a)
     for (int c = 0; c < HDD_MAX_COMP; ++c)
       v[c] = c < a.n_comp ? reinterpret_cast<const double2*>(a.v[c])[k] : make_double2(0.0, 0.0);
     for (int s = 0; s < a.n_s; ++s) {
-      double2 r = make_double2(0.0, 0.0);
+      lc_dvec2 r = {0.0, 0.0};
 #pragma unroll
       for (int c = 0; c < HDD_MAX_COMP; ++c) {
         if (c < a.n_comp) {
@@ -336,8 +338,7 @@ __global__ void __launch_bounds__(256) lincomb_kernel(const LincombArgs a)
           r.y += a.theta[s][c] * v[c].y;
         }
       }
-      __builtin_nontemporal_store(r.x, a.out + s * a.stride + 2 * k);
-      __builtin_nontemporal_store(r.y, a.out + s * a.stride + 2 * k + 1);
+      __builtin_nontemporal_store(r, reinterpret_cast<lc_dvec2*>(a.out + s * a.stride) + k);
     }
   }
   if ((a.nnz & 1) && blockIdx.x == 0 && threadIdx.x == 0) {

@@ -71,7 +71,7 @@ def c3(args):
     dofs = 3 * loc.n_own
     nif = int((loc.neighbors[:, :] >= 0).sum()) // 2
     alg = 8 * dp.nnz * 2 + loc.n_own * (84 + 16) + 12 * nif
-    lc_bytes = args.samples * 8 * dp.nnz + 2 * 8 * dp.nnz * math.ceil(args.samples / 16)
+    lc_bytes = args.samples * 8 * dp.nnz + 2 * 8 * dp.nnz * math.ceil(args.samples / 32)   # 32 samples per pass
     return dict(config="c3_os2014_multiquery_kuhn%dx%d" % (n, n), dofs=dofs, nnz_per_component=dp.nnz,
                 components=2, assembly_ms=t_asm * 1e3, assembled_dofs_per_s=dofs / t_asm,
                 assembly_alg_GBps=alg / t_asm / 1e9, samples=args.samples, lincomb_ms=t_lc * 1e3,

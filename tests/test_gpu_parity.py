@@ -354,3 +354,20 @@ def test_scrambled_quad_orientations(ctx, smooth):
     assert np.array_equal(col, ocol)
     worst, ok = compare_rows(rp, val, oval, RTOL)
     assert ok, worst
+
+
+@pytest.mark.parametrize("nnz,n_comp,n_s,stride_pad", [(1001, 3, 40, 6), (75460608 // 64, 2, 33, 0), (7, 1, 1, 2)])
+def test_affine_lincomb(ctx, nnz, n_comp, n_s, stride_pad):
+    """theta-lincomb A(mu_s) = sum_q theta_q(mu_s) A_q (freeze_parameter, base.hh:338-361): several passes of
+    32 samples, odd lengths (scalar tail), a padded output stride -- against numpy."""
+    torch = _torch()
+    rng = np.random.default_rng(nnz)
+    comps = [torch.from_numpy(rng.standard_normal(nnz)).cuda() for _ in range(n_comp)]
+    theta = rng.uniform(-2.0, 2.0, (n_s, n_comp))
+    stride = nnz + (nnz & 1) + stride_pad
+    out = torch.full((n_s, stride), np.nan, dtype=torch.float64, device="cuda")
+    H.affine_lincomb(ctx, comps, theta, out=out)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()[:, :nnz]
+    ref = theta @ np.stack([c.cpu().numpy() for c in comps])
+    assert np.max(np.abs(got - ref)) <= 1e-14 * np.max(np.abs(ref)) * n_comp
