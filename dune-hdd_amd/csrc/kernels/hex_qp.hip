@@ -797,11 +797,20 @@ __global__ void pattern_fill_kernel(const int32_t* __restrict__ nbrs, int32_t nf
       const int64_t t = blk[j]; blk[j] = blk[j - 1]; blk[j - 1] = t;
     }
   const int64_t base = elem_ptr[k];
-  const int64_t rl = int64_t(nb) * nblk;
-  for (int i = lane; i < nb; i += 64) row_ptr[k * nb + i] = base + i * rl;
-  if (k == n_own - 1 && lane == 0) row_ptr[n_own * nb] = base + nb * rl;
-  for (int64_t m = lane; m < nb * rl; m += 64) {
-    const int64_t c = m % rl;
+  const int rl = nb * nblk;   // <= 7 * 64 columns per row
+  for (int i = lane; i < nb; i += 64) row_ptr[k * nb + i] = base + int64_t(i) * rl;
+  if (k == n_own - 1 && lane == 0) row_ptr[n_own * nb] = base + int64_t(nb) * rl;
+  if (nb == 64) {   // Q3: one block row = one wave store, block ids uniform (no division, no indexed array)
+    for (int i = 0; i < 64; ++i) {
+      int32_t* crow = col + base + int64_t(i) * rl;
+#pragma unroll
+      for (int b = 0; b < 7; ++b)
+        if (b < nblk) crow[b * 64 + lane] = int32_t(blk[b] * 64 + lane);
+    }
+    return;
+  }
+  for (int m = lane; m < nb * rl; m += 64) {
+    const int c = m % rl;
     col[base + m] = int32_t(blk[c / nb] * nb + (c % nb));
   }
 }
