@@ -694,7 +694,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
           for (int rr = 0; rr < 4; ++rr) {
             const int row = af == 0 ? I + 4 * g + 16 * rr : (af == 1 ? g + 4 * I + 16 * rr : 16 * I + g + 4 * rr);
-            if (!HDD_HEX_ABL(a, 2)) out[int64_t(row) * rl + cofs + col] = E[I][rr];
+            if (!HDD_HEX_ABL(a, 2)) __builtin_nontemporal_store(E[I][rr], out + int64_t(row) * rl + cofs + col);
           }
       }
     }
@@ -702,7 +702,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     for (int I = 0; I < 4; ++I)
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr)
-        if (!HDD_HEX_ABL(a, 2)) out[(I * 16 + g + 4 * rr) * rl + sofs + col] = S[I][rr];
+        if (!HDD_HEX_ABL(a, 2)) __builtin_nontemporal_store(S[I][rr], out + (I * 16 + g + 4 * rr) * rl + sofs + col);
   }
 }
 
