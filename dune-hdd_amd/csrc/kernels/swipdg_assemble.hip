@@ -1613,7 +1613,7 @@ swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
           dvec2 v;
           v.x = lds[a0];
           v.y = lds[a0 + 1];
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ivec4, v), rsrc, d * 8, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ivec4, v), rsrc, d * 8, 0, 2);
         }
       } else {
 #pragma unroll
@@ -1623,7 +1623,7 @@ swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
           dvec2 v;
           v.x = lds[at(d)];
           v.y = lds[at(d + 1)];
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ivec4, v), rsrc, m2 * 8, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ivec4, v), rsrc, m2 * 8, 0, 2);
         }
       }
     } else {
@@ -1637,7 +1637,7 @@ swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
         const int idx = 2 * (lane + 64 * k);
         const int li = idx < IMG ? idx : 0;
         const dvec2 v = *reinterpret_cast<const dvec2*>(src + li);
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ivec4, v), rsrc, idx * 8, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ivec4, v), rsrc, idx * 8, 0, 2);
       }
     }
     if (!has_next) break;
