@@ -489,7 +489,7 @@ namespace {
 __global__ void __launch_bounds__(256) gather_values_kernel(const double* v, const int64_t* src, int64_t n, double* out)
 {
   for (int64_t k = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; k < n; k += int64_t(gridDim.x) * blockDim.x)
-    out[k] = v[src[k]];
+    __builtin_nontemporal_store(v[src[k]], out + k);
 }
 }  // namespace
 

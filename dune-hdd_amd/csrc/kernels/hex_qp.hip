@@ -889,7 +889,7 @@ __global__ void __launch_bounds__(64) pattern_fill_tile_kernel(const int32_t* __
     for (int64_t q = lane; q < n16; q += 64) {
       const int64_t g0 = al + 4 * q;
       if (g0 >= base && g0 + 4 <= tend) {
-        *reinterpret_cast<i32x4*>(col + g0) = *reinterpret_cast<const i32x4*>(img + 4 * q);
+        __builtin_nontemporal_store(*reinterpret_cast<const i32x4*>(img + 4 * q), reinterpret_cast<i32x4*>(col + g0));
       } else {
 #pragma unroll
         for (int u = 0; u < 4; ++u)

@@ -327,7 +327,7 @@ __global__ __launch_bounds__(256) void rhs2d_kernel(RhsArgs a)
       }
     }
 #pragma unroll
-    for (int i = 0; i < NB; ++i) a.out[k * NB + i] = acc[i];
+    for (int i = 0; i < NB; ++i) __builtin_nontemporal_store(acc[i], a.out + k * NB + i);
   }
 }
 
