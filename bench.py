@@ -213,18 +213,30 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # Kernel time: with a per-step halo, events bracket the assembly launches of every step (on the
+    # assembly stream); otherwise one event pair brackets the K back-to-back launches (per-step event records
+    # add ~9 us of queue work per launch on ROCm: scripts/study/gap.py -> profiles/r01/s2/gap.log), so
+    # kernel_ms is the average launch duration including the dispatch gaps between launches (conservative).
+    per_step = halo is not None
+    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(args.steps if per_step else 1)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(events[k])
+    if per_step:
+        for k in range(args.steps):
+            step(events[k])
+    else:
+        events[0][0].record(stream)
+        for k in range(args.steps):
+            step()
+        events[0][1].record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
+    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in events])) / (1 if per_step else args.steps)
     t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device="cuda" if args.backend == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
