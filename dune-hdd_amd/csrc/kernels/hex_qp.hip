@@ -514,6 +514,7 @@ __global__ __launch_bounds__(256) void hex_q3_setup_kernel(HexArgs a)
 }
 
 typedef const double __attribute__((address_space(4)))* cdptr;   // constant AS: uniform loads -> s_load
+typedef int32_t i32x2 __attribute__((ext_vector_type(2)));
 
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void hex_q3_kernel(HexArgs a)
 {
@@ -556,6 +557,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const int64_t hdr = d2i(R[1]);
     const int64_t rl = int64_t(NB) * int32_t(hdr & 0xffffffff);
     const int64_t sofs = (hdr >> 32) * NB;
+    // the element's row block (<= 7 x 64 x 64 doubles = 229 KB) as one buffer: per-lane part of a store
+    // address in voffset, the wave-uniform row / block part in soffset (no 64-bit VALU address math)
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(out, (short)0, int(rl * NB * 8), 0x00020000);
+    const int rli = int(rl);
     const double M[3][3] = {{R[2], R[3], R[4]}, {R[3], R[5], R[6]}, {R[4], R[6], R[7]}};
 
     dbl4 S[4];
@@ -689,20 +694,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       else face_steps(std::integral_constant<int, 2>{});
       if (inner) {
         const int64_t cofs = (fk >> 32) * NB;
+        const int vo = ((af == 0 ? 4 * g : g) * rli + col) * 8;
 #pragma unroll
         for (int I = 0; I < 4; ++I)
 #pragma unroll
           for (int rr = 0; rr < 4; ++rr) {
-            const int row = af == 0 ? I + 4 * g + 16 * rr : (af == 1 ? g + 4 * I + 16 * rr : 16 * I + g + 4 * rr);
-            if (!HDD_HEX_ABL(a, 2)) __builtin_nontemporal_store(E[I][rr], out + int64_t(row) * rl + cofs + col);
+            const int urow = af == 0 ? I + 16 * rr : (af == 1 ? 4 * I + 16 * rr : 16 * I + 4 * rr);
+            const double v = E[I][rr];   // (bit_cast of a vector element directly reads element 0)
+            if (!HDD_HEX_ABL(a, 2))
+              __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(i32x2, v), rs, vo,
+                                                    (urow * rli + int(cofs)) * 8, 2);
           }
       }
     }
+    const int vs = (g * rli + col) * 8;
 #pragma unroll
     for (int I = 0; I < 4; ++I)
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr)
-        if (!HDD_HEX_ABL(a, 2)) __builtin_nontemporal_store(S[I][rr], out + (I * 16 + g + 4 * rr) * rl + sofs + col);
+      for (int rr = 0; rr < 4; ++rr) {
+        const double v = S[I][rr];
+        if (!HDD_HEX_ABL(a, 2))
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(i32x2, v), rs, vs,
+                                                ((I * 16 + 4 * rr) * rli + int(sofs)) * 8, 2);
+      }
   }
 }
 
