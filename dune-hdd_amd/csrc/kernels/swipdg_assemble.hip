@@ -857,17 +857,30 @@ __device__ __forceinline__ int role_slot(uint32_t finfo, int f, int r)
   else return r == 2 ? E::fv(tw ^ 1, ka) : E::fv(tw ^ 1, 1 - ka);
 }
 
+// One lane's row block in the LDS tile image, written at index i -> (i + rot) mod RB (rot = 0: plain).
+// Uniform Q1 tiles use rot = 2 ((lane >> 1) & 15): see the persistent kernel's image comment.
+template <int RB>
+struct RotImg {
+  double* p;
+  int rot;
+  __device__ __forceinline__ double& operator[](int i) const
+  {
+    const unsigned q = unsigned(i + rot);
+    return p[q < unsigned(RB) ? q : q - unsigned(RB)];
+  }
+};
+
 template <class E, int NQV, int NQF, int TK, int KK>
 struct GenericPolicy {
   static constexpr int NB = E::NB, NF = E::NF, NV = E::NV;
   static constexpr int RB = (NF + 1) * NB * NB;
   // workgroups (single-wave tiles) per CU and the register cap: simplices (18 KB tiles) run 8 per CU at
   // <= 256 registers (2 waves / SIMD hide the sinusoid's VALU latency: C3 0.278 -> 0.241 ms per component,
-  // profiles/r01/s2/ab1.log); quads are LDS-bound at 3 per CU and keep the full register file (capping them
-  // at 256 spills: 0.84 -> 1.30 ms)
-  static constexpr int WGCU = NB == 4 ? 3 : 8;
+  // profiles/r01/s2/ab1.log); quads are LDS-bound at 4 per CU (40 KB rotated image) and keep the full
+  // register file (capping them at 256 spills: 0.84 -> 1.30 ms)
+  static constexpr int WGCU = NB == 4 ? 4 : 8;
   static constexpr int MINW = NB == 4 ? 1 : 2;
-  static constexpr bool PAD = NB == 4;   // padded LDS image for uniform tiles (see the persistent kernel)
+  static constexpr bool PAD = NB == 4;   // rotated LDS image for uniform tiles (see the persistent kernel)
   using Own = GOwn<E>;
   using Gat = GGat<E>;
 
@@ -914,7 +927,8 @@ struct GenericPolicy {
     return c;
   }
 
-  __device__ static void compute(const AssembleArgs& a, int64_t e, const Own& o, const Gat& gt, double* img)
+  template <class IMG>
+  __device__ static void compute(const AssembleArgs& a, int64_t e, const Own& o, const Gat& gt, IMG img)
   {
     Geom G;
     G.init(o.X[0], o.Y[0], o.X[1], o.Y[1], o.X[2], o.Y[2]);
@@ -1022,11 +1036,9 @@ struct GenericPolicy {
 #pragma unroll
         for (int r = 0; r < NB; ++r) slot[r] = role_slot<E>(o.finfo, f, r);
 #pragma unroll
-        for (int i = 0; i < NB; ++i) {
-          double* row = img + i * rowlen + pos[f] * NB;
+        for (int i = 0; i < NB; ++i)
 #pragma unroll
-          for (int r = 0; r < NB; ++r) row[slot[r]] = EN[i][r];
-        }
+          for (int r = 0; r < NB; ++r) img[i * rowlen + pos[f] * NB + slot[r]] = EN[i][r];
       } else {   // Dirichlet: SWIPDG::BoundaryLHS
 #pragma unroll
         for (int q = 0; q < NQF; ++q) {
@@ -1088,7 +1100,8 @@ struct Q1PwcPolicy : GenericPolicy<Cube, 1, 2, TK, KK> {
                   : ((k & 2) ? 1.0 : -1.0) * ((k & 1) ? x : 1.0 - x);
   }
 
-  __device__ static void compute(const AssembleArgs& a, int64_t e, const Own& o, const Gat& gt, double* img)
+  template <class IMG>
+  __device__ static void compute(const AssembleArgs& a, int64_t e, const Own& o, const Gat& gt, IMG img)
   {
     const double j00 = o.X[1] - o.X[0], j01 = o.X[2] - o.X[0], j10 = o.Y[1] - o.Y[0], j11 = o.Y[2] - o.Y[0];
     const double det = j00 * j11 - j01 * j10;
@@ -1185,13 +1198,12 @@ struct Q1PwcPolicy : GenericPolicy<Cube, 1, 2, TK, KK> {
         for (int i = 0; i < NB; ++i) {
           // int phi+_r phi_i: phi+_A = 1 - s, phi+_B = s (roles 0, 1); int phi+_r (A grad phi_i . n) likewise
           const double pi = i == fa ? L3 : (i == fb ? L6 : 0.0), qi = i == fa ? L6 : (i == fb ? L3 : 0.0);
-          double* row = img + i * rowlen + pos[f] * NB;
 #pragma unroll
           for (int r = 0; r < NB; ++r) {
             const double anr = pi * alp[r] + qi * bep[r];
             const double ai = r == 0 ? L3 * al[i] + L6 * be[i] : (r == 1 ? L6 * al[i] + L3 * be[i] : 0.0);
             const double mr = r == 0 ? pi : (r == 1 ? qi : 0.0);
-            row[slot[r]] = cp * anr + cm * ai - pen * mr;
+            img[i * rowlen + pos[f] * NB + slot[r]] = cp * anr + cm * ai - pen * mr;
           }
         }
       } else {   // Dirichlet: SWIPDG::BoundaryLHS
@@ -1522,8 +1534,12 @@ __device__ __forceinline__ int tile_offset(int c, bool active)
 // puts the lanes' row blocks RB doubles apart: for Q1 (RB = 80 = 160 dwords) a ds_write_b64 meets only
 // two bank pairs per 32 lanes, a 16-way conflict (80 such writes per tile).  Policies with P::PAD stage
 // *uniform* tiles (every element with all NF faces interior: tile length = nact * RB, the bulk of a mesh)
-// padded instead: lane i at lds[i * (RB + 1) + j], conflict-free ((RB + 1) odd), and the reader maps the
-// tile's CSR value d to lds[d + d / RB].  Other tiles use the contiguous image.
+// rotated instead: lane i's value j at lds[i RB + (j + 2 ((i >> 1) & 15)) mod RB] -- 2-way conflicts (the
+// floor for a layout that keeps value pairs 16-byte aligned), no padding, so the image is exactly 64 RB
+// doubles (40 KB for Q1: 4 tiles per CU instead of 3), and the reader fetches each 16-byte chunk of the
+// tile's CSR range with one ds_read_b128.  Other tiles use the contiguous image; for P::PAD policies their
+// tail lanes dump into the image's last row block (free: a non-uniform tile with < 64 elements holds at
+// most 63 RB - NB^2 values).
 template <class P, bool TL>   // TL: tiles come from a.tile_list (interior / halo split), else 0..n_tiles-1
 __global__ void __launch_bounds__(64, P::MINW)
 swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
@@ -1531,7 +1547,6 @@ swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
   constexpr int RB = P::RB;
   constexpr int IMG = 64 * RB;
   constexpr int STORES = (IMG / 2 + 63) / 64;
-  static_assert(!P::PAD || 64 * (RB + 1) <= IMG + 2 + RB, "padded image fits the LDS allocation");
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const int lane = threadIdx.x;
   const int64_t G = gridDim.x, b = blockIdx.x;
@@ -1545,7 +1560,7 @@ swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
     t_step = gx;
   }
   if (t >= t_end) return;
-  double* scratch = lds + IMG + 2;
+  double* scratch = P::PAD ? lds + IMG - RB : lds + IMG + 2;
   // optional tile list (interior / halo-boundary split of a sharded assembly): position -> tile
   auto tile_at = [&](int64_t pos) -> int64_t {
     if constexpr (TL) return int64_t(__builtin_amdgcn_readfirstlane(a.tile_list[pos]));
@@ -1585,8 +1600,13 @@ swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
     const int off = tile_offset<P::NB>(P::n_interior(own), active) + int(base - base_al);
     const int tlen = int(tile_end - base);
     const bool uni = P::PAD && tlen == RB * int(a.own_end - t0 < 64 ? a.own_end - t0 : 64);   // wave-uniform
-    double* img = uni ? lds + lane * (RB + 1) : (active ? lds + off : scratch);
-    if (!HDD_ABL(a, 1)) P::compute(a, e, own, gat, img);
+    if constexpr (P::PAD) {
+      const RotImg<RB> img{uni ? lds + lane * RB : (active ? lds + off : scratch), uni ? 2 * ((lane >> 1) & 15) : 0};
+      if (!HDD_ABL(a, 1)) P::compute(a, e, own, gat, img);
+    } else {
+      double* img = active ? lds + off : scratch;
+      if (!HDD_ABL(a, 1)) P::compute(a, e, own, gat, img);
+    }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1599,20 +1619,21 @@ swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
     const int nbytes = stop > start && !HDD_ABL(a, 2) ? int(stop - start) * 8 : 0;
     __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(out + start, (short)0, nbytes, 0x00020000);
     if (P::PAD && uni) {
-      auto at = [](int d) { return d + d / RB; };   // padded slot of the tile's CSR value d
-      const double head = lds[0];
+      auto at = [](int d) {   // rotated slot of the tile's CSR value d
+        const int l = d / RB, j = d - l * RB;
+        const int q = j + 2 * ((l >> 1) & 15);
+        return l * RB + (q < RB ? q : q - RB);
+      };
+      const double head = lds[at(0)];
       const double tail = lds[at(tlen - 1)];
       out[base] = head;
       out[tile_end - 1] = tail;
       const int d0 = int(start - base), dmax = tlen - 2;
-      if (d0 == 0) {   // element blocks start on even d: no 16-byte chunk straddles two elements
+      if (d0 == 0) {   // element blocks start on even d: every 16-byte chunk is one aligned LDS pair
 #pragma unroll
         for (int k = 0; k < STORES; ++k) {
           const int d = 2 * (lane + 64 * k);
-          const int a0 = at(d <= dmax ? d : 0);
-          dvec2 v;
-          v.x = lds[a0];
-          v.y = lds[a0 + 1];
+          const dvec2 v = *reinterpret_cast<const dvec2*>(lds + at(d <= dmax ? d : 0));
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ivec4, v), rsrc, d * 8, 0, 2);
         }
       } else {
@@ -1680,7 +1701,7 @@ static hipError_t launch_persistent(const AssembleArgs& a, hipStream_t s)
   if (n_own <= 0) return hipSuccess;
   const int64_t tiles = a.tile_list ? a.n_tile_list : (n_own + 63) / 64;
   if (tiles <= 0) return hipSuccess;
-  const size_t lds = (size_t(64) * P::RB + 2 + P::RB) * sizeof(double);
+  const size_t lds = (P::PAD ? size_t(64) * P::RB : size_t(64) * P::RB + 2 + P::RB) * sizeof(double);
   int dev = 0, cus = 256;
   (void)hipGetDevice(&dev);
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
