@@ -648,8 +648,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       for (int I = 0; I < 4; ++I) E[I] = dbl4{0.0, 0.0, 0.0, 0.0};
       // one face point row qt per iteration: k-step qt ([V] part) and k-step 4 + qt ([N] part) share every
       // basis evaluation
-      auto face_steps = [&](auto afc) __attribute__((always_inline)) {
-        constexpr int AF = decltype(afc)::value;
+      // face side and inner / boundary are template parameters: no runtime branch around an accumulator
+      // inside the face-point loop (such branches made the compiler route MFMA results through copies)
+      auto face_steps = [&](auto afc, auto sdc, auto inc, auto dsc, auto dec) __attribute__((always_inline)) {
+        constexpr int AF = decltype(afc)::value, SD = decltype(sdc)::value;
+        constexpr bool IN = decltype(inc)::value, DS = decltype(dsc)::value, DE = decltype(dec)::value;
 #pragma unroll 1
         for (int qt = 0; qt < 4; ++qt) {
           const double wq = wfg * T.wf[qt];
@@ -659,7 +662,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
           double Vo, No, Vn = 0.0, Nn = 0.0;
           q3_face_eval<AF>(Le0o, De0o, Le1o, De1o, Lfg0, Dfg0, Lfg1, Dfg1, lf1, df1, lfw, dfw, LeWo, DeWo, cm[0],
                            cm[1], cm[2], Vo, No);
-          if (inner)
+          if constexpr (IN)
             q3_face_eval<AF>(Le0n, De0n, Le1n, De1n, Lfg0, Dfg0, Lfg1, Dfg1, lf1, df1, lfw, dfw, LeWn, DeWn, cp[0],
                              cp[1], cp[2], Vn, Nn);
           const double bEv = et * Vo - al * No, bNv = -be * Nn - et * Vn;   // [V] rows of K
@@ -667,31 +670,57 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
           double Va[4], Na[4];   // rotated rows: tile I = normal index, lane (r & 3, r >> 2) = (qs, qt) axes
 #pragma unroll
           for (int I = 0; I < 4; ++I)
-            q3_face_eval<2>(0.0, 0.0, 0.0, 0.0, Lfg0, Dfg0, Lfg1, Dfg1, lf1, df1, 0.0, 0.0, T.Le[I][sd], T.De[I][sd],
+            q3_face_eval<2>(0.0, 0.0, 0.0, 0.0, Lfg0, Dfg0, Lfg1, Dfg1, lf1, df1, 0.0, 0.0, T.Le[I][SD], T.De[I][SD],
                             cr0, cr1, cr2, Va[I], Na[I]);
-          // [V] rows live on row tile 3 sd (uniform branch: no runtime-indexed accumulator)
-          if (sd) {
-            S[3] = mfma(Va[3], bEv, S[3]);
-            if (inner) E[3] = mfma(Va[3], bNv, E[3]);
-          } else {
-            S[0] = mfma(Va[0], bEv, S[0]);
-            if (inner) E[0] = mfma(Va[0], bNv, E[0]);
-          }
+          // [V] rows live on row tile 3 SD
+          S[3 * SD] = mfma(Va[3 * SD], bEv, S[3 * SD]);
+          if constexpr (IN) E[3 * SD] = mfma(Va[3 * SD], bNv, E[3 * SD]);
           // [N] rows of K: B = -alpha V- / alpha V+ at the columns; on z faces V vanishes off the face plane,
-          // i.e. outside column tile 3 sd (own side) / 3 (1 - sd) (neighbour side): wave-uniform skips
-          if (AF != 2 || wc == 3 * sd) {
+          // i.e. outside column tile 3 SD (own side) / 3 (1 - SD) (neighbour side): DS / DE false
+          if constexpr (DS) {
 #pragma unroll
             for (int I = 0; I < 4; ++I) S[I] = mfma(Na[I], bEn, S[I]);
           }
-          if (inner && (AF != 2 || wc == 3 * (1 - sd))) {
+          if constexpr (IN && DE) {
 #pragma unroll
             for (int I = 0; I < 4; ++I) E[I] = mfma(Na[I], bNn, E[I]);
           }
         }
       };
-      if (af == 0) face_steps(std::integral_constant<int, 0>{});
-      else if (af == 1) face_steps(std::integral_constant<int, 1>{});
-      else face_steps(std::integral_constant<int, 2>{});
+      // face kind -> compile-time loop variant (20 of them): side, inner / boundary, and on z faces
+      // whether this wave's column tile meets the own / neighbour [N] part at all
+      using BT = std::true_type;
+      using BF = std::false_type;
+      auto with_de = [&](auto afc, auto sdc, auto inc, auto dsc) __attribute__((always_inline)) {
+        constexpr int AF = decltype(afc)::value, SD = decltype(sdc)::value;
+        if (AF != 2 || wc == 3 * (1 - SD)) face_steps(afc, sdc, inc, dsc, BT{});
+        else face_steps(afc, sdc, inc, dsc, BF{});
+      };
+      auto with_ds = [&](auto afc, auto sdc, auto inc) __attribute__((always_inline)) {
+        constexpr int AF = decltype(afc)::value, SD = decltype(sdc)::value;
+        constexpr bool IN = decltype(inc)::value;
+        if constexpr (IN) {
+          if (AF != 2 || wc == 3 * SD) with_de(afc, sdc, inc, BT{});
+          else with_de(afc, sdc, inc, BF{});
+        } else {
+          if (AF != 2 || wc == 3 * SD) face_steps(afc, sdc, inc, BT{}, BF{});
+          else face_steps(afc, sdc, inc, BF{}, BF{});
+        }
+      };
+      auto by_kind = [&](auto afc) __attribute__((always_inline)) {
+        using I0 = std::integral_constant<int, 0>;
+        using I1 = std::integral_constant<int, 1>;
+        if (sd) {
+          if (inner) with_ds(afc, I1{}, BT{});
+          else with_ds(afc, I1{}, BF{});
+        } else {
+          if (inner) with_ds(afc, I0{}, BT{});
+          else with_ds(afc, I0{}, BF{});
+        }
+      };
+      if (af == 0) by_kind(std::integral_constant<int, 0>{});
+      else if (af == 1) by_kind(std::integral_constant<int, 1>{});
+      else by_kind(std::integral_constant<int, 2>{});
       if (inner) {
         const int64_t cofs = (fk >> 32) * NB;
         const int vo = ((af == 0 ? 4 * g : g) * rli + col) * 8;
