@@ -653,7 +653,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       auto face_steps = [&](auto afc, auto sdc, auto inc, auto dsc, auto dec) __attribute__((always_inline)) {
         constexpr int AF = decltype(afc)::value, SD = decltype(sdc)::value;
         constexpr bool IN = decltype(inc)::value, DS = decltype(dsc)::value, DE = decltype(dec)::value;
-#pragma unroll 1
+#pragma unroll   // (full unroll: 1.5 % over a rolled loop, profiles/r01/s2/c5/ab_qt_unroll.log)
         for (int qt = 0; qt < 4; ++qt) {
           const double wq = wfg * T.wf[qt];
           const double al = ca * wq, be = cb * wq, et = ce * wq;
