@@ -47,7 +47,7 @@ def parse():
     ap.add_argument("--ny", type=int, default=0, help="c2: 640; c4: 1200")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU work of the baseline sample")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01s2.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01s2d.json"))
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo = rehearsal of the N-rank path on one GPU (host-staged halo)")
     ap.add_argument("--no-overlap", action="store_true",
