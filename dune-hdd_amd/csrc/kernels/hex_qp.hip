@@ -30,6 +30,7 @@
 #include <type_traits>
 
 #include "swipdg_kernels.hh"
+#include "trig_phase.hh"
 
 namespace hdd {
 namespace dev {
@@ -160,7 +161,7 @@ __device__ __forceinline__ void elem_tensor(const HexArgs& a, int64_t e, double 
 __device__ __forceinline__ double kappa_at(const HexArgs& a, int64_t e, const double* x)
 {
   if (a.kkind == HDD_FN_PER_ELEM) return a.kper[e];
-  if (a.kkind == HDD_FN_SINUSOID) return a.kc + a.kb * sin(a.kx * x[0] + a.ky * x[1]);
+  if (a.kkind == HDD_FN_SINUSOID) return a.kc + a.kb * sin_phase(a.kx * x[0] + a.ky * x[1]);
   return a.kc;
 }
 

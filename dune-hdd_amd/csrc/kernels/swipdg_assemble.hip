@@ -29,6 +29,7 @@
 
 #include "hdd.h"
 #include "swipdg_kernels.hh"
+#include "trig_phase.hh"
 
 #ifndef HDD_MIN_WAVES_PER_EU
 #define HDD_MIN_WAVES_PER_EU 4
@@ -149,7 +150,7 @@ __device__ __forceinline__ double kappa_elem(const KappaArg& k, int64_t e)
 }
 __device__ __forceinline__ double kappa_at(const KappaArg& k, double pe, double x, double y)
 {
-  return k.kind == HDD_FN_SINUSOID ? k.c + k.b * sin(k.kx * x + k.ky * y) : pe;
+  return k.kind == HDD_FN_SINUSOID ? k.c + k.b * sin_phase(k.kx * x + k.ky * y) : pe;
 }
 
 typedef double dvec2 __attribute__((ext_vector_type(2)));
@@ -916,7 +917,7 @@ struct GenericPolicy {
   __device__ static double kap(const AssembleArgs& a, double x, double y)
   {
     const KappaArg& K = a.kappa[0];
-    return K.c + K.b * sin(K.kx * x + K.ky * y);
+    return K.c + K.b * sin_phase(K.kx * x + K.ky * y);
   }
 
   __device__ static int n_interior(const Own& o)
@@ -1272,7 +1273,7 @@ struct P1SmoothPolicy {
   {
     using E = Simplex;
     const KappaArg& K = a.kappa[0];
-    auto kap = [&](double x, double y) { return K.c + K.b * sin(K.kx * x + K.ky * y); };
+    auto kap = [&](double x, double y) { return K.c + K.b * sin_phase(K.kx * x + K.ky * y); };
     const double j00 = o.X[1] - o.X[0], j01 = o.X[2] - o.X[0], j10 = o.Y[1] - o.Y[0], j11 = o.Y[2] - o.Y[0];
     const double det = j00 * j11 - j01 * j10;
     const double id = rcp_nr(det);
