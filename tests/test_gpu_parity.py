@@ -371,3 +371,29 @@ def test_affine_lincomb(ctx, nnz, n_comp, n_s, stride_pad):
     got = out.cpu().numpy()[:, :nnz]
     ref = theta @ np.stack([c.cpu().numpy() for c in comps])
     assert np.max(np.abs(got - ref)) <= 1e-14 * np.max(np.abs(ref)) * n_comp
+
+
+@pytest.mark.parametrize("et,smooth", [(H.SIMPLEX, False), (H.SIMPLEX, True), (H.CUBE, False)])
+def test_penalty_exponent_beta(ctx, et, smooth):
+    """beta != 1 (penalty |F|^-beta; 2d default 1/(d-1) = 1 is taken inline, other values through the
+    out-of-line pow of the closed-form kernels) against the oracle with the same beta."""
+    torch = _torch()
+    grid = H.Grid.structured(et, 19, 13, (-1, -1), (1, 0.5))
+    local = grid.local()
+    beta = 0.5
+    prm = H.Params(O.SIGMA_INNER_P1, O.SIGMA_BOUNDARY_P1, beta, -1, -1)
+    if smooth:
+        (c, b, kx, ky) = os2014_components()[0]
+        fns, ofn = [H.scalar_fn(H.FN_SINUSOID, c, b, kx, ky, order=3)], O.scalar(O.FN_SINUSOID, c, b, kx, ky, order=3)
+    else:
+        fns, ofn = [H.scalar_fn(H.FN_CONST, 1.0)], O.scalar(O.FN_CONST, 1.0)
+    kc = 1.0 + np.arange(local.n_local) % 5.0
+    ten = H.tensor_fn(H.TENSOR_ISO_PER_ELEM, per_elem=torch.from_numpy(kc).cuda())
+    _, (rp, col, _), (val,) = _run_product(ctx, grid, fns, ten, prm)
+    og = O.Grid(*_oracle_mesh(et, 19, 13, (-1, -1), (1, 0.5)))
+    orp, ocol, oval = O.assemble(og, ofn, O.tensor(O.TENSOR_ISO_PER_ELEM, per_elem=kc), O.params(beta=beta))
+    assert np.array_equal(col, ocol)
+    worst, ok = compare_rows(rp, val, oval, RTOL)
+    assert ok, worst
+    _, _, (v1,) = _run_product(ctx, grid, fns, ten)   # beta = 1 differs (the exponent is really applied)
+    assert not np.allclose(v1, val)
