@@ -1231,7 +1231,9 @@ template <int TK, int KK, bool PEN = false>
 struct P1PwcPolicy {
   static constexpr int NB = 3, NF = 3;
   static constexpr int RB = 36;
-  static constexpr int WGCU = 4, MINW = 1;   // store-bound: 4 tiles per CU (sweep 1..8)
+  // store-bound: 8 tiles per CU since the out-of-line pow (191 VGPRs, 2 waves per SIMD): C2 0.310 / 0.305
+  // vs 0.312 / 0.314 ms at 4 (profiles/r01/s3/sweep_wgcu_s3.log; 4 was best at 226 VGPRs)
+  static constexpr int WGCU = 8, MINW = 1;
   static constexpr bool PAD = false;          // store-bound: its 4-way write conflicts stay hidden
   using Own = P1Own;
   using Gat = P1Gat;
