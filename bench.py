@@ -47,7 +47,9 @@ def parse():
     ap.add_argument("--ny", type=int, default=0, help="c2: 640; c4: 1200")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU work of the baseline sample")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01s2d.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r02", "traffic.json"),
+                    help="PMC traffic summary (scripts/traffic_summary.py); used only when its build_id matches the "
+                         "timed libhdd_amd.so")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo = rehearsal of the N-rank path on one GPU (host-staged halo)")
     ap.add_argument("--no-overlap", action="store_true",
@@ -114,12 +116,23 @@ def cpu_baseline(nx_full, ny, target_s, cube=False):
                 cpu_model=_cpu_model(), host_cpus=os.cpu_count())
 
 
+def lib_build_id():
+    """sha256 prefix of the timed libhdd_amd.so: PMC traffic files are stamped with it, and a traffic figure
+    measured on another build is not reported."""
+    import hashlib
+    import hdd_amd as H
+    try:
+        return hashlib.sha256(open(H.LIB_PATH, "rb").read()).hexdigest()[:16]
+    except OSError:
+        return None
+
+
 def main():
     args = parse()
     import torch
     import torch.distributed as dist
     import hdd_amd as H
-    from hdd_amd.halo import HaloExchange, strip_owner
+    from hdd_amd.halo import gloo_host_comm, rccl_comm
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -128,12 +141,10 @@ def main():
         raise SystemExit("--gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
     gpu = local_rank if args.backend == "nccl" else 0
     torch.cuda.set_device(gpu)
-    local_rank = gpu
     if world > 1:
-        if args.backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-        else:
-            dist.init_process_group("gloo")
+        # control plane only (barriers, the max-over-ranks timing, the RCCL id broadcast); the halo itself is
+        # moved by the library (hdd_comm: RCCL send/recv, or the host-staged rehearsal transport)
+        dist.init_process_group("gloo")
 
     c4 = args.workload == "c4"
     if c4:   # strong scaling: one 3520 x 1200 Q1 mesh, 8 x 8 subdomains, rank r owns a subdomain-column range
@@ -142,82 +153,59 @@ def main():
         grid = H.Grid.structured(H.CUBE, nx, ny, lower, upper, px=8, py=8)
         if world > grid.n_sub:
             raise SystemExit("c4 shards 64 subdomains: at most 64 ranks")
-        s0, s1 = (rank * grid.n_sub) // world, ((rank + 1) * grid.n_sub) // world
-        local = grid.local(s0, s1)
         ncx = 100
         perm = 10.0 ** np.random.default_rng(10).uniform(-3.0, 3.0, size=2000)
     else:    # weak scaling: rank r owns the r-th (nx x ny) Kuhn strip of a (nx N) x ny grid
         nx, ny = (args.nx or 3200) * world, (args.ny or 640)
         lower, upper = (0.0, 0.0), (5.0 * world, 1.0)
         grid = H.Grid.structured(H.SIMPLEX, nx, ny, lower, upper, px=world, py=1)
-        local = grid.local(rank, rank + 1)
         ncx = 100 * world
         perm = 10.0 ** np.random.default_rng(10).uniform(-3.0, 3.0, size=100 * world * 20)   # == oracle field at N=1
-    kcell = local.checkerboard(lower, upper, ncx, 20, perm)
-    ctx = H.Context(local_rank)
-    dmesh = H.DeviceMesh(local, local_rank, zero_ghosts=world > 1)
+    # the structured grid is implicit (O(subdomains) host memory); the shard holds the rank's owned elements
+    # + face ghosts only (C ABI hdd_shard_create: mesh, halo plan, tile lists on the device)
+    ctx = H.Context(gpu)
+    shard = H.Shard(ctx, grid, world, rank)
+    kcell = shard.checkerboard(lower, upper, ncx, 20, perm)
+    # every rank evaluates its OWNED coefficients only; the ghost columns arrive through the halo
+    kcell[:shard.own_begin] = np.nan
+    kcell[shard.own_end:] = np.nan
     tens = torch.from_numpy(kcell).cuda()
-    if world > 1:
-        tens[:local.own_begin] = 0
-        tens[local.own_end:] = 0
-    dpat = H.DevicePattern(local, local_rank)
+    _, _, _, pat_t = pat = shard.pattern(ctx, gpu)
     kappa = [H.scalar_fn(H.FN_CONST, 1.0)]
     tensor = H.tensor_fn(H.TENSOR_ISO_PER_ELEM, per_elem=tens)
-    vals = [torch.empty(dpat.nnz, dtype=torch.float64, device="cuda")]
-    halo = None
+    nnz = shard.info.nnz
+    vals = [torch.empty(nnz, dtype=torch.float64, device="cuda")]
+    comm = None
     if world > 1:
-        halo = HaloExchange(ctx, local, [(dmesh.coords, dmesh.coords.shape[0]), (tens.view(1, -1), 1)],
-                            strip_owner(grid.n_sub, world), rank, host_staging=args.backend == "gloo")
+        comm = rccl_comm(rank, world, gpu) if args.backend == "nccl" else gloo_host_comm(gpu)
+    flags = H.SHARD_NO_OVERLAP if args.no_overlap else 0
 
-    n_own = local.n_own
+    n_own = shard.n_own
     nbf = 4 if c4 else 3
     dofs_rank = nbf * n_own
-    nbr = local.neighbors[:, local.own_begin:local.own_end]
-    interior = nbr >= 0
-    owned_pair = interior & (nbr >= local.own_begin) & (nbr < local.own_end)
-    nif = int(owned_pair.sum()) // 2 + int((interior & ~owned_pair).sum())
     qp1 = 1
     b_elem = (104 if c4 else 84) + 8 * qp1                                  # quad / triangle record
-    alg_bytes = 8 * dpat.nnz * qp1 + n_own * b_elem + 12 * nif             # SURVEY.md 8(d) formula
+    # interior faces touched by the owned rows: nnz / nb^2 = n_own + 2 (owned-owned faces) + (owned-ghost faces)
+    sides = nnz // (nbf * nbf) - n_own
+    nif = (sides + shard.info.halo_faces) // 2
+    alg_bytes = 8 * nnz * qp1 + n_own * b_elem + 12 * nif                  # SURVEY.md 8(d) formula
 
     stream = torch.cuda.current_stream()
-    if halo is not None and args.halo == "once":
-        halo.exchange()
-        torch.cuda.synchronize()
-        halo = None
-    overlap = halo is not None and not args.no_overlap
-    if overlap:
-        t_in, t_bd = H.halo_tiles(local)
-        tiles_in = torch.from_numpy(t_in).cuda()
-        tiles_bd = torch.from_numpy(t_bd).cuda()
 
-    def step(ev=None):
-        if overlap:
-            # interior tiles (no ghost face neighbour) run while the face halo is in flight
-            halo.start()
-            if ev is not None:
-                ev[0].record(stream)
-            H.assemble_tiles(ctx, dmesh, dpat, kappa, tensor, tiles_in, vals)
-            halo.finish()
-            H.assemble_tiles(ctx, dmesh, dpat, kappa, tensor, tiles_bd, vals)
-            if ev is not None:
-                ev[1].record(stream)
-            return
-        if halo is not None:
-            halo.exchange()
-        if ev is not None:
-            ev[0].record(stream)
-        H.assemble(ctx, dmesh, dpat, kappa, tensor, vals=vals)
-        if ev is not None:
-            ev[1].record(stream)
+    def step(f=flags):
+        H.assemble_sharded(ctx, shard, comm, kappa, tensor, pat_t, vals, flags=f)
 
+    # the first step fills the ghost columns (NaN until then); --halo once keeps them for the timed steps
+    step()
+    if args.halo == "once":
+        flags = H.SHARD_NO_HALO
     for _ in range(args.warmup):
-        step()
-    # Kernel time: with a per-step halo, events bracket the assembly launches of every step (on the
-    # assembly stream); otherwise one event pair brackets the K back-to-back launches (per-step event records
-    # add ~9 us of queue work per launch on ROCm: scripts/study/gap.py -> profiles/r01/s2/gap.log), so
-    # kernel_ms is the average launch duration including the dispatch gaps between launches (conservative).
-    per_step = halo is not None
+        step(flags)
+    # Kernel time: with a per-step halo, events bracket each sharded step (pack, exchange, both tile sets,
+    # unpack) on the assembly stream; otherwise one event pair brackets the K back-to-back launches
+    # (per-step event records add ~9 us of queue work per launch on ROCm: scripts/study/gap.py ->
+    # profiles/r01/s2/gap.log), so kernel_ms is the average launch duration including the dispatch gaps.
+    per_step = world > 1 and args.halo == "step"
     events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
               for _ in range(args.steps if per_step else 1)]
     if world > 1:
@@ -226,32 +214,39 @@ def main():
     t0 = time.perf_counter()
     if per_step:
         for k in range(args.steps):
-            step(events[k])
+            events[k][0].record(stream)
+            step(flags)
+            events[k][1].record(stream)
     else:
         events[0][0].record(stream)
         for k in range(args.steps):
-            step()
+            step(flags)
         events[0][1].record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in events])) / (1 if per_step else args.steps)
-    t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device="cuda" if args.backend == "nccl" else "cpu")
+    t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, kernel_ms_max = float(t[0]), float(t[1])
+    if not np.isfinite(vals[0][:1024].cpu().numpy()).all():
+        raise SystemExit("non-finite values: a ghost column was not filled by the halo")
     total_dofs = nbf * grid.ne if c4 else dofs_rank * world
     value = total_dofs * args.steps / elapsed
 
     if rank == 0:
         achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
-        traffic = None
+        traffic, traffic_src = None, None
+        bid = lib_build_id()
         if os.path.exists(args.traffic_json):
             try:
                 tj = json.load(open(args.traffic_json))
-                if not c4 and world == 1 and tj.get("workload") == "spe10_swipdg_p1_kuhn_%dx%d" % (nx // world, ny):
+                if (not c4 and world == 1 and tj.get("workload") == "spe10_swipdg_p1_kuhn_%dx%d" % (nx // world, ny)
+                        and tj.get("build_id") == bid):
                     traffic = tj.get("hbm_bytes_per_launch")
+                    traffic_src = os.path.relpath(args.traffic_json, ROOT)
             except (OSError, ValueError):
                 traffic = None
         halo_desc = ""
@@ -259,7 +254,7 @@ def main():
             halo_desc = ", face halo exchanged once at setup (static mesh and coefficients)"
         elif world > 1:
             halo_desc = ", %s face halo%s" % ("RCCL" if args.backend == "nccl" else "gloo host-staged (rehearsal)",
-                                              " overlapped with interior tiles" if overlap else "")
+                                              " overlapped with interior tiles" if not args.no_overlap else "")
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(nx // world, ny, args.cpu_seconds, cube=c4)
@@ -278,28 +273,30 @@ def main():
             "data": "synthetic (SPE10 Model1 stand-in permeability: perm_case1.dat absent)",
             "config": ({"workload": "spe10_block_swipdg_q1_%dx%d_8x8_subdomains" % (nx, ny),
                         "elements": grid.ne, "elements_rank0": n_own, "total_dofs": total_dofs,
-                        "nnz_rank0": dpat.nnz, "components": qp1,
+                        "nnz_rank0": nnz, "components": qp1,
                         "parallelism": "subdomain columns x%d, owner-computes%s" % (world, halo_desc)}
                        if c4 else
                        {"workload": "spe10_swipdg_p1_kuhn_%dx%d_per_gpu" % (nx // world, ny),
-                        "elements_per_gpu": n_own, "dofs_per_gpu": dofs_rank, "nnz_per_gpu": dpat.nnz,
+                        "elements_per_gpu": n_own, "dofs_per_gpu": dofs_rank, "nnz_per_gpu": nnz,
                         "total_dofs": total_dofs, "components": qp1,
                         "parallelism": "block-swipdg strips x%d, owner-computes%s" % (world, halo_desc)
                         if world > 1 else "single GPU"}),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
+                         "build_id": bid,
                          "kernel": "swipdg_persistent_kernel<%s<1, 0, false>, %s>"
-                                   % ("Q1PwcPolicy" if c4 else "P1PwcPolicy", "true" if overlap else "false"),
+                                   % ("Q1PwcPolicy" if c4 else "P1PwcPolicy", "true" if per_step else "false"),
                          "kernel_ms_avg": kernel_ms, "kernel_ms_avg_max_rank": kernel_ms_max,
                          "algorithmic_bytes_per_launch": alg_bytes},
             "cpu_baseline": cpu,
         }
-        if halo is not None:
-            out["config"]["halo_bytes_per_step_rank0"] = halo.halo_bytes
+        out["config"]["entry"] = "hdd_block_assemble_sharded (C ABI)"
         if world > 1:
             out["config"]["halo"] = args.halo
+            out["config"]["halo_elements_rank0"] = [int(shard.info.halo_send), int(shard.info.halo_recv)]
         print(json.dumps(out), flush=True)
     if world > 1:
+        del comm
         dist.destroy_process_group()
 
 

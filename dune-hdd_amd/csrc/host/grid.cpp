@@ -379,6 +379,26 @@ extern "C" int hdd_grid_create_from_connectivity(int32_t elem_type, int64_t n_ve
     return set_error(HDD_ERR_INVALID, "hdd_grid_create_from_connectivity: invalid argument");
   if (elem_type != HDD_SIMPLEX && elem_type != HDD_CUBE)
     return set_error(HDD_ERR_UNSUPPORTED, "hdd_grid_create_from_connectivity: unknown element type");
+  // DoF columns (element * nb + i) and neighbour ids are int32 on the device
+  if (n_elements > int64_t(INT32_MAX) / nvpe_of(elem_type))
+    return set_error(HDD_ERR_RANGE, "hdd_grid_create_from_connectivity: too many elements for int32 DoF columns");
+  if (elem_type == HDD_CUBE) {
+    // the Q1 kernels (and the oracle) take the geometry from vertices 0, 1, 2 (affine map): every
+    // quadrilateral must be a parallelogram, x0 + x3 == x1 + x2 (Dune cube vertex order)
+    for (int64_t e = 0; e < n_elements; ++e) {
+      const int32_t* v = elem_vert + 4 * e;
+      for (int k = 0; k < 4; ++k)
+        if (v[k] < 0 || v[k] >= n_vertices) return set_error(HDD_ERR_RANGE, "hdd_grid_create_from_connectivity: bad vertex");
+      for (int c = 0; c < 2; ++c) {
+        const double x0 = vertex_coords[2 * v[0] + c], x1 = vertex_coords[2 * v[1] + c];
+        const double x2 = vertex_coords[2 * v[2] + c], x3 = vertex_coords[2 * v[3] + c];
+        const double scale = std::max(std::max(std::fabs(x1 - x0), std::fabs(x2 - x0)), std::fabs(x3 - x0));
+        if (std::fabs((x0 + x3) - (x1 + x2)) > 1e-10 * std::max(scale, 1e-300))
+          return set_error(HDD_ERR_UNSUPPORTED, "hdd_grid_create_from_connectivity: element " + std::to_string(e) +
+                                                    " is not a parallelogram (bilinear quadrilaterals are not supported)");
+      }
+    }
+  }
   auto G = std::make_unique<ExplicitGrid>();
   G->elem_type = elem_type;
   G->nvpe = nvpe_of(elem_type);
@@ -692,6 +712,25 @@ extern "C" int hdd_checkerboard(int64_t n, const double* centers, const double l
     cx = std::min<int64_t>(std::max<int64_t>(cx, 0), ncx - 1);
     cy = std::min<int64_t>(std::max<int64_t>(cy, 0), ncy - 1);
     out[e] = cell_values[cy * ncx + cx];
+  }
+  return HDD_OK;
+}
+
+extern "C" int hdd_indicator(int64_t n, const double* centers, int32_t n_boxes, const double* boxes, double* out)
+{
+  if (!centers || !out || n_boxes < 0 || (n_boxes && !boxes))
+    return set_error(HDD_ERR_INVALID, "hdd_indicator: invalid argument");
+  for (int64_t e = 0; e < n; ++e) {
+    const double x = centers[e], y = centers[n + e];
+    double v = 0.0;
+    for (int32_t k = 0; k < n_boxes; ++k) {
+      const double* b = boxes + 5 * k;
+      if (b[0] <= x && x <= b[2] && b[1] <= y && y <= b[3]) {
+        v = b[4];
+        break;
+      }
+    }
+    out[e] = v;
   }
   return HDD_OK;
 }

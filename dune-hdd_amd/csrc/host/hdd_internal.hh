@@ -4,7 +4,10 @@
 #pragma once
 #include <string>
 
+#include "hdd.h"
+
 namespace hdd {
 std::string& last_error_slot();
 int set_error(int code, const std::string& msg);
+int ctx_device(const hdd_ctx* ctx);   // HIP device ordinal a context is bound to
 }  // namespace hdd

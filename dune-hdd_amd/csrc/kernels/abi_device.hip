@@ -21,7 +21,13 @@ struct hdd_ctx {
   int device = 0;
   void* ws = nullptr;       // device workspace (per-element coefficient records of the p=3 hex kernel)
   size_t ws_bytes = 0;
+  // read once at hdd_ctx_create, never per launch
+  int n_cu = 256;           // hipDeviceAttributeMultiprocessorCount
+  int debug_flags = 0;      // HDD_DEBUG_FLAGS: profiling ablations only (0 in production)
+  int wgcu = 0;             // HDD_P1_WGCU: tiles-per-CU sweep override (0: the policy's measured value)
 };
+
+int hdd::ctx_device(const hdd_ctx* ctx) { return ctx ? ctx->device : 0; }
 
 // grows the context workspace; allocation happens only on the first call of a size class, so warm the
 // context up once before capturing hdd_swipdg_assemble into a hipGraph
@@ -58,6 +64,11 @@ extern "C" int hdd_ctx_create(int hip_device, hdd_ctx** out)
   if (e != hipSuccess) return hip_fail(e, "hdd_ctx_create: hipSetDevice");
   auto* c = new hdd_ctx;
   c->device = hip_device;
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, hip_device) == hipSuccess && cus > 0)
+    c->n_cu = cus;
+  if (const char* df = getenv("HDD_DEBUG_FLAGS")) c->debug_flags = atoi(df);
+  if (const char* w = getenv("HDD_P1_WGCU")) c->wgcu = std::max(0, atoi(w));
   *out = c;
   return HDD_OK;
 }
@@ -173,10 +184,7 @@ static int assemble_hex(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_fn* ka
     a.sigma_inner = p->sigma_inner;
     a.sigma_boundary = p->sigma_boundary;
     a.beta = p->beta;
-    {
-      const char* df = getenv("HDD_DEBUG_FLAGS");   // profiling ablations (HDD_ABLATION builds only)
-      a.debug_flags = df ? atoi(df) : 0;
-    }
+    a.debug_flags = ctx->debug_flags;   // profiling ablations (HDD_ABLATION builds only)
     gauss_legendre01(nq1v, a.tab.sv, a.tab.wv);
     gauss_legendre01(nq1f, a.tab.sf, a.tab.wf);
     for (int r = 0; r <= deg; ++r) {
@@ -254,10 +262,9 @@ static int assemble_impl(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_fn* k
   a.beta = p->beta;
   a.tile_list = d_tiles;
   a.n_tile_list = n_tiles;
-  {
-    const char* df = getenv("HDD_DEBUG_FLAGS");   // profiling ablations only
-    a.debug_flags = df ? atoi(df) : 0;
-  }
+  a.n_cu = ctx->n_cu;
+  a.debug_flags = ctx->debug_flags;   // profiling ablations only
+  a.wgcu = ctx->wgcu;
   // integrand orders of LocalEvaluation::Elliptic / SWIPDG::Inner / BoundaryLHS at p = 1 (piecewise
   // constant tensors): volume ord(kappa); faces ord(kappa) + 2.  One kernel serves components of equal
   // order -- the caller splits mixed-order component sets.
@@ -563,7 +570,7 @@ extern "C" int hdd_pattern_fill_device(hdd_ctx* ctx, const hdd_mesh* m, int32_t 
   hipError_t e = hipSetDevice(ctx->device);
   if (e != hipSuccess) return hip_fail(e, "hdd_pattern_fill_device: hipSetDevice");
   e = hdd::dev::launch_pattern_fill(m->neighbors, nf, nb, m->n_local, m->own_begin, m->own_end, d_global_id,
-                                    d_elem_ptr, d_row_ptr, d_col, static_cast<hipStream_t>(stream));
+                                    d_elem_ptr, d_row_ptr, d_col, ctx->n_cu, static_cast<hipStream_t>(stream));
   return e == hipSuccess ? HDD_OK : hip_fail(e, "hdd_pattern_fill_device: launch");
 }
 
@@ -686,6 +693,7 @@ extern "C" int hdd_swipdg_rhs(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_
   a.sigma_boundary = p->sigma_boundary;
   a.beta = p->beta;
   a.out = d_rhs;
+  a.n_cu = ctx->n_cu;
   if (force) {
     const int order = fn_order(*force) + deg;
     a.nqv = m->elem_type == HDD_SIMPLEX ? simplex_rule(order, a.qv, 64) : tensor_rule(dim, order, a.qv, 64);
@@ -801,6 +809,9 @@ extern "C" int hdd_product_assemble(hdd_ctx* ctx, const hdd_mesh* m, int32_t pro
     f.beta = p->beta;
     f.kappa[0] = a.kappa;
     f.vals[0] = d_vals;
+    f.n_cu = ctx->n_cu;
+    f.debug_flags = ctx->debug_flags;
+    f.wgcu = ctx->wgcu;
     bool fast = false;
     e = launch_product_fast(f, product, static_cast<hipStream_t>(stream), &fast);
     if (fast) return e == hipSuccess ? HDD_OK : hip_fail(e, "hdd_product_assemble: launch");

@@ -958,14 +958,11 @@ hipError_t launch_pattern_counts(const int32_t* nbrs, int32_t nf, int64_t n_loca
 
 hipError_t launch_pattern_fill(const int32_t* nbrs, int32_t nf, int32_t nb, int64_t n_local, int64_t own_begin,
                                int64_t own_end, const int64_t* gid, const int64_t* elem_ptr, int64_t* row_ptr,
-                               int32_t* col, hipStream_t s)
+                               int32_t* col, int cus, hipStream_t s)
 {
   const int64_t n_own = own_end - own_begin;
   if (n_own <= 0) return hipSuccess;
   if ((nb == 3 && nf == 3) || (nb == 4 && nf == 4)) {
-    int dev = 0, cus = 256;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     const int64_t tiles = (n_own + 63) / 64;
     const unsigned grid = unsigned(std::min<int64_t>(tiles, int64_t(cus) * 8));
     if (nb == 3)

@@ -589,10 +589,7 @@ hipError_t launch_rhs(const RhsArgs& a, hipStream_t s)
 {
   const int64_t n_own = a.own_end - a.own_begin;
   if (a.elem_type != HDD_HEX && n_own > 0) {
-    int dev = 0, cus = 256;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const int64_t blocks = std::min<int64_t>((n_own + 255) / 256, int64_t(cus) * 8);
+    const int64_t blocks = std::min<int64_t>((n_own + 255) / 256, int64_t(a.n_cu) * 8);
     if (a.elem_type == HDD_SIMPLEX)
       hipLaunchKernelGGL(rhs2d_kernel<true>, dim3(unsigned(blocks)), dim3(256), 0, s, a);
     else

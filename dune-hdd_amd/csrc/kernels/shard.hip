@@ -1,0 +1,693 @@
+// dune-hdd_amd/csrc/kernels/shard.hip
+//
+// Sharded BlockSWIPDG behind the C ABI (SURVEY.md 8(b) hdd_block_assemble_sharded, 8(e)).
+//
+// The reference assembles BlockSWIPDG sequentially over subdomains (block-swipdg.hh:271, 334): the local
+// operator of ss, the boundary terms of a domain-boundary subdomain (assemble_boundary_contributions,
+// 1136-1179) and, for each neighbour nn > ss, the SWIPDG::Inner coupling into A_ss, A_ss,nn, A_nn,ss, A_nn
+// (assemble_coupling_contributions, 1270-1326).  Here one rank (process or thread, one GPU each) owns a
+// contiguous subdomain range and writes exactly the rows of its elements -- the rows of A_ss and A_ss,nn
+// (block-swipdg.hh:355-382) -- computing both sides of every face it touches (owner-computes), so no
+// matrix entry is ever summed across ranks.  The only exchange is the face halo: the per-element records
+// (diffusion tensor, per-element diffusion factors [, vertex coordinates]) of the ghost elements.
+//
+// One step: pack (one kernel, every peer) -> post the exchange (RCCL group send/recv on the
+// communicator's transfer stream, or a host transport) -> interior 64-element tiles on the caller's
+// stream while the halo is in flight -> stream waits for the receives -> unpack into the ghost columns
+// -> the tiles that touch a ghost.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <dlfcn.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "hdd.h"
+#include "../host/hdd_internal.hh"
+
+using hdd::set_error;
+
+namespace {
+
+int hip_fail(hipError_t e, const char* where)
+{
+  return set_error(HDD_ERR_HIP, std::string(where) + ": " + hipGetErrorString(e));
+}
+
+// ------------------------------------------------------------------------------------------------
+// RCCL, resolved at run time: in a PyTorch process this is torch's own librccl (already loaded, found
+// through the library's rpath), so the process holds one RCCL and one HIP runtime.
+// ------------------------------------------------------------------------------------------------
+struct RcclApi {
+  bool ok = false;
+  std::string err;
+  ncclResult_t (*GetUniqueId)(ncclUniqueId*) = nullptr;
+  ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+  ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*GroupStart)() = nullptr;
+  ncclResult_t (*GroupEnd)() = nullptr;
+  ncclResult_t (*Send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*Recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+  const char* (*GetErrorString)(ncclResult_t) = nullptr;
+};
+
+RcclApi load_rccl()
+{
+  RcclApi r;
+  void* h = nullptr;
+  for (const char* name : {"librccl.so", "librccl.so.1", "/opt/rocm/lib/librccl.so.1"}) {
+    h = dlopen(name, RTLD_NOW | RTLD_NOLOAD);
+    if (h) break;
+  }
+  if (!h)
+    for (const char* name : {"librccl.so", "librccl.so.1", "/opt/rocm/lib/librccl.so.1"}) {
+      h = dlopen(name, RTLD_NOW | RTLD_GLOBAL);
+      if (h) break;
+    }
+  if (!h) {
+    const char* e = dlerror();
+    r.err = std::string("librccl not found: ") + (e ? e : "");
+    return r;
+  }
+  bool all = true;
+  auto sym = [&](auto& fp, const char* name) {
+    fp = reinterpret_cast<std::remove_reference_t<decltype(fp)>>(dlsym(h, name));
+    if (!fp) {
+      all = false;
+      r.err += std::string(" missing ") + name;
+    }
+  };
+  sym(r.GetUniqueId, "ncclGetUniqueId");
+  sym(r.CommInitRank, "ncclCommInitRank");
+  sym(r.CommDestroy, "ncclCommDestroy");
+  sym(r.GroupStart, "ncclGroupStart");
+  sym(r.GroupEnd, "ncclGroupEnd");
+  sym(r.Send, "ncclSend");
+  sym(r.Recv, "ncclRecv");
+  sym(r.GetErrorString, "ncclGetErrorString");
+  r.ok = all;
+  return r;
+}
+
+const RcclApi& rccl()
+{
+  static RcclApi api;
+  static std::once_flag once;
+  std::call_once(once, [] { api = load_rccl(); });
+  return api;
+}
+
+int nccl_fail(ncclResult_t r, const char* where)
+{
+  const char* s = rccl().GetErrorString ? rccl().GetErrorString(r) : "?";
+  return set_error(HDD_ERR_HIP, std::string(where) + ": RCCL error " + std::to_string(int(r)) + " (" + s + ")");
+}
+
+// ------------------------------------------------------------------------------------------------
+// halo pack / unpack: message of peer p = [rows][count_p] doubles at buf + R * prefix[p]
+// ------------------------------------------------------------------------------------------------
+constexpr int SH_MAX_ARR = 16;
+constexpr int SH_MAX_PEERS = 64;
+
+struct HaloArgs {
+  double* arr[SH_MAX_ARR];             // element-column arrays [rows][ld]
+  int32_t row_first[SH_MAX_ARR + 1];   // first halo row of each array
+  int32_t n_arrays, n_peers;
+  int64_t ld;
+  int64_t prefix[SH_MAX_PEERS + 1];    // element prefix over the peers' messages
+  int64_t col0[SH_MAX_PEERS];          // unpack: first ghost column of peer p
+  const int32_t* idx;                  // pack: concatenated send lists (local element ids)
+  double* buf;
+};
+
+__device__ __forceinline__ void halo_slot(const HaloArgs& a, int64_t t, int& p, int& arr, int64_t& rr, int64_t& i)
+{
+  const int R = a.row_first[a.n_arrays];
+  p = 0;
+  while (p + 1 < a.n_peers && int64_t(R) * a.prefix[p + 1] <= t) ++p;
+  const int64_t cnt = a.prefix[p + 1] - a.prefix[p];
+  const int64_t loc = t - int64_t(R) * a.prefix[p];
+  const int64_t r = loc / cnt;
+  i = loc - r * cnt;
+  arr = 0;
+  while (arr + 1 < a.n_arrays && a.row_first[arr + 1] <= r) ++arr;
+  rr = r - a.row_first[arr];
+}
+
+__global__ void __launch_bounds__(256) halo_pack_kernel(const HaloArgs a)
+{
+  const int64_t total = int64_t(a.row_first[a.n_arrays]) * a.prefix[a.n_peers];
+  for (int64_t t = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; t < total; t += int64_t(gridDim.x) * blockDim.x) {
+    int p, arr;
+    int64_t rr, i;
+    halo_slot(a, t, p, arr, rr, i);
+    a.buf[t] = a.arr[arr][rr * a.ld + a.idx[a.prefix[p] + i]];
+  }
+}
+
+__global__ void __launch_bounds__(256) halo_unpack_kernel(const HaloArgs a)
+{
+  const int64_t total = int64_t(a.row_first[a.n_arrays]) * a.prefix[a.n_peers];
+  for (int64_t t = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; t < total; t += int64_t(gridDim.x) * blockDim.x) {
+    int p, arr;
+    int64_t rr, i;
+    halo_slot(a, t, p, arr, rr, i);
+    a.arr[arr][rr * a.ld + a.col0[p] + i] = a.buf[t];
+  }
+}
+
+template <class T>
+hipError_t upload(T** d, const std::vector<T>& h)
+{
+  *d = nullptr;
+  if (h.empty()) return hipSuccess;
+  hipError_t e = hipMalloc(d, h.size() * sizeof(T));
+  if (e != hipSuccess) return e;
+  return hipMemcpy(*d, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice);
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------------
+// communicators
+// ------------------------------------------------------------------------------------------------
+struct hdd_comm {
+  enum Kind { RCCL_OWNED, RCCL_WRAPPED, HOST } kind = HOST;
+  int device = 0;
+  ncclComm_t nccl = nullptr;
+  hipStream_t xfer = nullptr;          // RCCL transfer stream
+  hipEvent_t ready = nullptr, done = nullptr;
+  bool posted = false;
+  hdd_host_exchange_fn fn = nullptr;
+  void* user = nullptr;
+  double* pinned = nullptr;            // host staging (HOST)
+  size_t pinned_doubles = 0;
+};
+
+static int comm_rccl_streams(hdd_comm* c)
+{
+  hipError_t e = hipSetDevice(c->device);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->xfer, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ready, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->done, hipEventDisableTiming);
+  return e == hipSuccess ? HDD_OK : hip_fail(e, "hdd_comm: transfer stream / events");
+}
+
+extern "C" int hdd_rccl_get_unique_id(void* id)
+{
+  if (!id) return set_error(HDD_ERR_INVALID, "hdd_rccl_get_unique_id: null id");
+  static_assert(sizeof(ncclUniqueId) == HDD_RCCL_ID_BYTES, "ncclUniqueId size");
+  const RcclApi& R = rccl();
+  if (!R.ok) return set_error(HDD_ERR_UNSUPPORTED, "hdd_rccl_get_unique_id: " + R.err);
+  ncclUniqueId u;
+  const ncclResult_t r = R.GetUniqueId(&u);
+  if (r != ncclSuccess) return nccl_fail(r, "ncclGetUniqueId");
+  std::memcpy(id, &u, sizeof(u));
+  return HDD_OK;
+}
+
+extern "C" int hdd_comm_create_rccl(const void* id, int32_t nranks, int32_t rank, int32_t hip_device, hdd_comm** out)
+{
+  if (!id || !out || nranks < 1 || rank < 0 || rank >= nranks)
+    return set_error(HDD_ERR_INVALID, "hdd_comm_create_rccl: invalid argument");
+  const RcclApi& R = rccl();
+  if (!R.ok) return set_error(HDD_ERR_UNSUPPORTED, "hdd_comm_create_rccl: " + R.err);
+  auto* c = new hdd_comm;
+  c->kind = hdd_comm::RCCL_OWNED;
+  c->device = hip_device;
+  int rc = comm_rccl_streams(c);
+  if (rc) {
+    hdd_comm_destroy(c);
+    return rc;
+  }
+  ncclUniqueId u;
+  std::memcpy(&u, id, sizeof(u));
+  const ncclResult_t r = R.CommInitRank(&c->nccl, nranks, u, rank);
+  if (r != ncclSuccess) {
+    c->nccl = nullptr;
+    hdd_comm_destroy(c);
+    return nccl_fail(r, "ncclCommInitRank");
+  }
+  *out = c;
+  return HDD_OK;
+}
+
+extern "C" int hdd_comm_wrap_rccl(void* nccl_comm, int32_t hip_device, hdd_comm** out)
+{
+  if (!nccl_comm || !out) return set_error(HDD_ERR_INVALID, "hdd_comm_wrap_rccl: invalid argument");
+  const RcclApi& R = rccl();
+  if (!R.ok) return set_error(HDD_ERR_UNSUPPORTED, "hdd_comm_wrap_rccl: " + R.err);
+  auto* c = new hdd_comm;
+  c->kind = hdd_comm::RCCL_WRAPPED;
+  c->device = hip_device;
+  c->nccl = static_cast<ncclComm_t>(nccl_comm);
+  int rc = comm_rccl_streams(c);
+  if (rc) {
+    hdd_comm_destroy(c);
+    return rc;
+  }
+  *out = c;
+  return HDD_OK;
+}
+
+extern "C" int hdd_comm_create_host(hdd_host_exchange_fn fn, void* user, int32_t hip_device, hdd_comm** out)
+{
+  if (!fn || !out) return set_error(HDD_ERR_INVALID, "hdd_comm_create_host: invalid argument");
+  auto* c = new hdd_comm;
+  c->kind = hdd_comm::HOST;
+  c->device = hip_device;
+  c->fn = fn;
+  c->user = user;
+  *out = c;
+  return HDD_OK;
+}
+
+extern "C" void hdd_comm_destroy(hdd_comm* c)
+{
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->xfer) (void)hipStreamSynchronize(c->xfer);
+  if (c->kind == hdd_comm::RCCL_OWNED && c->nccl && rccl().ok) (void)rccl().CommDestroy(c->nccl);
+  if (c->ready) (void)hipEventDestroy(c->ready);
+  if (c->done) (void)hipEventDestroy(c->done);
+  if (c->xfer) (void)hipStreamDestroy(c->xfer);
+  if (c->pinned) (void)hipHostFree(c->pinned);
+  delete c;
+}
+
+extern "C" int hdd_comm_post(hdd_comm* c, int32_t n_peers, const int32_t* peers, const double* const* d_send,
+                             const int64_t* send_count, double* const* d_recv, const int64_t* recv_count, void* stream)
+{
+  if (!c || n_peers < 0 || (n_peers && (!peers || !d_send || !send_count || !d_recv || !recv_count)))
+    return set_error(HDD_ERR_INVALID, "hdd_comm_post: invalid argument");
+  const hipStream_t s = static_cast<hipStream_t>(stream);
+  hipError_t e = hipSetDevice(c->device);
+  if (e != hipSuccess) return hip_fail(e, "hdd_comm_post: hipSetDevice");
+  if (c->kind != hdd_comm::HOST) {
+    // the transfer stream starts after the packs already enqueued on `stream`
+    e = hipEventRecord(c->ready, s);
+    if (e == hipSuccess) e = hipStreamWaitEvent(c->xfer, c->ready, 0);
+    if (e != hipSuccess) return hip_fail(e, "hdd_comm_post: order transfer after pack");
+    const RcclApi& R = rccl();
+    ncclResult_t r = R.GroupStart();
+    if (r != ncclSuccess) return nccl_fail(r, "ncclGroupStart");
+    for (int32_t k = 0; k < n_peers; ++k) {
+      if (send_count[k] > 0) {
+        r = R.Send(d_send[k], size_t(send_count[k]), ncclFloat64, peers[k], c->nccl, c->xfer);
+        if (r != ncclSuccess) break;
+      }
+      if (recv_count[k] > 0) {
+        r = R.Recv(d_recv[k], size_t(recv_count[k]), ncclFloat64, peers[k], c->nccl, c->xfer);
+        if (r != ncclSuccess) break;
+      }
+    }
+    const ncclResult_t r2 = R.GroupEnd();
+    if (r != ncclSuccess) return nccl_fail(r, "ncclSend/ncclRecv");
+    if (r2 != ncclSuccess) return nccl_fail(r2, "ncclGroupEnd");
+    e = hipEventRecord(c->done, c->xfer);
+    if (e != hipSuccess) return hip_fail(e, "hdd_comm_post: record completion");
+    c->posted = true;
+    return HDD_OK;
+  }
+  // host-staged: device -> pinned host -> fn -> device, all ordered on `stream`
+  size_t total = 0;
+  for (int32_t k = 0; k < n_peers; ++k) {
+    if (send_count[k] < 0 || recv_count[k] < 0) return set_error(HDD_ERR_INVALID, "hdd_comm_post: negative count");
+    total += size_t(send_count[k]) + size_t(recv_count[k]);
+  }
+  if (total > c->pinned_doubles) {
+    if (c->pinned) (void)hipHostFree(c->pinned);
+    c->pinned = nullptr;
+    c->pinned_doubles = 0;
+    e = hipHostMalloc(reinterpret_cast<void**>(&c->pinned), std::max<size_t>(total, 1) * sizeof(double), 0);
+    if (e != hipSuccess) return hip_fail(e, "hdd_comm_post: pinned staging");
+    c->pinned_doubles = total;
+  }
+  std::vector<const double*> hs(n_peers);
+  std::vector<double*> hr(n_peers);
+  size_t off = 0;
+  for (int32_t k = 0; k < n_peers; ++k) {
+    hs[k] = c->pinned + off;
+    off += size_t(send_count[k]);
+    hr[k] = c->pinned + off;
+    off += size_t(recv_count[k]);
+    if (send_count[k]) {
+      e = hipMemcpyAsync(const_cast<double*>(hs[k]), d_send[k], size_t(send_count[k]) * sizeof(double),
+                         hipMemcpyDeviceToHost, s);
+      if (e != hipSuccess) return hip_fail(e, "hdd_comm_post: D2H");
+    }
+  }
+  e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return hip_fail(e, "hdd_comm_post: synchronize");
+  const int rc = c->fn(c->user, n_peers, peers, hs.data(), send_count, hr.data(), recv_count);
+  if (rc != HDD_OK) return set_error(rc, "hdd_comm_post: host transport failed (status " + std::to_string(rc) + ")");
+  for (int32_t k = 0; k < n_peers; ++k)
+    if (recv_count[k]) {
+      e = hipMemcpyAsync(d_recv[k], hr[k], size_t(recv_count[k]) * sizeof(double), hipMemcpyHostToDevice, s);
+      if (e != hipSuccess) return hip_fail(e, "hdd_comm_post: H2D");
+    }
+  // the staging buffer is reused by the next post: the copies must have left it
+  e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return hip_fail(e, "hdd_comm_post: synchronize");
+  c->posted = true;
+  return HDD_OK;
+}
+
+extern "C" int hdd_comm_wait(hdd_comm* c, void* stream)
+{
+  if (!c) return set_error(HDD_ERR_INVALID, "hdd_comm_wait: null comm");
+  if (!c->posted) return HDD_OK;
+  c->posted = false;
+  if (c->kind == hdd_comm::HOST) return HDD_OK;   // already ordered on the stream by hdd_comm_post
+  hipError_t e = hipSetDevice(c->device);
+  if (e == hipSuccess) e = hipStreamWaitEvent(static_cast<hipStream_t>(stream), c->done, 0);
+  return e == hipSuccess ? HDD_OK : hip_fail(e, "hdd_comm_wait");
+}
+
+// ------------------------------------------------------------------------------------------------
+// shards
+// ------------------------------------------------------------------------------------------------
+struct hdd_shard {
+  int device = 0;
+  hdd_local* local = nullptr;
+  hdd_grid_info gi{};
+  hdd_local_info li{};
+  int32_t rank = 0, nranks = 1, s_begin = 0, s_end = 0, degree = 1;
+  int64_t nnz = 0;
+  std::vector<int64_t> gid;            // host global ids [n_local]
+  // device mesh (shard-owned)
+  double* d_coords = nullptr;
+  int32_t* d_nbrs = nullptr;
+  uint32_t* d_finfo = nullptr;
+  int64_t* d_gid = nullptr;
+  // halo
+  std::vector<int32_t> peers;
+  std::vector<int64_t> send_prefix, recv_prefix, recv_col0;
+  int32_t* d_send_idx = nullptr;
+  double* d_sbuf = nullptr;
+  double* d_rbuf = nullptr;
+  int32_t max_rows = 0;
+  // tiles
+  int32_t* d_tiles_in = nullptr;
+  int32_t* d_tiles_bd = nullptr;
+  int64_t n_tiles = 0, n_in = 0, n_bd = 0;
+  int64_t halo_faces = 0;
+};
+
+extern "C" void hdd_shard_destroy(hdd_shard* sh)
+{
+  if (!sh) return;
+  (void)hipSetDevice(sh->device);
+  for (void* p : {static_cast<void*>(sh->d_coords), static_cast<void*>(sh->d_nbrs), static_cast<void*>(sh->d_finfo),
+                  static_cast<void*>(sh->d_gid), static_cast<void*>(sh->d_send_idx), static_cast<void*>(sh->d_sbuf),
+                  static_cast<void*>(sh->d_rbuf), static_cast<void*>(sh->d_tiles_in),
+                  static_cast<void*>(sh->d_tiles_bd)})
+    if (p) (void)hipFree(p);
+  if (sh->local) hdd_local_destroy(sh->local);
+  delete sh;
+}
+
+extern "C" int hdd_shard_create(hdd_ctx* ctx, const hdd_grid* g, int32_t nranks, int32_t rank, const int32_t* owner,
+                                hdd_shard** out)
+{
+  if (!ctx || !g || !out || nranks < 1 || rank < 0 || rank >= nranks)
+    return set_error(HDD_ERR_INVALID, "hdd_shard_create: invalid argument");
+  hdd_grid_info gi{};
+  int rc = hdd_grid_get_info(g, &gi);
+  if (rc) return rc;
+  std::vector<int32_t> own(size_t(gi.n_subdomains));
+  if (owner) {
+    std::copy(owner, owner + gi.n_subdomains, own.begin());
+  } else {
+    if (nranks > gi.n_subdomains)
+      return set_error(HDD_ERR_INVALID, "hdd_shard_create: more ranks than subdomains");
+    for (int32_t r = 0; r < nranks; ++r)
+      for (int64_t s = int64_t(r) * gi.n_subdomains / nranks; s < int64_t(r + 1) * gi.n_subdomains / nranks; ++s)
+        own[size_t(s)] = r;
+  }
+  int32_t s0 = -1, s1 = -1;
+  for (int32_t s = 0; s < gi.n_subdomains; ++s) {
+    if (own[s] < 0 || own[s] >= nranks) return set_error(HDD_ERR_RANGE, "hdd_shard_create: owner out of range");
+    if (own[s] != rank) continue;
+    if (s0 < 0) s0 = s;
+    else if (s1 != s) return set_error(HDD_ERR_UNSUPPORTED, "hdd_shard_create: owned subdomains must be contiguous");
+    s1 = s + 1;
+  }
+  if (s0 < 0) return set_error(HDD_ERR_INVALID, "hdd_shard_create: rank owns no subdomain");
+
+  auto* sh = new hdd_shard;
+  auto fail = [&](int code) {
+    hdd_shard_destroy(sh);
+    return code;
+  };
+  sh->device = hdd::ctx_device(ctx);
+  sh->gi = gi;
+  sh->rank = rank;
+  sh->nranks = nranks;
+  sh->s_begin = s0;
+  sh->s_end = s1;
+  if (gi.elem_type == HDD_HEX)
+    while ((sh->degree + 1) * (sh->degree + 1) * (sh->degree + 1) < gi.nb) ++sh->degree;
+  rc = hdd_local_create(g, s0, s1, &sh->local);
+  if (rc) return fail(rc);
+  rc = hdd_local_get_info(sh->local, &sh->li);
+  if (rc) return fail(rc);
+  const int64_t nl = sh->li.n_local, ob = sh->li.own_begin, oe = sh->li.own_end;
+  std::vector<double> coords(size_t(gi.dim) * gi.nvpe * nl);
+  std::vector<int32_t> nbrs(size_t(gi.nfaces) * nl);
+  std::vector<uint32_t> finfo(static_cast<size_t>(nl));
+  sh->gid.resize(size_t(nl));
+  rc = hdd_local_fill(sh->local, coords.data(), nbrs.data(), finfo.data(), sh->gid.data(), nullptr);
+  if (rc) return fail(rc);
+  rc = hdd_dg_pattern_count(gi.nfaces, gi.nb, nl, ob, oe, nbrs.data(), &sh->nnz);
+  if (rc) return fail(rc);
+
+  // halo plan: peers ascending, send lists concatenated in peer order
+  int32_t np = 0;
+  rc = hdd_local_halo_plan(sh->local, own.data(), rank, &np, nullptr, nullptr, nullptr, nullptr);
+  if (rc) return fail(rc);
+  if (np > SH_MAX_PEERS) return fail(set_error(HDD_ERR_UNSUPPORTED, "hdd_shard_create: more than 64 halo peers"));
+  sh->peers.resize(size_t(np));
+  std::vector<int64_t> sc(static_cast<size_t>(np)), ro(static_cast<size_t>(np)), rcnt(static_cast<size_t>(np));
+  rc = hdd_local_halo_plan(sh->local, own.data(), rank, &np, sh->peers.data(), sc.data(), ro.data(), rcnt.data());
+  if (rc) return fail(rc);
+  sh->send_prefix.assign(size_t(np) + 1, 0);
+  sh->recv_prefix.assign(size_t(np) + 1, 0);
+  sh->recv_col0 = ro;
+  for (int32_t k = 0; k < np; ++k) {
+    sh->send_prefix[k + 1] = sh->send_prefix[k] + sc[k];
+    sh->recv_prefix[k + 1] = sh->recv_prefix[k] + rcnt[k];
+  }
+  std::vector<int32_t> send_idx(size_t(sh->send_prefix[np]));
+  for (int32_t k = 0; k < np; ++k) {
+    if (!sc[k]) continue;
+    rc = hdd_local_send_list(sh->local, own.data(), rank, k, send_idx.data() + sh->send_prefix[k]);
+    if (rc) return fail(rc);
+  }
+
+  // interior / halo-boundary tiles (64 owned elements; a boundary tile has an element with a ghost face)
+  const int64_t n_own = oe - ob;
+  sh->n_tiles = (n_own + 63) / 64;
+  std::vector<int32_t> tin, tbd;
+  for (int64_t t = 0; t < sh->n_tiles; ++t) {
+    bool ghost = false;
+    for (int64_t e = ob + 64 * t; e < std::min(oe, ob + 64 * t + 64); ++e)
+      for (int f = 0; f < gi.nfaces; ++f) {
+        const int32_t n = nbrs[size_t(f) * nl + e];
+        if (n >= 0 && (n < ob || n >= oe)) {
+          ghost = true;
+          ++sh->halo_faces;
+        }
+      }
+    (ghost ? tbd : tin).push_back(int32_t(t));
+  }
+  sh->n_in = int64_t(tin.size());
+  sh->n_bd = int64_t(tbd.size());
+
+  hipError_t e = hipSetDevice(sh->device);
+  if (e == hipSuccess) e = upload(&sh->d_coords, coords);
+  if (e == hipSuccess) e = upload(&sh->d_nbrs, nbrs);
+  if (e == hipSuccess) e = upload(&sh->d_finfo, finfo);
+  if (e == hipSuccess) e = upload(&sh->d_gid, sh->gid);
+  if (e == hipSuccess) e = upload(&sh->d_send_idx, send_idx);
+  if (e == hipSuccess) e = upload(&sh->d_tiles_in, tin);
+  if (e == hipSuccess) e = upload(&sh->d_tiles_bd, tbd);
+  // message rows: coordinates + symmetric tensor + one row per diffusion-factor component
+  sh->max_rows = gi.dim * gi.nvpe + (gi.dim == 3 ? 6 : 3) + HDD_MAX_COMP;
+  if (e == hipSuccess && sh->send_prefix[np])
+    e = hipMalloc(&sh->d_sbuf, size_t(sh->max_rows) * sh->send_prefix[np] * sizeof(double));
+  if (e == hipSuccess && sh->recv_prefix[np])
+    e = hipMalloc(&sh->d_rbuf, size_t(sh->max_rows) * sh->recv_prefix[np] * sizeof(double));
+  if (e != hipSuccess) return fail(hip_fail(e, "hdd_shard_create: upload"));
+  *out = sh;
+  return HDD_OK;
+}
+
+extern "C" int hdd_shard_get_info(const hdd_shard* sh, hdd_shard_info* o)
+{
+  if (!sh || !o) return set_error(HDD_ERR_INVALID, "hdd_shard_get_info: null argument");
+  o->n_local = sh->li.n_local;
+  o->own_begin = sh->li.own_begin;
+  o->own_end = sh->li.own_end;
+  o->n_ghost = sh->li.n_ghost;
+  o->global_first = sh->li.global_first;
+  o->n_rows = int64_t(sh->gi.nb) * (sh->li.own_end - sh->li.own_begin);
+  o->n_cols = int64_t(sh->gi.nb) * sh->gi.n_elements;
+  o->nnz = sh->nnz;
+  o->rank = sh->rank;
+  o->nranks = sh->nranks;
+  o->s_begin = sh->s_begin;
+  o->s_end = sh->s_end;
+  o->n_peers = int32_t(sh->peers.size());
+  o->nb = sh->gi.nb;
+  o->n_tiles = sh->n_tiles;
+  o->n_tiles_interior = sh->n_in;
+  o->n_tiles_boundary = sh->n_bd;
+  o->halo_send = sh->send_prefix.back();
+  o->halo_recv = sh->recv_prefix.back();
+  o->halo_faces = sh->halo_faces;
+  return HDD_OK;
+}
+
+extern "C" int hdd_shard_mesh(const hdd_shard* sh, hdd_mesh* m)
+{
+  if (!sh || !m) return set_error(HDD_ERR_INVALID, "hdd_shard_mesh: null argument");
+  *m = hdd_mesh{sh->gi.elem_type, sh->gi.elem_type == HDD_HEX ? sh->degree : 1, sh->li.n_local, sh->li.own_begin,
+                sh->li.own_end, sh->d_coords, sh->d_nbrs, sh->d_finfo};
+  return HDD_OK;
+}
+
+extern "C" int hdd_shard_global_ids(const hdd_shard* sh, int64_t* global_id)
+{
+  if (!sh || !global_id) return set_error(HDD_ERR_INVALID, "hdd_shard_global_ids: null argument");
+  std::copy(sh->gid.begin(), sh->gid.end(), global_id);
+  return HDD_OK;
+}
+
+extern "C" int hdd_shard_centers(const hdd_shard* sh, double* centers)
+{
+  if (!sh || !centers) return set_error(HDD_ERR_INVALID, "hdd_shard_centers: null argument");
+  return hdd_local_centers(sh->local, centers);
+}
+
+extern "C" int hdd_shard_pattern_fill(hdd_ctx* ctx, const hdd_shard* sh, int64_t* d_row_ptr, int32_t* d_col,
+                                      int64_t* d_elem_ptr, void* stream)
+{
+  if (!ctx || !sh || !d_row_ptr || !d_col || !d_elem_ptr)
+    return set_error(HDD_ERR_INVALID, "hdd_shard_pattern_fill: null argument");
+  hdd_mesh m;
+  hdd_shard_mesh(sh, &m);
+  int64_t nnz = 0;
+  int rc = hdd_pattern_elem_ptr_device(ctx, &m, sh->gi.nb, d_elem_ptr, &nnz, stream);
+  if (rc) return rc;
+  if (nnz != sh->nnz) return set_error(HDD_ERR_INVALID, "hdd_shard_pattern_fill: nnz mismatch (internal)");
+  rc = hdd_pattern_fill_device(ctx, &m, sh->gi.nb, sh->d_gid, d_elem_ptr, d_row_ptr, d_col, stream);
+  if (rc) return rc;
+  const hipError_t e = hipStreamSynchronize(static_cast<hipStream_t>(stream));
+  return e == hipSuccess ? HDD_OK : hip_fail(e, "hdd_shard_pattern_fill: synchronize");
+}
+
+static hipError_t launch_halo(bool pack, const HaloArgs& a, hipStream_t s)
+{
+  const int64_t total = int64_t(a.row_first[a.n_arrays]) * a.prefix[a.n_peers];
+  if (total == 0) return hipSuccess;
+  const unsigned grid = unsigned(std::min<int64_t>((total + 255) / 256, 1024));
+  if (pack) hipLaunchKernelGGL(halo_pack_kernel, dim3(grid), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(halo_unpack_kernel, dim3(grid), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+extern "C" int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm* comm, const hdd_scalar_fn* kappa,
+                                          int32_t n_comp, const hdd_tensor_fn* tensor,
+                                          const hdd_swipdg_params* params, const hdd_csr* pattern,
+                                          double* const* d_vals, uint32_t flags, void* stream)
+{
+  if (!ctx || !sh || !kappa || !tensor || !params || !pattern || !d_vals)
+    return set_error(HDD_ERR_INVALID, "hdd_block_assemble_sharded: null argument");
+  if (n_comp < 1 || n_comp > HDD_MAX_COMP)
+    return set_error(HDD_ERR_INVALID, "hdd_block_assemble_sharded: need 1 <= n_comp <= HDD_MAX_COMP");
+  if (pattern->nnz != sh->nnz || pattern->n_rows != int64_t(sh->gi.nb) * (sh->li.own_end - sh->li.own_begin))
+    return set_error(HDD_ERR_INVALID, "hdd_block_assemble_sharded: pattern does not belong to this shard");
+  hdd_mesh m;
+  hdd_shard_mesh(sh, &m);
+  const hipStream_t s = static_cast<hipStream_t>(stream);
+
+  // halo rows: [coordinates] [tensor] [per-element diffusion factors (each distinct array once)]
+  HaloArgs h{};
+  h.ld = sh->li.n_local;
+  h.n_peers = int32_t(sh->peers.size());
+  // (no de-duplication of arrays passed twice: the message layout must depend on the kinds only, which
+  // every rank passes alike, never on pointer identity)
+  auto add = [&](double* p, int rows) {
+    h.arr[h.n_arrays] = p;
+    h.row_first[h.n_arrays + 1] = h.row_first[h.n_arrays] + rows;
+    ++h.n_arrays;
+  };
+  if (flags & HDD_SHARD_HALO_GEOMETRY) add(sh->d_coords, sh->gi.dim * sh->gi.nvpe);
+  if (tensor->kind == HDD_TENSOR_ISO_PER_ELEM || tensor->kind == HDD_TENSOR_SYM_PER_ELEM) {
+    if (!tensor->per_elem) return set_error(HDD_ERR_INVALID, "hdd_block_assemble_sharded: tensor per_elem missing");
+    add(const_cast<double*>(tensor->per_elem),
+        tensor->kind == HDD_TENSOR_ISO_PER_ELEM ? 1 : (sh->gi.dim == 3 ? 6 : 3));
+  }
+  for (int32_t c = 0; c < n_comp; ++c)
+    if (kappa[c].kind == HDD_FN_PER_ELEM) {
+      if (!kappa[c].per_elem) return set_error(HDD_ERR_INVALID, "hdd_block_assemble_sharded: kappa per_elem missing");
+      add(const_cast<double*>(kappa[c].per_elem), 1);
+    }
+  const bool exchange = h.n_peers > 0 && !(flags & HDD_SHARD_NO_HALO) && h.n_arrays > 0;
+  if (!exchange) return hdd_swipdg_assemble(ctx, &m, kappa, n_comp, tensor, params, pattern, d_vals, stream);
+  if (!comm) return set_error(HDD_ERR_INVALID, "hdd_block_assemble_sharded: the shard has halo peers but comm is NULL");
+  const int32_t R = h.row_first[h.n_arrays];
+  if (R > sh->max_rows) return set_error(HDD_ERR_INVALID, "hdd_block_assemble_sharded: too many halo rows");
+
+  hipError_t e = hipSetDevice(sh->device);
+  if (e != hipSuccess) return hip_fail(e, "hdd_block_assemble_sharded: hipSetDevice");
+  // 1. pack the records the peers need (one launch for every peer)
+  for (int k = 0; k <= h.n_peers; ++k) h.prefix[k] = sh->send_prefix[k];
+  h.idx = sh->d_send_idx;
+  h.buf = sh->d_sbuf;
+  e = launch_halo(true, h, s);
+  if (e != hipSuccess) return hip_fail(e, "hdd_block_assemble_sharded: pack");
+  // 2. post the exchange
+  std::vector<const double*> sp(size_t(h.n_peers));
+  std::vector<double*> rp(size_t(h.n_peers));
+  std::vector<int64_t> sn(size_t(h.n_peers)), rn(size_t(h.n_peers));
+  for (int k = 0; k < h.n_peers; ++k) {
+    sp[k] = sh->d_sbuf + int64_t(R) * sh->send_prefix[k];
+    sn[k] = int64_t(R) * (sh->send_prefix[k + 1] - sh->send_prefix[k]);
+    rp[k] = sh->d_rbuf + int64_t(R) * sh->recv_prefix[k];
+    rn[k] = int64_t(R) * (sh->recv_prefix[k + 1] - sh->recv_prefix[k]);
+  }
+  int rc = hdd_comm_post(comm, h.n_peers, sh->peers.data(), sp.data(), sn.data(), rp.data(), rn.data(), stream);
+  if (rc) return rc;
+  // 3. interior tiles overlap the transfer (the kernels that take tile lists: P1 / Q1 persistent policies)
+  bool overlap = !(flags & HDD_SHARD_NO_OVERLAP) && sh->n_in > 0 && sh->gi.elem_type != HDD_HEX;
+  if (overlap) {
+    rc = hdd_swipdg_assemble_tiles(ctx, &m, kappa, n_comp, tensor, params, pattern, d_vals, sh->d_tiles_in, sh->n_in,
+                                   stream);
+    if (rc == HDD_ERR_UNSUPPORTED) overlap = false;   // no tile-list kernel: assemble everything after the halo
+    else if (rc) {
+      (void)hdd_comm_wait(comm, stream);
+      return rc;
+    }
+  }
+  // 4. ghost columns after the receives
+  rc = hdd_comm_wait(comm, stream);
+  if (rc) return rc;
+  for (int k = 0; k <= h.n_peers; ++k) h.prefix[k] = sh->recv_prefix[k];
+  for (int k = 0; k < h.n_peers; ++k) h.col0[k] = sh->recv_col0[k];
+  h.idx = nullptr;
+  h.buf = sh->d_rbuf;
+  e = launch_halo(false, h, s);
+  if (e != hipSuccess) return hip_fail(e, "hdd_block_assemble_sharded: unpack");
+  // 5. the tiles that read a ghost (or everything without overlap)
+  if (overlap)
+    return hdd_swipdg_assemble_tiles(ctx, &m, kappa, n_comp, tensor, params, pattern, d_vals, sh->d_tiles_bd, sh->n_bd,
+                                     stream);
+  return hdd_swipdg_assemble(ctx, &m, kappa, n_comp, tensor, params, pattern, d_vals, stream);
+}

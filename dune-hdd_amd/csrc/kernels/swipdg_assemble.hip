@@ -1709,11 +1709,10 @@ static hipError_t launch_persistent(const AssembleArgs& a, hipStream_t s)
   const int64_t tiles = a.tile_list ? a.n_tile_list : (n_own + 63) / 64;
   if (tiles <= 0) return hipSuccess;
   const size_t lds = (P::PAD ? size_t(64) * P::RB : size_t(64) * P::RB + 2 + P::RB) * sizeof(double);
-  int dev = 0, cus = 256;
-  (void)hipGetDevice(&dev);
-  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  int wgcu = P::WGCU;   // measured per policy (profiles/r01/sweep_wg_per_cu.log, profiles/r01/s2/)
-  if (const char* w = getenv("HDD_P1_WGCU")) wgcu = atoi(w);   // profiling sweeps only
+  const int cus = a.n_cu;
+  // tiles per CU measured per policy (profiles/r01/sweep_wg_per_cu.log, profiles/r01/s2/); a.wgcu > 0 is the
+  // HDD_P1_WGCU sweep override, read once per context
+  int wgcu = a.wgcu > 0 ? a.wgcu : P::WGCU;
   wgcu = std::max(1, std::min<int>(wgcu, int((160 * 1024) / lds)));   // resident by LDS (Q1 tiles: 3 per CU)
   const int64_t G = std::min<int64_t>(tiles, int64_t(cus) * wgcu);
   for (int c = 0; c < a.n_comp; ++c) {

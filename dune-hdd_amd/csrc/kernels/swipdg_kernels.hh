@@ -22,11 +22,11 @@ struct AssembleArgs {
   const int32_t* nbrs;
   const uint32_t* finfo;
   const int64_t* elem_ptr;
-  int32_t tkind, pad;
+  int32_t tkind, n_cu;         // n_cu: compute units of the device (cached in hdd_ctx)
   double tc0, tc1, tc2;
   const double* tper;
   double sigma_inner, sigma_boundary, beta;
-  int32_t debug_flags, pad2;   // ablation switches (HDD_DEBUG_FLAGS), 0 in production
+  int32_t debug_flags, wgcu;   // ablation switches (HDD_DEBUG_FLAGS, 0 in production); wgcu: tiles per CU override (0: policy default)
   const int32_t* tile_list;    // optional: 64-element tiles to assemble (relative to own_begin)
   int64_t n_tile_list;         // entries of tile_list (tile_list == nullptr: all tiles)
   KappaArg kappa[HDD_MAX_COMP];
@@ -73,7 +73,7 @@ hipError_t launch_pattern_counts(const int32_t* nbrs, int32_t nf, int64_t n_loca
                                  int64_t nb2, int64_t* d_counts, hipStream_t s);
 hipError_t launch_pattern_fill(const int32_t* nbrs, int32_t nf, int32_t nb, int64_t n_local, int64_t own_begin,
                                int64_t own_end, const int64_t* gid, const int64_t* elem_ptr, int64_t* row_ptr,
-                               int32_t* col, hipStream_t s);
+                               int32_t* col, int n_cu, hipStream_t s);
 
 // right-hand side functionals (rhs.hip)
 struct RhsArgs {
@@ -86,7 +86,7 @@ struct RhsArgs {
   KappaArg force, kappa, dirichlet, neumann;
   int32_t has_force, has_dirichlet, has_neumann, pad;
   double sigma_boundary, beta;
-  int32_t nqv, nqd, nqn, pad2;
+  int32_t nqv, nqd, nqn, n_cu;
   double qv[64][4];    // volume rule: reference point (3) + weight
   double qd[16][3];    // Dirichlet face rule: face parameters (2) + weight
   double qn[16][3];    // Neumann face rule

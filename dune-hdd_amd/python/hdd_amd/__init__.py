@@ -91,6 +91,23 @@ class CsrT(C.Structure):
                 ("col", C.c_void_p), ("elem_ptr", C.c_void_p)]
 
 
+class ShardInfo(C.Structure):
+    _fields_ = [("n_local", C.c_int64), ("own_begin", C.c_int64), ("own_end", C.c_int64), ("n_ghost", C.c_int64),
+                ("global_first", C.c_int64), ("n_rows", C.c_int64), ("n_cols", C.c_int64), ("nnz", C.c_int64),
+                ("rank", C.c_int32), ("nranks", C.c_int32), ("s_begin", C.c_int32), ("s_end", C.c_int32),
+                ("n_peers", C.c_int32), ("nb", C.c_int32), ("n_tiles", C.c_int64), ("n_tiles_interior", C.c_int64),
+                ("n_tiles_boundary", C.c_int64), ("halo_send", C.c_int64), ("halo_recv", C.c_int64),
+                ("halo_faces", C.c_int64)]
+
+
+# int (*)(void* user, int32 n_peers, const int32* peers, const double* const* send, const int64* send_count,
+#         double* const* recv, const int64* recv_count)
+HOST_EXCHANGE_FN = C.CFUNCTYPE(C.c_int32, C.c_void_p, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_void_p),
+                               C.POINTER(C.c_int64), C.POINTER(C.c_void_p), C.POINTER(C.c_int64))
+RCCL_ID_BYTES = 128
+SHARD_NO_OVERLAP, SHARD_HALO_GEOMETRY, SHARD_NO_HALO = 1, 2, 4
+
+
 _LIB = None
 _VP, _I32, _I64, _D = C.c_void_p, C.c_int32, C.c_int64, C.c_double
 
@@ -128,6 +145,7 @@ def lib():
         "hdd_local_halo_plan": (_I32, [_VP, _VP, _I32, C.POINTER(_I32), _VP, _VP, _VP, _VP]),
         "hdd_local_send_list": (_I32, [_VP, _VP, _I32, _I32, _VP]),
         "hdd_checkerboard": (_I32, [_I64, _VP, _VP, _VP, _I32, _I32, _VP, _VP]),
+        "hdd_indicator": (_I32, [_I64, _VP, _I32, _VP, _VP]),
         "hdd_pattern_count": (_I32, [_I32, _I64, _I64, _I64, _VP, C.POINTER(_I64)]),
         "hdd_pattern_fill": (_I32, [_I32, _I64, _I64, _I64, _VP, _VP, _VP, _VP, _VP]),
         "hdd_dg_pattern_count": (_I32, [_I32, _I32, _I64, _I64, _I64, _VP, C.POINTER(_I64)]),
@@ -146,6 +164,22 @@ def lib():
         "hdd_gather_values": (_I32, [_VP, _VP, _VP, _I64, _VP, _VP]),
         "hdd_soa_gather": (_I32, [_VP, _VP, _VP, _I32, _I64, _VP, _I64, _VP, _VP]),
         "hdd_soa_scatter": (_I32, [_VP, _VP, _VP, _I32, _I64, _I64, _I64, _VP, _VP]),
+        "hdd_rccl_get_unique_id": (_I32, [_VP]),
+        "hdd_comm_create_rccl": (_I32, [_VP, _I32, _I32, _I32, _VP]),
+        "hdd_comm_wrap_rccl": (_I32, [_VP, _I32, _VP]),
+        "hdd_comm_create_host": (_I32, [HOST_EXCHANGE_FN, _VP, _I32, _VP]),
+        "hdd_comm_destroy": (None, [_VP]),
+        "hdd_comm_post": (_I32, [_VP, _I32, _VP, _VP, _VP, _VP, _VP, _VP]),
+        "hdd_comm_wait": (_I32, [_VP, _VP]),
+        "hdd_shard_create": (_I32, [_VP, _VP, _I32, _I32, _VP, _VP]),
+        "hdd_shard_destroy": (None, [_VP]),
+        "hdd_shard_get_info": (_I32, [_VP, C.POINTER(ShardInfo)]),
+        "hdd_shard_mesh": (_I32, [_VP, C.POINTER(MeshT)]),
+        "hdd_shard_global_ids": (_I32, [_VP, _VP]),
+        "hdd_shard_centers": (_I32, [_VP, _VP]),
+        "hdd_shard_pattern_fill": (_I32, [_VP, _VP, _VP, _VP, _VP, _VP]),
+        "hdd_block_assemble_sharded": (_I32, [_VP, _VP, _VP, C.POINTER(ScalarFn), _I32, C.POINTER(TensorFn),
+                                              C.POINTER(Params), C.POINTER(CsrT), _VP, C.c_uint32, _VP]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -170,6 +204,15 @@ def declared_symbols(header=HEADER):
     import re
     txt = open(header).read()
     return sorted(set(re.findall(r"\b(hdd_[a-z0-9_]+)\s*\(", txt)))
+
+
+def indicator(centers, boxes):
+    """dune-stuff Indicator at points centers [2][n] (hdd_indicator): boxes [k][5] = lx, ly, ux, uy, value."""
+    c = np.ascontiguousarray(centers, np.float64)
+    b = np.ascontiguousarray(boxes, np.float64).reshape(-1, 5)
+    out = np.empty(c.shape[1])
+    _check(lib().hdd_indicator(c.shape[1], _p(c), b.shape[0], _p(b), _p(out)), "hdd_indicator")
+    return out
 
 
 # ----------------------------------------------------------------------------------------------------
@@ -454,7 +497,7 @@ def assemble(ctx, dmesh, dpattern, kappas, tensor, prm=None, vals=None, stream=N
         vals = [torch.empty(dpattern.nnz, dtype=torch.float64, device=dmesh.coords.device) for _ in range(n)]
     arr = (ScalarFn * n)(*kappas)
     ptrs = (C.c_void_p * n)(*[v.data_ptr() for v in vals])
-    prm = prm or params()
+    prm = prm or params_for(dmesh.local.degree, dmesh.local.dim)
     s = stream if stream is not None else torch.cuda.current_stream(dmesh.coords.device).cuda_stream
     _check(lib().hdd_swipdg_assemble(ctx.h, C.byref(dmesh.t), arr, n, C.byref(tensor), C.byref(prm),
                                      C.byref(dpattern.t), ptrs, C.c_void_p(s)), "hdd_swipdg_assemble")
@@ -468,7 +511,7 @@ def assemble_tiles(ctx, dmesh, dpattern, kappas, tensor, tiles, vals, prm=None, 
     n = len(kappas)
     arr = (ScalarFn * n)(*kappas)
     ptrs = (C.c_void_p * n)(*[v.data_ptr() for v in vals])
-    prm = prm or params()
+    prm = prm or params_for(dmesh.local.degree, dmesh.local.dim)
     s = stream if stream is not None else torch.cuda.current_stream(dmesh.coords.device).cuda_stream
     _check(lib().hdd_swipdg_assemble_tiles(ctx.h, C.byref(dmesh.t), arr, n, C.byref(tensor), C.byref(prm),
                                            C.byref(dpattern.t), ptrs, tiles.data_ptr(), tiles.numel(),
@@ -532,13 +575,15 @@ def affine_lincomb(ctx, comps, theta, out=None, stream=None):
     theta = np.ascontiguousarray(theta, np.float64)
     ns, nc = theta.shape
     nnz = comps[0].numel()
-    if out is None:
-        out = torch.empty((ns, nnz), dtype=torch.float64, device=comps[0].device)
+    ret = None
+    if out is None:   # the kernel writes 16-byte pairs: pad the row stride to even, hand back the nnz view
+        ret = out = torch.empty((ns, nnz + (nnz & 1)), dtype=torch.float64, device=comps[0].device)
+        ret = out[:, :nnz]
     ptrs = (C.c_void_p * nc)(*[c.data_ptr() for c in comps])
     s = stream if stream is not None else torch.cuda.current_stream(comps[0].device).cuda_stream
     _check(lib().hdd_affine_lincomb(ctx.h, nnz, ptrs, nc, _p(theta), ns, out.data_ptr(), out.stride(0),
                                     C.c_void_p(s)), "hdd_affine_lincomb")
-    return out
+    return out if ret is None else ret
 
 
 def soa_gather(ctx, arrays, rows, ld, idx, buf, stream=None):
@@ -559,3 +604,151 @@ def soa_scatter(ctx, arrays, rows, ld, offset, n_items, buf, stream=None):
     s = stream if stream is not None else torch.cuda.current_stream(buf.device).cuda_stream
     _check(lib().hdd_soa_scatter(ctx.h, ptrs, r, n, ld, offset, n_items, buf.data_ptr(), C.c_void_p(s)),
            "hdd_soa_scatter")
+
+
+# ----------------------------------------------------------------------------------------------------
+# sharded BlockSWIPDG (hdd_shard_* / hdd_comm_* / hdd_block_assemble_sharded)
+# ----------------------------------------------------------------------------------------------------
+class Comm:
+    """Face-halo transport (hdd_comm): RCCL (one GPU per rank) or a host-staged callback."""
+
+    def __init__(self, handle, keep=None):
+        self.h = handle
+        self._keep = keep
+
+    @staticmethod
+    def rccl_unique_id():
+        buf = (C.c_char * RCCL_ID_BYTES)()
+        _check(lib().hdd_rccl_get_unique_id(buf), "hdd_rccl_get_unique_id")
+        return bytes(buf)
+
+    @classmethod
+    def rccl(cls, unique_id, nranks, rank, device):
+        if len(unique_id) != RCCL_ID_BYTES:
+            raise HddError("RCCL unique id must be %d bytes" % RCCL_ID_BYTES)
+        buf = (C.c_char * RCCL_ID_BYTES).from_buffer_copy(unique_id)
+        h = C.c_void_p()
+        _check(lib().hdd_comm_create_rccl(buf, nranks, rank, device, C.byref(h)), "hdd_comm_create_rccl")
+        return cls(h)
+
+    @classmethod
+    def host(cls, exchange, device=0):
+        """exchange(peers, sends, recvs): sends / recvs are lists of numpy float64 views of the host staging
+        buffers (fill the recv views in place); returns nothing (raise on failure)."""
+        def cb(user, n_peers, peers, send, send_count, recv, recv_count):
+            try:
+                pe = [int(peers[k]) for k in range(n_peers)]
+                sv = [np.ctypeslib.as_array(C.cast(send[k], C.POINTER(C.c_double)), (int(send_count[k]),))
+                      if send_count[k] else np.empty(0) for k in range(n_peers)]
+                rv = [np.ctypeslib.as_array(C.cast(recv[k], C.POINTER(C.c_double)), (int(recv_count[k]),))
+                      if recv_count[k] else np.empty(0) for k in range(n_peers)]
+                exchange(pe, sv, rv)
+                return 0
+            except Exception:   # never unwind through the C ABI
+                import traceback
+                traceback.print_exc()
+                return 1
+        fn = HOST_EXCHANGE_FN(cb)
+        h = C.c_void_p()
+        _check(lib().hdd_comm_create_host(fn, None, device, C.byref(h)), "hdd_comm_create_host")
+        return cls(h, keep=fn)
+
+    def post(self, peers, sends, recvs, stream=None):
+        """hdd_comm_post of device tensors (float64), then the caller calls wait()."""
+        torch = _torch()
+        n = len(peers)
+        pe = (C.c_int32 * n)(*peers)
+        sp = (C.c_void_p * n)(*[t.data_ptr() for t in sends])
+        rp = (C.c_void_p * n)(*[t.data_ptr() for t in recvs])
+        sc = (C.c_int64 * n)(*[t.numel() for t in sends])
+        rc = (C.c_int64 * n)(*[t.numel() for t in recvs])
+        s = stream if stream is not None else torch.cuda.current_stream().cuda_stream
+        _check(lib().hdd_comm_post(self.h, n, pe, sp, sc, rp, rc, C.c_void_p(s)), "hdd_comm_post")
+
+    def wait(self, stream=None):
+        torch = _torch()
+        s = stream if stream is not None else torch.cuda.current_stream().cuda_stream
+        _check(lib().hdd_comm_wait(self.h, C.c_void_p(s)), "hdd_comm_wait")
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            try:
+                lib().hdd_comm_destroy(self.h)
+            except Exception:   # interpreter shutdown
+                pass
+            self.h = None
+
+
+class Shard:
+    """Rank-local shard of a (block) grid (hdd_shard): owned subdomains + face ghosts, device mesh, halo
+    plan and tile lists.  owner: subdomain -> rank (None: contiguous near-equal ranges)."""
+
+    def __init__(self, ctx, grid, nranks, rank, owner=None):
+        own = None if owner is None else np.ascontiguousarray(owner, np.int32)
+        h = C.c_void_p()
+        _check(lib().hdd_shard_create(ctx.h, grid.h, nranks, rank, _p(own), C.byref(h)), "hdd_shard_create")
+        self.h = h
+        self.grid = grid                      # the shard references the grid: keep it alive
+        self.info = ShardInfo()
+        _check(lib().hdd_shard_get_info(self.h, C.byref(self.info)), "hdd_shard_get_info")
+        self.mesh = MeshT()
+        _check(lib().hdd_shard_mesh(self.h, C.byref(self.mesh)), "hdd_shard_mesh")
+        i = self.info
+        self.n_local, self.own_begin, self.own_end = i.n_local, i.own_begin, i.own_end
+        self.n_own = i.own_end - i.own_begin
+        self.nb, self.dim = i.nb, grid.dim
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            try:
+                lib().hdd_shard_destroy(self.h)
+            except Exception:   # interpreter shutdown
+                pass
+            self.h = None
+
+    def global_ids(self):
+        g = np.empty(self.n_local, np.int64)
+        _check(lib().hdd_shard_global_ids(self.h, _p(g)), "hdd_shard_global_ids")
+        return g
+
+    def centers(self):
+        c = np.empty((self.dim, self.n_local))
+        _check(lib().hdd_shard_centers(self.h, _p(c)), "hdd_shard_centers")
+        return c
+
+    def checkerboard(self, lower, upper, ncx, ncy, values):
+        c = self.centers()
+        vals = np.ascontiguousarray(values, np.float64)
+        out = np.empty(self.n_local)
+        _check(lib().hdd_checkerboard(self.n_local, _p(c), (C.c_double * 2)(*lower), (C.c_double * 2)(*upper),
+                                      ncx, ncy, _p(vals), _p(out)), "hdd_checkerboard")
+        return out
+
+    def pattern(self, ctx, device=0):
+        """Device pattern of the owned rows (caller-owned torch buffers) -> (row_ptr, col, elem_ptr, CsrT)."""
+        torch = _torch()
+        dev = torch.device("cuda", device)
+        rp = torch.empty(self.info.n_rows + 1, dtype=torch.int64, device=dev)
+        col = torch.empty(self.info.nnz, dtype=torch.int32, device=dev)
+        ep = torch.empty(self.n_own + 1, dtype=torch.int64, device=dev)
+        s = torch.cuda.current_stream(dev).cuda_stream
+        _check(lib().hdd_shard_pattern_fill(ctx.h, self.h, rp.data_ptr(), col.data_ptr(), ep.data_ptr(),
+                                            C.c_void_p(s)), "hdd_shard_pattern_fill")
+        t = CsrT(self.info.n_rows, self.info.n_cols, self.info.nnz, rp.data_ptr(), col.data_ptr(), ep.data_ptr())
+        t._keep = (rp, col, ep)        # the descriptor holds raw device pointers: keep the buffers alive
+        return rp, col, ep, t
+
+
+def assemble_sharded(ctx, shard, comm, kappas, tensor, pattern_t, vals, prm=None, flags=0, stream=None):
+    """hdd_block_assemble_sharded: one sharded assembly step (halo exchange + owned rows)."""
+    torch = _torch()
+    kappas = list(kappas)
+    n = len(kappas)
+    arr = (ScalarFn * n)(*kappas)
+    ptrs = (C.c_void_p * n)(*[v.data_ptr() for v in vals])
+    prm = prm or params_for(1 if shard.grid.elem_type != HEX else shard.grid.degree, shard.grid.dim)
+    s = stream if stream is not None else torch.cuda.current_stream().cuda_stream
+    _check(lib().hdd_block_assemble_sharded(ctx.h, shard.h, None if comm is None else comm.h, arr, n, C.byref(tensor),
+                                            C.byref(prm), C.byref(pattern_t), ptrs, flags, C.c_void_p(s)),
+           "hdd_block_assemble_sharded")
+    return vals

@@ -9,7 +9,36 @@ needed (rows are owned), so there is no all-reduce on the data path.
 """
 import numpy as np
 
-from . import soa_gather, soa_scatter
+from . import Comm, soa_gather, soa_scatter
+
+
+def gloo_host_comm(device=0, group=None):
+    """hdd_comm host transport over torch.distributed point-to-point (gloo: host tensors).  The C++ step
+    (hdd_block_assemble_sharded) stages the halo through pinned host memory and calls this synchronously --
+    the rehearsal transport for several ranks on one GPU, where RCCL refuses duplicate devices."""
+    import torch
+    import torch.distributed as dist
+
+    def exchange(peers, sends, recvs):
+        ops = []
+        for p, sv, rv in zip(peers, sends, recvs):
+            if sv.size:
+                ops.append(dist.P2POp(dist.isend, torch.from_numpy(sv), p, group=group))
+            if rv.size:
+                ops.append(dist.P2POp(dist.irecv, torch.from_numpy(rv), p, group=group))
+        for r in (dist.batch_isend_irecv(ops) if ops else []):
+            r.wait()
+
+    return Comm.host(exchange, device)
+
+
+def rccl_comm(rank, world, device, group=None):
+    """hdd_comm over RCCL (one GPU per rank): rank 0's ncclUniqueId is broadcast over the (gloo) control
+    group, then every rank runs ncclCommInitRank inside the library."""
+    import torch.distributed as dist
+    obj = [Comm.rccl_unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0, group=group)
+    return Comm.rccl(obj[0], world, rank, device)
 
 
 class HaloExchange:

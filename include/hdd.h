@@ -13,7 +13,9 @@
  *     hdd_soa_gather / hdd_soa_scatter, and no allocation either except that hdd_swipdg_assemble on
  *     HDD_HEX p=3 meshes grows a context-owned workspace (576 B per owned element) the first time a
  *     context sees a larger mesh: warm a context up once, then the calls are hipGraph-capturable;
- *   - one context per thread at a time (thread-compatible, like the reference's single-threaded init()).
+ *   - one context per thread at a time (thread-compatible, like the reference's single-threaded init()),
+ *     and one stream at a time per context: the HDD_HEX p=3 coefficient records live in a per-context
+ *     workspace, so concurrent assemblies on different streams need different contexts.
  *
  * Numbering: DoF (row / column) of local basis function i of element g is g*nb + i (element-blocked,
  * as dune-fem's DG mapper); a CSR row holds the DoFs of its element and of every face neighbour, sorted
@@ -145,6 +147,10 @@ int hdd_local_send_list(const hdd_local* l, const int32_t* owner, int32_t my_ran
 /* dune-stuff Checkerboard evaluated at element barycentres: value of cell (cx, cy), x fastest */
 int hdd_checkerboard(int64_t n, const double* centers /*[2][n]*/, const double lower[2], const double upper[2],
                      int32_t ncx, int32_t ncy, const double* cell_values, double* out);
+/* dune-stuff Indicator evaluated at element barycentres (problems/spe10.hh:144, 157: the SPE10 channel and
+ * force): value of the first closed box [lx, ux] x [ly, uy] containing the barycentre, 0 if none;
+ * boxes[5k .. 5k+4] = lx, ly, ux, uy, value */
+int hdd_indicator(int64_t n, const double* centers /*[2][n]*/, int32_t n_boxes, const double* boxes, double* out);
 
 /* ---------------------------------------------------------------------------------------------- */
 /* sparsity pattern (host) -- replaces EllipticSWIPDG::pattern(test, ansatz) (swipdg.hh:169) and the */
@@ -291,6 +297,83 @@ int hdd_block_operator_map(const hdd_grid* g, int32_t ss, int32_t nn, const int6
                            int64_t* out_row_ptr, int32_t* out_col, int64_t* out_src, int64_t* nnz);
 /* d_out[k] = d_vals[d_src[k]] for k < n (device arrays) */
 int hdd_gather_values(hdd_ctx* ctx, const double* d_vals, const int64_t* d_src, int64_t n, double* d_out, void* stream);
+
+/* ---------------------------------------------------------------------------------------------- */
+/* sharded BlockSWIPDG (SURVEY.md 8(b) hdd_block_assemble_sharded, 8(e)): one process (or thread) per  */
+/* GPU owns a contiguous range of subdomains and assembles their rows -- A_ss and A_ss,nn are written  */
+/* by the owner of ss (block-swipdg.hh:355-382, coupling 1270-1326, boundary 1136-1179), so there is  */
+/* no reduction; the only exchange is the face halo (per-element records of the ghost elements).      */
+/* ---------------------------------------------------------------------------------------------- */
+typedef struct hdd_comm hdd_comm;
+typedef struct hdd_shard hdd_shard;
+
+#define HDD_RCCL_ID_BYTES 128   /* sizeof(ncclUniqueId) */
+
+/* Host transport: moves n_peers messages (host memory, doubles) and returns HDD_OK; message k goes to
+ * rank peers[k] (send[k], send_count[k] doubles) and the message of that rank lands in recv[k]
+ * (recv_count[k] doubles).  Called synchronously from hdd_comm_post on the caller's thread (e.g. MPI,
+ * gloo or an in-process mailbox). */
+typedef int (*hdd_host_exchange_fn)(void* user, int32_t n_peers, const int32_t* peers, const double* const* send,
+                                    const int64_t* send_count, double* const* recv, const int64_t* recv_count);
+
+/* RCCL (librccl, resolved at run time in the calling process: PyTorch-ROCm's copy when it is loaded)
+ * -- ncclGetUniqueId on one rank, broadcast the HDD_RCCL_ID_BYTES bytes, ncclCommInitRank on every rank */
+int hdd_rccl_get_unique_id(void* id);
+int hdd_comm_create_rccl(const void* id, int32_t nranks, int32_t rank, int32_t hip_device, hdd_comm** out);
+/* wrap an existing ncclComm_t (not destroyed by hdd_comm_destroy) */
+int hdd_comm_wrap_rccl(void* nccl_comm, int32_t hip_device, hdd_comm** out);
+/* host-staged transport: device -> pinned host -> fn -> device (synchronous; rehearsal / tests / MPI) */
+int hdd_comm_create_host(hdd_host_exchange_fn fn, void* user, int32_t hip_device, hdd_comm** out);
+void hdd_comm_destroy(hdd_comm* comm);
+/* Post one exchange of device buffers: it starts after the work enqueued on `stream` so far; RCCL runs
+ * it on the communicator's own transfer stream (ncclGroupStart / ncclSend / ncclRecv / ncclGroupEnd), so
+ * work enqueued on `stream` afterwards overlaps it until hdd_comm_wait(comm, stream). */
+int hdd_comm_post(hdd_comm* comm, int32_t n_peers, const int32_t* peers, const double* const* d_send,
+                  const int64_t* send_count, double* const* d_recv, const int64_t* recv_count, void* stream);
+/* make `stream` wait for the receives of the last hdd_comm_post (no host blocking with RCCL) */
+int hdd_comm_wait(hdd_comm* comm, void* stream);
+
+typedef struct {
+  int64_t n_local, own_begin, own_end, n_ghost, global_first;   /* as hdd_local_info */
+  int64_t n_rows, n_cols, nnz;      /* owned rows (nb per owned element), global columns, pattern nnz */
+  int32_t rank, nranks, s_begin, s_end, n_peers, nb;
+  int64_t n_tiles, n_tiles_interior, n_tiles_boundary;   /* 64-element tiles of the owned elements */
+  int64_t halo_send, halo_recv;     /* elements sent / ghost elements received per exchange */
+  int64_t halo_faces;               /* faces between an owned and a ghost element */
+} hdd_shard_info;
+
+/* Rank `rank` of `nranks` owns the subdomains s with owner[s] == rank, which must form one contiguous
+ * range (owner == NULL: contiguous near-equal ranges, [n_sub r / nranks, n_sub (r+1) / nranks)).  Builds
+ * the rank-local mesh (host work O(owned + ghost elements): the structured grids are implicit, nothing
+ * global is materialised), uploads it with the ghost geometry, the halo plan, the device send lists and
+ * the interior / halo-boundary 64-element tile lists. */
+int hdd_shard_create(hdd_ctx* ctx, const hdd_grid* g, int32_t nranks, int32_t rank, const int32_t* owner,
+                     hdd_shard** out);
+void hdd_shard_destroy(hdd_shard* sh);
+int hdd_shard_get_info(const hdd_shard* sh, hdd_shard_info* out);
+/* the shard's device mesh (shard-owned arrays; usable with every hdd_* device call) */
+int hdd_shard_mesh(const hdd_shard* sh, hdd_mesh* out);
+/* host arrays [n_local]: global element ids; element barycentres [dim][n_local] (coefficient lookup) */
+int hdd_shard_global_ids(const hdd_shard* sh, int64_t* global_id);
+int hdd_shard_centers(const hdd_shard* sh, double* centers);
+/* device pattern of the owned rows (global columns) into caller buffers d_row_ptr [n_rows+1],
+ * d_col [nnz], d_elem_ptr [own_end-own_begin+1]; synchronises `stream` */
+int hdd_shard_pattern_fill(hdd_ctx* ctx, const hdd_shard* sh, int64_t* d_row_ptr, int32_t* d_col,
+                           int64_t* d_elem_ptr, void* stream);
+
+enum {
+  HDD_SHARD_NO_OVERLAP = 1,     /* exchange, then assemble every tile (default: interior tiles overlap the halo) */
+  HDD_SHARD_HALO_GEOMETRY = 2,  /* also send the ghost vertex coordinates (default: geometry is rank-local) */
+  HDD_SHARD_NO_HALO = 4         /* ghost columns already valid (static coefficients): no exchange at all */
+};
+/* One sharded assembly step -- the LHS of BlockSWIPDG::init() for the owned subdomains: pack the halo
+ * records (per-element tensor / kappa rows, [+ coordinates]) of the elements the peers need -> post the
+ * exchange -> interior tiles -> wait -> unpack into the ghost columns -> halo-boundary tiles.  The
+ * per-element arrays of `kappa` / `tensor` must span n_local columns: their owned columns are read and
+ * their GHOST COLUMNS ARE WRITTEN by the unpack.  comm may be NULL when the shard has no peers. */
+int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm* comm, const hdd_scalar_fn* kappa,
+                               int32_t n_comp, const hdd_tensor_fn* tensor, const hdd_swipdg_params* params,
+                               const hdd_csr* pattern, double* const* d_vals, uint32_t flags, void* stream);
 
 #ifdef __cplusplus
 }

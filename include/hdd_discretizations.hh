@@ -3,40 +3,199 @@
 // Mirrors, for the assembly hot path, the reference's discretization classes (header-only C++ like the
 // reference itself) on top of the C ABI in hdd.h:
 //   Dune::HDD::LinearElliptic::Discretizations::SWIPDG       (discretizations/swipdg.hh:109-520)
-//     ctor validation (swipdg.hh:172-176), pattern() (201-204), init() (206-512: system matrix, right-hand
-//     side, products), system_matrix() / rhs() (base.hh:240-258, affinely decomposed containers: affine part
-//     + components with ParameterFunctional coefficients), freeze_parameter(mu) (base.hh:338-341, 357-361),
-//     available_products() / get_product(id) (base.hh:266-322; "l2", "h1_semi", "elliptic", "boundary_l2",
-//     "penalty", "energy" as registered at swipdg.hh:358-508)
+//     ctor(grid_provider, boundary_cfg, problem, level_or_subdomain, only_these_products) (swipdg.hh:159-198)
+//     with its validation (172-176), pattern() (201-204), init(out, prefix) (206-512: "assembling... done
+//     (took Xs)", system matrix, right-hand side with the parametric force / Dirichlet / Neumann component
+//     structure of 251-356, the requested products 358-508), system_matrix() / rhs() / get_operator() /
+//     get_rhs() (base.hh:240-270), available_products() / get_product(id) (base.hh:272-291),
+//     freeze_parameter(mu) (base.hh:338-341, 357-361)
 //   Dune::HDD::LinearElliptic::Discretizations::BlockSWIPDG  (discretizations/block-swipdg.hh:177-846)
-//     num_subdomains() (553), neighbouring_subdomains(ss) (558), localize_vector (567),
-//     globalize_vectors (583), get_local_operator(ss) (625), get_coupling_operator(ss, nn) (639)
+//     ctor(ms_grid_provider, ignored cfg, problem, products) with the ZeroBoundary / AllDirichlet
+//     replacement (172-176, 230-255), init(out, prefix) (262-551), num_subdomains() (553),
+//     neighbouring_subdomains(ss) (558), localize_vector (567), globalize_vectors (583),
+//     get_local_product(ss, id) (612), get_local_operator(ss) (625), get_coupling_operator(ss, nn) (639),
+//     get_local_functional(ss) (678), get_local_discretization(ss) (761)
+//   ShardedBlockSWIPDG: BlockSWIPDG with its subdomains distributed over one process / thread per GPU
+//     (SURVEY.md 8(e)); each rank owns a contiguous subdomain range and assembles its rows through
+//     hdd_block_assemble_sharded, the face halo moved by a Parallel::Communicator (RCCL or host transport).
 // Errors are thrown as exceptions on this side (DUNE_THROW's role), never across the C ABI.
 #pragma once
 
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
+#include <chrono>
+#include <cmath>
 #include <cstdint>
+#include <cstring>
+#include <limits>
+#include <map>
 #include <memory>
+#include <ostream>
+#include <set>
 #include <stdexcept>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "hdd.h"
 
 namespace Dune {
+
+// DUNE_THROW(NotImplemented, ...) of the reference (swipdg.hh:174)
+struct NotImplemented : std::logic_error {
+  using std::logic_error::logic_error;
+};
+
+namespace Stuff {
+namespace Exceptions {   // dune-stuff exception types the reference throws (base.hh:285-289, block-swipdg.hh:560-562)
+struct wrong_input_given : std::invalid_argument {
+  using std::invalid_argument::invalid_argument;
+};
+struct you_are_using_this_wrong : std::logic_error {
+  using std::logic_error::logic_error;
+};
+struct index_out_of_range : std::out_of_range {
+  using std::out_of_range::out_of_range;
+};
+struct internal_error : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+struct requirements_not_met : std::logic_error {
+  using std::logic_error::logic_error;
+};
+}  // namespace Exceptions
+
+namespace Common {
+// Stuff::Common::Configuration: the key/value tree the reference passes boundary infos and problems as
+class Configuration {
+ public:
+  Configuration() = default;
+  Configuration(std::initializer_list<std::pair<const std::string, std::string>> kv) : m_(kv) {}
+  bool has_key(const std::string& k) const { return m_.count(k) > 0; }
+  std::string get(const std::string& k, const std::string& def = "") const
+  {
+    const auto it = m_.find(k);
+    return it == m_.end() ? def : it->second;
+  }
+  std::string& operator[](const std::string& k) { return m_[k]; }
+
+ private:
+  std::map<std::string, std::string> m_;
+};
+// Stuff::Common::Logger().devnull(): the default `out` of init()
+inline std::ostream& devnull()
+{
+  static std::ostream null(nullptr);
+  return null;
+}
+}  // namespace Common
+
+namespace Grid {
+namespace BoundaryInfos {
+struct AllDirichlet {
+  static std::string static_id() { return "stuff.grid.boundaryinfo.alldirichlet"; }
+  static Common::Configuration default_config() { return {{"type", static_id()}}; }
+};
+struct AllNeumann {
+  static std::string static_id() { return "stuff.grid.boundaryinfo.allneumann"; }
+  static Common::Configuration default_config() { return {{"type", static_id()}}; }
+};
+// boundary info config -> neighbour code of domain-boundary faces
+inline int32_t boundary_code(const Common::Configuration& cfg)
+{
+  const std::string t = cfg.get("type", AllDirichlet::static_id());
+  if (t == AllDirichlet::static_id() || t == "alldirichlet") return HDD_NBR_DIRICHLET;
+  if (t == AllNeumann::static_id() || t == "allneumann") return HDD_NBR_NEUMANN;
+  throw Exceptions::wrong_input_given("unknown boundary info type '" + t + "' (AllDirichlet / AllNeumann)");
+}
+}  // namespace BoundaryInfos
+
+namespace Providers {
+// Stuff::Grid::Providers::Cube + globalRefine: a structured nx x ny grid of [lower, upper] (quads, or the Kuhn
+// triangulation for simplices) and its uniform refinements; level l has nx 2^l x ny 2^l squares
+// (testcases/ESV2007.hh:123-129, testcases/spe10.hh:301-307, the refinement ladder of testcases/base.hh:92-103)
+class Cube {
+ public:
+  Cube(int elem_type, std::array<double, 2> lower, std::array<double, 2> upper, std::array<int, 2> num_elements,
+       int num_refinements = 0)
+  {
+    for (int l = 0; l <= num_refinements; ++l) {
+      hdd_structured_desc d{elem_type, num_elements[0] << l, num_elements[1] << l, 1, 1, HDD_BOUNDARY_ALL_DIRICHLET, 0,
+                            {lower[0], lower[1]}, {upper[0], upper[1]}};
+      hdd_grid* g = nullptr;
+      if (hdd_grid_create_structured(&d, &g) != HDD_OK)
+        throw Exceptions::wrong_input_given(std::string("Providers::Cube: ") + hdd_last_error(nullptr));
+      levels_.emplace_back(g, hdd_grid_destroy);
+    }
+  }
+  int num_levels() const { return int(levels_.size()); }
+  const hdd_grid* grid(int level) const
+  {
+    if (level < 0 || level >= num_levels())
+      throw Exceptions::index_out_of_range("level " + std::to_string(level) + " not in [0, " +
+                                           std::to_string(num_levels()) + ")");
+    return levels_[size_t(level)].get();
+  }
+
+ private:
+  std::vector<std::shared_ptr<hdd_grid>> levels_;
+};
+}  // namespace Providers
+}  // namespace Grid
+}  // namespace Stuff
+
+namespace grid {
+namespace Multiscale {
+namespace Providers {
+// grid::Multiscale::Providers::Cube with num_partitions [px py 1] (testcases/base.hh:150-191): one grid whose
+// subdomain-major element order is the block numbering
+class Cube {
+ public:
+  Cube(int elem_type, std::array<double, 2> lower, std::array<double, 2> upper, std::array<int, 2> num_elements,
+       std::array<int, 2> num_partitions)
+  {
+    hdd_structured_desc d{elem_type, num_elements[0], num_elements[1], num_partitions[0], num_partitions[1],
+                          HDD_BOUNDARY_ALL_DIRICHLET, 0, {lower[0], lower[1]}, {upper[0], upper[1]}};
+    hdd_grid* g = nullptr;
+    if (hdd_grid_create_structured(&d, &g) != HDD_OK)
+      throw Stuff::Exceptions::wrong_input_given(std::string("Multiscale::Providers::Cube: ") + hdd_last_error(nullptr));
+    g_.reset(g, hdd_grid_destroy);
+  }
+  // adopt a grid carrying a subdomain partition (not destroyed)
+  explicit Cube(const hdd_grid* g) : g_(const_cast<hdd_grid*>(g), [](hdd_grid*) {}) {}
+  const hdd_grid* grid() const { return g_.get(); }
+  int num_subdomains() const
+  {
+    hdd_grid_info gi{};
+    hdd_grid_get_info(g_.get(), &gi);
+    return gi.n_subdomains;
+  }
+
+ private:
+  std::shared_ptr<hdd_grid> g_;
+};
+}  // namespace Providers
+}  // namespace Multiscale
+}  // namespace grid
+
 namespace HDD {
 namespace LinearElliptic {
 
 namespace internal {
 inline void check(int rc, const char* what)
 {
-  if (rc != HDD_OK) throw std::runtime_error(std::string(what) + ": " + hdd_last_error(nullptr));
+  if (rc == HDD_OK) return;
+  const std::string msg = std::string(what) + ": " + hdd_last_error(nullptr);
+  if (rc == HDD_ERR_RANGE) throw Stuff::Exceptions::index_out_of_range(msg);
+  if (rc == HDD_ERR_INVALID) throw Stuff::Exceptions::wrong_input_given(msg);
+  if (rc == HDD_ERR_UNSUPPORTED) throw NotImplemented(msg);
+  throw Stuff::Exceptions::internal_error(msg);
 }
 inline void hip_check(hipError_t e, const char* what)
 {
-  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+  if (e != hipSuccess) throw Stuff::Exceptions::internal_error(std::string(what) + ": " + hipGetErrorString(e));
 }
 // owning device buffer
 template <class T>
@@ -71,31 +230,57 @@ class DeviceArray {
   T* p_ = nullptr;
   size_t n_ = 0;
 };
+using Timer = std::chrono::steady_clock;
+inline double seconds_since(Timer::time_point t0)
+{
+  return std::chrono::duration<double>(Timer::now() - t0).count();
+}
 }  // namespace internal
 
 namespace Pymor {
-// theta(mu) = scale * mu: the ParameterFunctional forms of the reference's parametric problems
-// ("mu", problems/OS2014.hh:74; "-1.0*mu", problems/spe10.hh:167)
+// theta(mu) = scale * mu^power: the ParameterFunctional forms of the reference's parametric problems ("mu",
+// problems/OS2014.hh:74; "-1.0*mu", problems/spe10.hh:167) and their products, which SWIPDG registers for
+// the kappa_p x g_D,q right-hand-side components ("(" + theta_p + ")*(" + theta_q + ")", swipdg.hh:317-330)
 class ParameterFunctional {
  public:
-  ParameterFunctional(std::string name = "mu", std::string expression = "mu", double scale = 1.0)
-    : name_(std::move(name)), expression_(std::move(expression)), scale_(scale) {}
-  double evaluate(double mu) const { return scale_ * mu; }
+  ParameterFunctional(std::string name = "mu", std::string expression = "mu", double scale = 1.0, int power = 1)
+    : name_(std::move(name)), expression_(std::move(expression)), scale_(scale), power_(power) {}
+  double evaluate(double mu) const { return scale_ * std::pow(mu, power_); }
   const std::string& expression() const { return expression_; }
-  bool operator==(const ParameterFunctional& o) const { return name_ == o.name_ && scale_ == o.scale_; }
+  const std::string& name() const { return name_; }
+  ParameterFunctional operator*(const ParameterFunctional& o) const
+  {
+    return ParameterFunctional(name_, "(" + expression_ + ")*(" + o.expression_ + ")", scale_ * o.scale_,
+                               power_ + o.power_);
+  }
+  bool operator==(const ParameterFunctional& o) const
+  {
+    return name_ == o.name_ && scale_ == o.scale_ && power_ == o.power_;
+  }
+
  private:
   std::string name_, expression_;
   double scale_;
+  int power_;
 };
 }  // namespace Pymor
 
 namespace Problems {
-// a (localizable) scalar function as the assembly path evaluates it
+// a (localizable) scalar function as the assembly path evaluates it: analytic kinds are evaluated on the
+// device at quadrature points; Checkerboard / Indicator (order 0, entity-centre based) are evaluated at the
+// element barycentres on the host and uploaded as per-element values
 struct ScalarFunction {
+  enum Host { DEVICE = 0, CHECKERBOARD = 1, INDICATOR = 2 };
   int kind = HDD_FN_CONST;
+  int host = DEVICE;
   int order = 0;
   double c = 1.0, b = 0.0, kx = 0.0, ky = 0.0;
-  std::vector<double> per_element;   // global element order
+  std::vector<double> per_element;   // PER_ELEM: global element order
+  // CHECKERBOARD: cells (x fastest) on [lower, upper]; INDICATOR: boxes [5k..5k+4] = lx, ly, ux, uy, value
+  std::array<double, 2> lower{{0.0, 0.0}}, upper{{1.0, 1.0}};
+  int ncx = 1, ncy = 1;
+  std::vector<double> table;
+
   static ScalarFunction constant(double v) { ScalarFunction f; f.c = v; return f; }
   static ScalarFunction piecewise_constant(std::vector<double> v)
   {
@@ -111,12 +296,32 @@ struct ScalarFunction {
   {
     ScalarFunction f; f.kind = HDD_FN_COS_PRODUCT; f.c = a; f.b = kz; f.kx = kx; f.ky = ky; f.order = order; return f;
   }
-  bool is_zero() const { return kind == HDD_FN_CONST && c == 0.0; }
+  // Stuff::Functions::Checkerboard (the Spe10::Model1 permeability field, problems/spe10.hh:151-156)
+  static ScalarFunction checkerboard(std::array<double, 2> lower, std::array<double, 2> upper, int ncx, int ncy,
+                                     std::vector<double> cells)
+  {
+    if (int64_t(cells.size()) != int64_t(ncx) * ncy)
+      throw Stuff::Exceptions::wrong_input_given("Checkerboard: need ncx * ncy cell values");
+    ScalarFunction f; f.kind = HDD_FN_PER_ELEM; f.host = CHECKERBOARD; f.lower = lower; f.upper = upper;
+    f.ncx = ncx; f.ncy = ncy; f.table = std::move(cells); return f;
+  }
+  // Stuff::Functions::Indicator (problems/spe10.hh:144, 157): value of the first box holding the entity centre
+  static ScalarFunction indicator(std::vector<std::array<double, 5>> boxes)
+  {
+    ScalarFunction f; f.kind = HDD_FN_PER_ELEM; f.host = INDICATOR;
+    for (const auto& bx : boxes) f.table.insert(f.table.end(), bx.begin(), bx.end());
+    return f;
+  }
+  bool is_zero() const { return kind == HDD_FN_CONST && host == DEVICE && c == 0.0; }
 };
+
 struct TensorFunction {
+  enum Host { DEVICE = 0, CHECKERBOARD_ISO = 1 };
   int kind = HDD_TENSOR_CONST;
+  int host = DEVICE;
   double c[6] = {1.0, 0.0, 1.0, 0.0, 0.0, 0.0};   // 2d a11 a12 a22; 3d a11 a12 a13 a22 a23 a33 (see identity3d)
-  std::vector<double> per_element;   // ISO: [ne]; SYM: [3 | 6][ne]
+  std::vector<double> per_element;   // ISO: [ne]; SYM: [3 | 6][ne] (global element order)
+  ScalarFunction field;              // CHECKERBOARD_ISO: A = field(x) I
   static TensorFunction identity3d()
   {
     TensorFunction t;
@@ -129,26 +334,142 @@ struct TensorFunction {
   {
     TensorFunction t; t.kind = HDD_TENSOR_ISO_PER_ELEM; t.per_element = std::move(v); return t;
   }
+  static TensorFunction symmetric(std::vector<double> v)
+  {
+    TensorFunction t; t.kind = HDD_TENSOR_SYM_PER_ELEM; t.per_element = std::move(v); return t;
+  }
+  // Stuff::Functions::Spe10::Model1 (problems/spe10.hh:151-156): checkerboard value times the identity
+  static TensorFunction spe10_model1(std::vector<double> cells, std::array<double, 2> lower = {{0.0, 0.0}},
+                                     std::array<double, 2> upper = {{5.0, 1.0}}, int ncx = 100, int ncy = 20)
+  {
+    TensorFunction t; t.kind = HDD_TENSOR_ISO_PER_ELEM; t.host = CHECKERBOARD_ISO;
+    t.field = ScalarFunction::checkerboard(lower, upper, ncx, ncy, std::move(cells));
+    return t;
+  }
 };
-// AffinelyDecomposable diffusion factor: kappa(mu) = kappa_aff + sum_q theta_q(mu) kappa_q
-struct DiffusionFactor {
+
+// Pymor AffinelyDecomposableDefault: f(mu) = f_aff + sum_q theta_q(mu) f_q; a plain ScalarFunction converts
+// to the nonparametric form (affine part only)
+struct AffinelyDecomposedFunction {
   bool has_affine_part = true;
   ScalarFunction affine_part = ScalarFunction::constant(1.0);
   std::vector<ScalarFunction> components;
   std::vector<Pymor::ParameterFunctional> coefficients;
+  AffinelyDecomposedFunction() = default;
+  AffinelyDecomposedFunction(const ScalarFunction& f) : affine_part(f) {}   // NOLINT: implicit by design
   int num_components() const { return int(components.size()); }
+  bool parametric() const { return !components.empty(); }
+  void register_component(ScalarFunction f, Pymor::ParameterFunctional theta)
+  {
+    components.push_back(std::move(f));
+    coefficients.push_back(std::move(theta));
+  }
 };
+using DiffusionFactor = AffinelyDecomposedFunction;
+
 struct Problem {
   DiffusionFactor diffusion_factor;
   TensorFunction diffusion_tensor;
   bool diffusion_tensor_parametric = false;
   bool diffusion_tensor_empty = false;
-  // right-hand side data (non-parametric): force, Dirichlet and Neumann values (zero = absent)
-  ScalarFunction force = ScalarFunction::constant(0.0);
-  ScalarFunction dirichlet = ScalarFunction::constant(0.0);
-  ScalarFunction neumann = ScalarFunction::constant(0.0);
+  AffinelyDecomposedFunction force = ScalarFunction::constant(0.0);
+  AffinelyDecomposedFunction dirichlet = ScalarFunction::constant(0.0);
+  AffinelyDecomposedFunction neumann = ScalarFunction::constant(0.0);
 };
+
+// Problems::ZeroBoundary (problems/zero-boundary.hh:54-60): same data, Dirichlet and Neumann values 0
+inline Problem ZeroBoundary(const Problem& p)
+{
+  Problem z = p;
+  z.dirichlet = ScalarFunction::constant(0.0);
+  z.neumann = ScalarFunction::constant(0.0);
+  return z;
+}
+
+// ESV2007 (problems/ESV2007.hh:75-81): kappa = 1, A = I, f = 1/2 pi^2 cos(pi x/2) cos(pi y/2), g_D = g_N = 0
+inline Problem ESV2007()
+{
+  Problem p;
+  p.force = ScalarFunction::cos_product(0.5 * M_PI * M_PI, 0.5 * M_PI, 0.5 * M_PI, 0.0, 3);
+  return p;
+}
+
+// OS2014 (problems/OS2014.hh:63-76): kappa(mu) = 1 + 3/4 sin(4 pi (x + y/2)) - mu 3/4 sin(4 pi (x + y/2)), A = I,
+// f = 1 (integration order 3 of the Expression functions, 88-96)
+inline Problem OS2014()
+{
+  Problem p;
+  const double kx = 4.0 * M_PI, ky = 2.0 * M_PI;
+  p.diffusion_factor.affine_part = ScalarFunction::sinusoid(1.0, 0.75, kx, ky, 3);
+  p.diffusion_factor.register_component(ScalarFunction::sinusoid(0.0, -0.75, kx, ky, 3),
+                                        Pymor::ParameterFunctional("mu", "mu", 1.0));
+  p.force = ScalarFunction::constant(1.0);
+  return p;
+}
+
+// Spe10::Model1 (problems/spe10.hh:131-185): A = permeability checkerboard (100 x 20 cells on [0,5]x[0,1]),
+// force = Indicator(force boxes), g_D = g_N = 0; diffusion factor 1 + 0.9 channel, or with
+// parametric_channel the affine part 1 + channel and the component channel with theta = -1.0*mu
+// (problems/spe10.hh:160-172).  The channel is an Indicator (channel_boundary_layer = 0,
+// testcases/spe10.hh:257; FlatTop layers are not supported).
+inline Problem Spe10Model1(std::vector<double> permeability, std::vector<std::array<double, 5>> channel,
+                           std::vector<std::array<double, 5>> forces, bool parametric_channel)
+{
+  Problem p;
+  p.diffusion_tensor = TensorFunction::spe10_model1(std::move(permeability));
+  p.force = ScalarFunction::indicator(std::move(forces));
+  if (channel.empty()) return p;   // no channel: diffusion factor 1 (problems/spe10.hh:141-142)
+  std::vector<std::array<double, 5>> one_plus = channel, scaled = channel;
+  for (auto& bx : one_plus) bx[4] = 1.0 + bx[4];    // 1 + channel (boxes disjoint, 1 outside)
+  for (auto& bx : scaled) bx[4] = 1.0 + 0.9 * bx[4];
+  auto affine = ScalarFunction::indicator(parametric_channel ? one_plus : scaled);
+  affine.table.insert(affine.table.end(), {-1e300, -1e300, 1e300, 1e300, 1.0});   // outside the channel: 1
+  p.diffusion_factor.affine_part = affine;
+  if (parametric_channel)
+    p.diffusion_factor.register_component(ScalarFunction::indicator(std::move(channel)),
+                                          Pymor::ParameterFunctional("mu", "-1.0*mu", -1.0));
+  return p;
+}
 }  // namespace Problems
+
+namespace Parallel {
+// the face-halo transport of a ShardedBlockSWIPDG (hdd_comm): RCCL between one process per GPU, an existing
+// ncclComm_t, or a host callback (MPI, an in-process mailbox, ...)
+class Communicator {
+ public:
+  Communicator() = default;   // no peers (a single rank)
+  static std::string rccl_unique_id()
+  {
+    std::string id(HDD_RCCL_ID_BYTES, '\0');
+    internal::check(hdd_rccl_get_unique_id(&id[0]), "hdd_rccl_get_unique_id");
+    return id;
+  }
+  static Communicator rccl(const std::string& unique_id, int nranks, int rank, int hip_device)
+  {
+    if (unique_id.size() != HDD_RCCL_ID_BYTES) throw Stuff::Exceptions::wrong_input_given("RCCL unique id size");
+    hdd_comm* c = nullptr;
+    internal::check(hdd_comm_create_rccl(unique_id.data(), nranks, rank, hip_device, &c), "hdd_comm_create_rccl");
+    return Communicator(c);
+  }
+  static Communicator wrap_rccl(void* nccl_comm, int hip_device)
+  {
+    hdd_comm* c = nullptr;
+    internal::check(hdd_comm_wrap_rccl(nccl_comm, hip_device, &c), "hdd_comm_wrap_rccl");
+    return Communicator(c);
+  }
+  static Communicator host(hdd_host_exchange_fn fn, void* user, int hip_device)
+  {
+    hdd_comm* c = nullptr;
+    internal::check(hdd_comm_create_host(fn, user, hip_device, &c), "hdd_comm_create_host");
+    return Communicator(c);
+  }
+  hdd_comm* get() const { return c_.get(); }
+
+ private:
+  explicit Communicator(hdd_comm* c) : c_(c, hdd_comm_destroy) {}
+  std::shared_ptr<hdd_comm> c_;
+};
+}  // namespace Parallel
 
 namespace Discretizations {
 
@@ -175,8 +496,9 @@ class AffinelyDecomposedMatrix {
   bool has_affine_part() const { return bool(affine); }
   int num_components() const { return int(comps.size()); }
   bool parametric() const { return !comps.empty(); }
-  std::vector<double> affine_part() const { return affine->download(); }
-  std::vector<double> component(int q) const { return comps.at(q)->download(); }
+  std::vector<double> affine_part() const { return trimmed(*affine); }
+  std::vector<double> component(int q) const { return trimmed(*comps.at(size_t(q))); }
+  const Pymor::ParameterFunctional& coefficient(int q) const { return coefficients.at(size_t(q)); }
   // A(mu) = A_aff + sum_q theta_q(mu) A_q on the shared pattern (hdd_affine_lincomb)
   std::vector<double> freeze_parameter(double mu) const
   {
@@ -192,6 +514,14 @@ class AffinelyDecomposedMatrix {
     h.resize(size_t(pattern->nnz));
     return h;
   }
+
+ private:
+  std::vector<double> trimmed(const internal::DeviceArray<double>& a) const
+  {
+    auto h = a.download();
+    h.resize(size_t(pattern->nnz));
+    return h;
+  }
 };
 
 // AffinelyDecomposedContainer<Vector> (the right-hand side)
@@ -203,8 +533,21 @@ class AffinelyDecomposedVector {
   int64_t size = 0;
   bool has_affine_part() const { return bool(affine); }
   int num_components() const { return int(comps.size()); }
+  bool parametric() const { return !comps.empty(); }
   std::vector<double> affine_part() const { auto h = affine->download(); h.resize(size_t(size)); return h; }
-  std::vector<double> component(int q) const { auto h = comps.at(q)->download(); h.resize(size_t(size)); return h; }
+  std::vector<double> component(int q) const { auto h = comps.at(size_t(q))->download(); h.resize(size_t(size)); return h; }
+  const Pymor::ParameterFunctional& coefficient(int q) const { return coefficients.at(size_t(q)); }
+  // b(mu) = b_aff + sum_q theta_q(mu) b_q (host)
+  std::vector<double> freeze_parameter(double mu) const
+  {
+    std::vector<double> out = affine ? affine_part() : std::vector<double>(size_t(size), 0.0);
+    for (int q = 0; q < num_components(); ++q) {
+      const auto c = component(q);
+      const double t = coefficients[size_t(q)].evaluate(mu);
+      for (size_t i = 0; i < out.size(); ++i) out[i] += t * c[i];
+    }
+    return out;
+  }
 };
 
 namespace detail {
@@ -222,23 +565,144 @@ inline hdd_swipdg_params swipdg_params(int p, int dim)
   const double sb = p <= 1 ? 14.0 : (p == 2 ? 38.0 : (p == 3 ? 74.0 : 99.0));
   return hdd_swipdg_params{si, sb, 1.0 / (dim - 1), -1, -1};
 }
+
+// the element columns a function is localized to: n local columns with barycentres and global ids; with
+// halo_ghosts the ghost columns are left NaN (a sharded assembly fills them through the face halo)
+struct ElementView {
+  int64_t n = 0, own_begin = 0, own_end = 0;
+  int dim = 2;
+  const double* centers = nullptr;    // [dim][n]
+  const int64_t* gid = nullptr;       // [n]
+  int64_t n_global = 0;
+  bool halo_ghosts = false;
+};
+
+inline std::vector<double> localize(const Problems::ScalarFunction& f, const ElementView& v)
+{
+  std::vector<double> h(static_cast<size_t>(v.n));
+  if (f.host == Problems::ScalarFunction::CHECKERBOARD || f.host == Problems::ScalarFunction::INDICATOR) {
+    if (v.dim != 2) throw NotImplemented("Checkerboard / Indicator functions are 2d");
+    if (f.host == Problems::ScalarFunction::CHECKERBOARD)
+      internal::check(hdd_checkerboard(v.n, v.centers, f.lower.data(), f.upper.data(), f.ncx, f.ncy, f.table.data(),
+                                       h.data()), "hdd_checkerboard");
+    else
+      internal::check(hdd_indicator(v.n, v.centers, int32_t(f.table.size() / 5), f.table.data(), h.data()),
+                      "hdd_indicator");
+  } else {
+    if (int64_t(f.per_element.size()) != v.n_global)
+      throw Stuff::Exceptions::wrong_input_given("per-element function: " + std::to_string(f.per_element.size()) +
+                                                 " values for " + std::to_string(v.n_global) + " elements");
+    for (int64_t e = 0; e < v.n; ++e) h[size_t(e)] = f.per_element[size_t(v.gid[e])];
+  }
+  if (v.halo_ghosts)
+    for (int64_t e = 0; e < v.n; ++e)
+      if (e < v.own_begin || e >= v.own_end) h[size_t(e)] = std::numeric_limits<double>::quiet_NaN();
+  return h;
+}
+
+// a scalar function bound to the device (per-element values uploaded, kept alive with the descriptor)
+struct DeviceFn {
+  hdd_scalar_fn fn{};
+  std::shared_ptr<internal::DeviceArray<double>> pe;
+  DeviceFn() = default;
+  DeviceFn(const Problems::ScalarFunction& f, const ElementView& v)
+  {
+    if (f.kind == HDD_FN_PER_ELEM) pe = std::make_shared<internal::DeviceArray<double>>(localize(f, v));
+    fn = hdd_scalar_fn{f.kind, f.order, f.c, f.b, f.kx, f.ky, pe ? pe->get() : nullptr};
+  }
+};
+
+struct DeviceTensor {
+  hdd_tensor_fn fn{};
+  std::shared_ptr<internal::DeviceArray<double>> pe;
+  DeviceTensor() = default;
+  DeviceTensor(const Problems::TensorFunction& T, const ElementView& v)
+  {
+    fn = hdd_tensor_fn{T.kind, 0, {T.c[0], T.c[1], T.c[2], T.c[3], T.c[4], T.c[5]}, nullptr};
+    if (T.kind == HDD_TENSOR_CONST) return;
+    std::vector<double> h;
+    if (T.host == Problems::TensorFunction::CHECKERBOARD_ISO) {
+      h = localize(T.field, v);
+    } else {
+      const int rows = T.kind == HDD_TENSOR_ISO_PER_ELEM ? 1 : (v.dim == 3 ? 6 : 3);
+      if (int64_t(T.per_element.size()) != rows * v.n_global)
+        throw Stuff::Exceptions::wrong_input_given("per-element tensor: wrong number of values");
+      h.resize(size_t(rows * v.n));
+      for (int r = 0; r < rows; ++r)
+        for (int64_t e = 0; e < v.n; ++e) {
+          const bool ghost = e < v.own_begin || e >= v.own_end;
+          h[size_t(r * v.n + e)] = (v.halo_ghosts && ghost) ? std::numeric_limits<double>::quiet_NaN()
+                                                             : T.per_element[size_t(r * v.n_global + v.gid[e])];
+        }
+    }
+    pe = std::make_shared<internal::DeviceArray<double>>(h);
+    fn.per_elem = pe->get();
+  }
+};
+
+inline const std::vector<std::string>& all_products()
+{
+  static const std::vector<std::string> p = {"l2", "h1_semi", "elliptic", "boundary_l2", "penalty", "energy"};
+  return p;
+}
 }  // namespace detail
 
+// ------------------------------------------------------------------------------------------------
+// SWIPDG (swipdg.hh:109-520)
+// ------------------------------------------------------------------------------------------------
 class SWIPDG {
  public:
-  // grid: the (multiscale) grid provider; the boundary info is part of the grid (AllDirichlet /
-  // AllNeumann); problem: diffusion factor (affinely decomposed) and tensor.
+  // which elements the discretization lives on: the whole grid (leaf / level layer) or one subdomain of a
+  // multiscale grid (ChooseLayer::local: faces to other subdomains are domain boundary, local numbering)
+  enum class Layer { leaf, local };
+
+  // swipdg.hh:159-163: level provider, boundary info config, problem, level, requested products
+  SWIPDG(const Stuff::Grid::Providers::Cube& grid_provider, const Stuff::Common::Configuration& bound_inf_cfg,
+         const Problems::Problem& prob, int level_or_subdomain = 0,
+         const std::vector<std::string>& only_these_products = {}, int hip_device = 0)
+    : SWIPDG(grid_provider.grid(level_or_subdomain), bound_inf_cfg, prob, Layer::leaf, 0, only_these_products,
+             hip_device) {}
+
+  // swipdg.hh:180-198: multiscale provider -> the (local layer) discretization of subdomain `level_or_subdomain`
+  SWIPDG(const grid::Multiscale::Providers::Cube& grid_provider, const Stuff::Common::Configuration& bound_inf_cfg,
+         const Problems::Problem& prob, int level_or_subdomain = 0,
+         const std::vector<std::string>& only_these_products = {}, int hip_device = 0)
+    : SWIPDG(grid_provider.grid(), bound_inf_cfg, prob, Layer::local, level_or_subdomain, only_these_products,
+             hip_device) {}
+
+  // convenience: the whole grid with the boundary the grid carries and every product available
   SWIPDG(const hdd_grid* grid, const Problems::Problem& problem, int hip_device = 0)
-    : grid_(grid), problem_(problem)
+    : SWIPDG(grid, Stuff::Common::Configuration(), problem, Layer::leaf, 0, detail::all_products(), hip_device,
+             /*grid_boundary=*/true) {}
+
+  SWIPDG(const hdd_grid* grid, const Stuff::Common::Configuration& bound_inf_cfg, const Problems::Problem& problem,
+         Layer layer, int subdomain, const std::vector<std::string>& only_these_products, int hip_device = 0,
+         bool grid_boundary = false)
+    : grid_(grid), problem_(problem), layer_(layer), subdomain_(subdomain), only_these_products_(only_these_products)
   {
     // swipdg.hh:172-176
-    if (problem.diffusion_tensor_parametric) throw std::logic_error("The diffusion tensor must not be parametric!");
-    if (problem.diffusion_tensor_empty) throw std::invalid_argument("The diffusion tensor must not be empty!");
+    if (problem.diffusion_tensor_parametric) throw NotImplemented("The diffusion tensor must not be parametric!");
+    if (problem.diffusion_tensor_empty)
+      throw Stuff::Exceptions::wrong_input_given("The diffusion tensor must not be empty!");
+    for (const auto& id : only_these_products)
+      if (std::find(detail::all_products().begin(), detail::all_products().end(), id) == detail::all_products().end())
+        throw Stuff::Exceptions::wrong_input_given("unknown product '" + id + "'");
     internal::check(hdd_grid_get_info(grid, &info_), "hdd_grid_get_info");
+    boundary_code_ = grid_boundary ? 0 : Stuff::Grid::BoundaryInfos::boundary_code(bound_inf_cfg);
     internal::check(hdd_ctx_create(hip_device, &ctx_), "hdd_ctx_create");
-    internal::check(hdd_local_create(grid, 0, info_.n_subdomains, &local_), "hdd_local_create");
+    int32_t s0 = 0, s1 = info_.n_subdomains;
+    if (layer == Layer::local) {
+      if (subdomain < 0 || subdomain >= info_.n_subdomains)
+        throw Stuff::Exceptions::index_out_of_range("Given subdomain " + std::to_string(subdomain) +
+                                                    " too large (has to be smaller than " +
+                                                    std::to_string(info_.n_subdomains) + "!");
+      s0 = subdomain;
+      s1 = subdomain + 1;
+    }
+    internal::check(hdd_local_create(grid, s0, s1, &local_), "hdd_local_create");
     internal::check(hdd_local_get_info(local_, &linfo_), "hdd_local_get_info");
     degree_ = detail::degree_of(info_);
+    build_view();
     build_pattern();
   }
   virtual ~SWIPDG()
@@ -249,74 +713,242 @@ class SWIPDG {
   SWIPDG(const SWIPDG&) = delete;
   SWIPDG& operator=(const SWIPDG&) = delete;
 
+  static std::string static_id() { return "hdd.linearelliptic.discretizations.containerbased.swipdg"; }
+
   const Pattern& pattern() const { return *pattern_; }
 
-  // assembles the system matrix (every diffusion-factor component + the affine part), the right-hand side
-  // and the requested products on the device; idempotent (container_based_initialized_, swipdg.hh:208)
-  void init()
+  // assembles the system matrix (every diffusion-factor component + the affine part), the right-hand side and
+  // the requested products on the device; idempotent (container_based_initialized_, swipdg.hh:208, 510)
+  void init(std::ostream& out = Stuff::Common::devnull(), const std::string& prefix = "")
   {
     if (initialized_) return;
-    const int64_t n = linfo_.n_local;
-    const int dim = info_.dim;
-    std::vector<double> coords(size_t(dim * info_.nvpe * n));
-    std::vector<int32_t> nbrs(size_t(info_.nfaces * n));
-    std::vector<uint32_t> finfo(static_cast<size_t>(n));
-    internal::check(hdd_local_fill(local_, coords.data(), nbrs.data(), finfo.data(), nullptr, nullptr), "hdd_local_fill");
-    d_coords_ = internal::DeviceArray<double>(coords);
-    d_nbrs_ = internal::DeviceArray<int32_t>(nbrs);
-    d_finfo_ = internal::DeviceArray<uint32_t>(finfo);
-    const auto& T = problem_.diffusion_tensor;
-    if (T.kind != HDD_TENSOR_CONST) d_tensor_ = internal::DeviceArray<double>(T.per_element);
-    mesh_ = hdd_mesh{info_.elem_type, degree_, n, linfo_.own_begin, linfo_.own_end, d_coords_.get(), d_nbrs_.get(),
-                     d_finfo_.get()};
-    tensor_ = hdd_tensor_fn{T.kind, 0, {T.c[0], T.c[1], T.c[2], T.c[3], T.c[4], T.c[5]}, d_tensor_.get()};
-    prm_ = detail::swipdg_params(degree_, dim);
+    out << prefix << "assembling... " << std::flush;
+    const auto t0 = internal::Timer::now();
+    upload_mesh();
     const hdd_csr pat = pattern_->csr();
+    matrix_ = AffinelyDecomposedMatrix();
     matrix_.pattern = pattern_;
     matrix_.ctx = ctx_;
-    matrix_.coefficients = problem_.diffusion_factor.coefficients;
-    auto assemble = [&](const Problems::ScalarFunction& f) {
-      auto vals = std::make_shared<internal::DeviceArray<double>>(size_t(pattern_->nnz) + 1);
-      Fn k(f);
-      double* v = vals->get();
-      internal::check(hdd_swipdg_assemble(ctx_, &mesh_, &k.fn, 1, &tensor_, &prm_, &pat, &v, nullptr),
-                      "hdd_swipdg_assemble");
-      internal::hip_check(hipDeviceSynchronize(), "init");
-      return vals;
-    };
-    for (const auto& c : problem_.diffusion_factor.components) matrix_.comps.push_back(assemble(c));
-    if (problem_.diffusion_factor.has_affine_part) matrix_.affine = assemble(problem_.diffusion_factor.affine_part);
+    const auto& K = problem_.diffusion_factor;
+    matrix_.coefficients = K.coefficients;
+    for (const auto& c : K.components) matrix_.comps.push_back(assemble_lhs(c, pat));
+    if (K.has_affine_part) matrix_.affine = assemble_lhs(K.affine_part, pat);
     assemble_rhs();
+    products_.clear();
+    for (const auto& id : only_these_products_) products_[id] = std::make_shared<AffinelyDecomposedMatrix>(product(id));
+    internal::hip_check(hipDeviceSynchronize(), "init");
+    out << "done (took " << internal::seconds_since(t0) << "s)" << std::endl;
     initialized_ = true;
   }
 
+  // base.hh:240-270
   const AffinelyDecomposedMatrix& system_matrix() const
   {
-    if (!initialized_) throw std::logic_error("system_matrix(): call init() first");
+    assert_everything_is_ready();
     return matrix_;
   }
+  const AffinelyDecomposedMatrix& get_operator() const { return system_matrix(); }
   const AffinelyDecomposedVector& rhs() const
   {
-    if (!initialized_) throw std::logic_error("rhs(): call init() first");
+    assert_everything_is_ready();
     return rhs_;
   }
+  const AffinelyDecomposedVector& get_rhs() const { return rhs(); }
 
-  // base.hh:266-322: "l2", "h1_semi", "elliptic", "boundary_l2", "penalty", "energy"
+  // base.hh:272-291: only the products requested in the ctor (only_these_products, swipdg.hh:496-508)
   std::vector<std::string> available_products() const
   {
-    return {"l2", "h1_semi", "elliptic", "boundary_l2", "penalty", "energy"};
+    std::vector<std::string> ret;
+    for (const auto& kv : products_) ret.push_back(kv.first);
+    return ret;
   }
-  AffinelyDecomposedMatrix get_product(const std::string& id)
+  const AffinelyDecomposedMatrix& get_product(const std::string& id) const
   {
-    init();
-    if (id == "energy") return matrix_;
+    if (products_.empty())
+      throw Stuff::Exceptions::you_are_using_this_wrong("Do not call get_product() if available_products() is empty!");
+    const auto it = products_.find(id);
+    if (it == products_.end()) throw Stuff::Exceptions::wrong_input_given("Product '" + id + "' not available!");
+    return *it->second;
+  }
+
+  // true if no Dirichlet face was found (DirichletDetector, swipdg.hh:219, 488-489)
+  bool purely_neumann() const
+  {
+    assert_everything_is_ready();
+    return purely_neumann_;
+  }
+  int64_t num_dofs() const { return pattern_->rows; }
+  hdd_ctx* context() const { return ctx_; }
+  const hdd_grid* grid() const { return grid_; }
+  const Problems::Problem& problem() const { return problem_; }
+  int polynomial_order() const { return degree_; }
+  Layer layer() const { return layer_; }
+  int subdomain() const { return subdomain_; }
+
+ protected:
+  void assert_everything_is_ready() const
+  {
+    if (!initialized_)
+      throw Stuff::Exceptions::you_are_using_this_wrong("The user has to call init() before calling any other method!");
+  }
+
+  // host view of the elements: neighbour codes with the boundary info applied, columns (global / local)
+  void build_view()
+  {
+    const int64_t n = linfo_.n_local;
+    coords_.assign(size_t(info_.dim * info_.nvpe * n), 0.0);
+    nbrs_.assign(size_t(info_.nfaces * n), 0);
+    finfo_.assign(size_t(n), 0u);
+    gid_.assign(size_t(n), 0);
+    centers_.assign(size_t(info_.dim * n), 0.0);
+    internal::check(hdd_local_fill(local_, coords_.data(), nbrs_.data(), finfo_.data(), gid_.data(), nullptr),
+                    "hdd_local_fill");
+    internal::check(hdd_local_centers(local_, centers_.data()), "hdd_local_centers");
+    const int64_t ob = linfo_.own_begin, oe = linfo_.own_end;
+    for (int f = 0; f < info_.nfaces; ++f)
+      for (int64_t e = ob; e < oe; ++e) {
+        int32_t& nb = nbrs_[size_t(f * n + e)];
+        // faces to other subdomains are boundary of a local-layer discretization (its grid part ends there)
+        if (layer_ == Layer::local && nb >= 0 && (nb < ob || nb >= oe)) nb = HDD_NBR_DIRICHLET;
+        if (nb < 0 && boundary_code_ != 0) nb = boundary_code_;
+      }
+    // local layer: columns in the subdomain's own numbering (mapToGlobal is the block mapper's job)
+    cols_.assign(size_t(n), 0);
+    for (int64_t e = 0; e < n; ++e) cols_[size_t(e)] = layer_ == Layer::local ? e - ob : gid_[size_t(e)];
+    n_cols_ = layer_ == Layer::local ? (oe - ob) * info_.nb : info_.n_elements * info_.nb;
+    view_ = detail::ElementView{n, ob, oe, info_.dim, centers_.data(), gid_.data(), info_.n_elements, false};
+  }
+
+  std::shared_ptr<Pattern> host_pattern(int n_faces) const
+  {
+    auto P = std::make_shared<Pattern>();
+    const int64_t n = linfo_.n_local;
+    internal::check(hdd_dg_pattern_count(n_faces, info_.nb, n, linfo_.own_begin, linfo_.own_end, nbrs_.data(), &P->nnz),
+                    "hdd_dg_pattern_count");
+    const int64_t own = linfo_.own_end - linfo_.own_begin;
+    P->rows = own * info_.nb;
+    P->cols = n_cols_;
+    P->row_ptr.resize(size_t(P->rows + 1));
+    P->col.resize(size_t(P->nnz));
+    P->elem_ptr.resize(size_t(own + 1));
+    internal::check(hdd_dg_pattern_fill(n_faces, info_.nb, n, linfo_.own_begin, linfo_.own_end, nbrs_.data(),
+                                        cols_.data(), P->row_ptr.data(), P->col.data(), P->elem_ptr.data()),
+                    "hdd_dg_pattern_fill");
+    P->d_row_ptr = internal::DeviceArray<int64_t>(P->row_ptr);
+    P->d_col = internal::DeviceArray<int32_t>(P->col);
+    P->d_elem_ptr = internal::DeviceArray<int64_t>(P->elem_ptr);
+    return P;
+  }
+
+  void build_pattern() { pattern_ = host_pattern(info_.nfaces); }
+
+  std::shared_ptr<const Pattern> volume_pattern()
+  {
+    if (!volume_pattern_) volume_pattern_ = host_pattern(0);
+    return volume_pattern_;
+  }
+
+  void upload_mesh()
+  {
+    d_coords_ = internal::DeviceArray<double>(coords_);
+    d_nbrs_ = internal::DeviceArray<int32_t>(nbrs_);
+    d_finfo_ = internal::DeviceArray<uint32_t>(finfo_);
+    tensor_ = detail::DeviceTensor(problem_.diffusion_tensor, view_);
+    mesh_ = hdd_mesh{info_.elem_type, degree_, linfo_.n_local, linfo_.own_begin, linfo_.own_end, d_coords_.get(),
+                     d_nbrs_.get(), d_finfo_.get()};
+    prm_ = detail::swipdg_params(degree_, info_.dim);
+    purely_neumann_ = true;
+    for (int f = 0; f < info_.nfaces; ++f)
+      for (int64_t e = linfo_.own_begin; e < linfo_.own_end; ++e)
+        if (nbrs_[size_t(f * linfo_.n_local + e)] == HDD_NBR_DIRICHLET) purely_neumann_ = false;
+  }
+
+  std::shared_ptr<internal::DeviceArray<double>> assemble_lhs(const Problems::ScalarFunction& f, const hdd_csr& pat)
+  {
+    auto vals = std::make_shared<internal::DeviceArray<double>>(size_t(pattern_->nnz) + 1);
+    detail::DeviceFn k(f, view_);
+    double* v = vals->get();
+    internal::check(hdd_swipdg_assemble(ctx_, &mesh_, &k.fn, 1, &tensor_.fn, &prm_, &pat, &v, nullptr),
+                    "hdd_swipdg_assemble");
+    internal::hip_check(hipDeviceSynchronize(), "assemble");
+    return vals;
+  }
+
+  // one functional evaluation: L2Volume(force) + DirichletBoundarySWIPDG(kappa, A, g_D) + L2Face(g_N), each
+  // nullable (hdd_swipdg_rhs)
+  std::shared_ptr<internal::DeviceArray<double>> rhs_vector(const Problems::ScalarFunction* force,
+                                                            const Problems::ScalarFunction* kappa,
+                                                            const Problems::ScalarFunction* dirichlet,
+                                                            const Problems::ScalarFunction* neumann)
+  {
+    const int64_t size = pattern_->rows;
+    auto b = std::make_shared<internal::DeviceArray<double>>(size_t(size) + 1);
+    detail::DeviceFn f, k, d, nm;
+    if (force) f = detail::DeviceFn(*force, view_);
+    if (dirichlet) { k = detail::DeviceFn(*kappa, view_); d = detail::DeviceFn(*dirichlet, view_); }
+    if (neumann) nm = detail::DeviceFn(*neumann, view_);
+    internal::check(hdd_swipdg_rhs(ctx_, &mesh_, force ? &f.fn : nullptr, dirichlet ? &k.fn : nullptr, &tensor_.fn,
+                                   dirichlet ? &d.fn : nullptr, neumann ? &nm.fn : nullptr, &prm_, b->get(), nullptr),
+                    "hdd_swipdg_rhs");
+    internal::hip_check(hipDeviceSynchronize(), "rhs");
+    return b;
+  }
+
+  // swipdg.hh:251-356: the component structure of the reference's rhs container --
+  //   force components (theta_f,q)                      L2Volume(f_q)
+  //   affine part                                       L2Volume(f_aff) + Dirichlet(kappa_aff, g_D,aff) + L2Face(g_N,aff)
+  //   kappa_aff x g_D components (theta_D,q)            Dirichlet(kappa_aff, g_D,q)
+  //   kappa components x g_D,aff (theta_k,q)            Dirichlet(kappa_q, g_D,aff)
+  //   kappa_p x g_D,q ((theta_k,p)*(theta_D,q))         Dirichlet(kappa_p, g_D,q)
+  //   Neumann components (theta_N,q)                    L2Face(g_N,q)
+  void assemble_rhs()
+  {
+    const auto& P = problem_;
+    const auto& K = P.diffusion_factor;
+    const auto& F = P.force;
+    const auto& D = P.dirichlet;
+    const auto& N = P.neumann;
+    rhs_ = AffinelyDecomposedVector();
+    rhs_.size = pattern_->rows;
+    auto add = [&](std::shared_ptr<internal::DeviceArray<double>> v, const Pymor::ParameterFunctional& theta) {
+      rhs_.comps.push_back(std::move(v));
+      rhs_.coefficients.push_back(theta);
+    };
+    for (int q = 0; q < F.num_components(); ++q)
+      add(rhs_vector(&F.components[size_t(q)], nullptr, nullptr, nullptr), F.coefficients[size_t(q)]);
+    const bool dir_aff = K.has_affine_part && D.has_affine_part;
+    if (F.has_affine_part || dir_aff || N.has_affine_part)
+      rhs_.affine = rhs_vector(F.has_affine_part ? &F.affine_part : nullptr, dir_aff ? &K.affine_part : nullptr,
+                               dir_aff ? &D.affine_part : nullptr, N.has_affine_part ? &N.affine_part : nullptr);
+    if (K.has_affine_part)
+      for (int q = 0; q < D.num_components(); ++q)
+        add(rhs_vector(nullptr, &K.affine_part, &D.components[size_t(q)], nullptr), D.coefficients[size_t(q)]);
+    if (D.has_affine_part)
+      for (int q = 0; q < K.num_components(); ++q)
+        add(rhs_vector(nullptr, &K.components[size_t(q)], &D.affine_part, nullptr), K.coefficients[size_t(q)]);
+    for (int p = 0; p < K.num_components(); ++p)
+      for (int q = 0; q < D.num_components(); ++q)
+        add(rhs_vector(nullptr, &K.components[size_t(p)], &D.components[size_t(q)], nullptr),
+            K.coefficients[size_t(p)] * D.coefficients[size_t(q)]);
+    for (int q = 0; q < N.num_components(); ++q)
+      add(rhs_vector(nullptr, nullptr, nullptr, &N.components[size_t(q)]), N.coefficients[size_t(q)]);
+  }
+
+  // swipdg.hh:358-508 (over_integrate = 2): "l2", "h1_semi", "boundary_l2" nonparametric; "elliptic" and
+  // "penalty" affinely decomposed like kappa; "energy" = a copy of the system matrix
+  AffinelyDecomposedMatrix product(const std::string& id)
+  {
+    if (id == "energy") {
+      AffinelyDecomposedMatrix e = matrix_;   // shares the value arrays (read-only copy)
+      return e;
+    }
     int kind;
     if (id == "l2") kind = HDD_PRODUCT_L2;
     else if (id == "h1_semi") kind = HDD_PRODUCT_H1_SEMI;
     else if (id == "elliptic") kind = HDD_PRODUCT_ELLIPTIC;
     else if (id == "boundary_l2") kind = HDD_PRODUCT_BOUNDARY_L2;
     else if (id == "penalty") kind = HDD_PRODUCT_PENALTY;
-    else throw std::invalid_argument("Product '" + id + "' not available!");
+    else throw Stuff::Exceptions::wrong_input_given("Product '" + id + "' not available!");
     const bool volume = kind != HDD_PRODUCT_PENALTY;
     std::shared_ptr<const Pattern> P = volume ? volume_pattern() : std::shared_ptr<const Pattern>(pattern_);
     const hdd_csr pat = P->csr();
@@ -325,14 +957,14 @@ class SWIPDG {
     out.ctx = ctx_;
     auto run = [&](const Problems::ScalarFunction& f) {
       auto vals = std::make_shared<internal::DeviceArray<double>>(size_t(P->nnz) + 1);
-      Fn k(f);
-      internal::check(hdd_product_assemble(ctx_, &mesh_, kind, &k.fn, &tensor_, &prm_, &pat, vals->get(), nullptr),
+      detail::DeviceFn k(f, view_);
+      internal::check(hdd_product_assemble(ctx_, &mesh_, kind, &k.fn, &tensor_.fn, &prm_, &pat, vals->get(), nullptr),
                       "hdd_product_assemble");
-      internal::hip_check(hipDeviceSynchronize(), "get_product");
+      internal::hip_check(hipDeviceSynchronize(), "product");
       return vals;
     };
     const auto& K = problem_.diffusion_factor;
-    if (kind == HDD_PRODUCT_ELLIPTIC || kind == HDD_PRODUCT_PENALTY) {   // affinely decomposed like kappa
+    if (kind == HDD_PRODUCT_ELLIPTIC || kind == HDD_PRODUCT_PENALTY) {
       out.coefficients = K.coefficients;
       for (const auto& c : K.components) out.comps.push_back(run(c));
       if (K.has_affine_part) out.affine = run(K.affine_part);
@@ -342,156 +974,173 @@ class SWIPDG {
     return out;
   }
 
-  int64_t num_dofs() const { return pattern_->rows; }
-  hdd_ctx* context() const { return ctx_; }
-  const hdd_grid* grid() const { return grid_; }
-  int polynomial_order() const { return degree_; }
-
- protected:
-  // a scalar function bound to the device (per-element values uploaded, kept alive with the descriptor)
-  struct Fn {
-    hdd_scalar_fn fn;
-    std::unique_ptr<internal::DeviceArray<double>> pe;
-    explicit Fn(const Problems::ScalarFunction& f)
-    {
-      if (f.kind == HDD_FN_PER_ELEM) pe.reset(new internal::DeviceArray<double>(f.per_element));
-      fn = hdd_scalar_fn{f.kind, f.order, f.c, f.b, f.kx, f.ky, pe ? pe->get() : nullptr};
-    }
-  };
-
-  // swipdg.hh:251-347: affine part = L2Volume(f) + DirichletBoundarySWIPDG(kappa_aff, A, g_D) + L2Face(g_N);
-  // component q = DirichletBoundarySWIPDG(kappa_q, A, g_D) with kappa's coefficient theta_q
-  void assemble_rhs()
-  {
-    const auto& P = problem_;
-    const int64_t size = pattern_->rows;
-    rhs_.size = size;
-    rhs_.coefficients.clear();
-    auto run = [&](const Problems::ScalarFunction* force, const Problems::ScalarFunction* kappa) {
-      auto b = std::make_shared<internal::DeviceArray<double>>(size_t(size) + 1);
-      std::unique_ptr<Fn> f, k, d, nm;
-      if (force && !force->is_zero()) f.reset(new Fn(*force));
-      if (kappa && !P.dirichlet.is_zero()) { k.reset(new Fn(*kappa)); d.reset(new Fn(P.dirichlet)); }
-      if (force && !P.neumann.is_zero()) nm.reset(new Fn(P.neumann));
-      internal::check(hdd_swipdg_rhs(ctx_, &mesh_, f ? &f->fn : nullptr, k ? &k->fn : nullptr, &tensor_,
-                                     d ? &d->fn : nullptr, nm ? &nm->fn : nullptr, &prm_, b->get(), nullptr),
-                      "hdd_swipdg_rhs");
-      internal::hip_check(hipDeviceSynchronize(), "rhs");
-      return b;
-    };
-    const auto& K = P.diffusion_factor;
-    rhs_.affine = run(&P.force, K.has_affine_part ? &K.affine_part : nullptr);
-    if (!P.dirichlet.is_zero())
-      for (int q = 0; q < K.num_components(); ++q) {
-        rhs_.comps.push_back(run(nullptr, &K.components[q]));
-        rhs_.coefficients.push_back(K.coefficients[q]);
-      }
-  }
-
-  std::shared_ptr<const Pattern> volume_pattern()
-  {
-    if (volume_pattern_) return volume_pattern_;
-    auto P = std::make_shared<Pattern>();
-    const int64_t n = linfo_.n_local, own = linfo_.own_end - linfo_.own_begin;
-    std::vector<int32_t> nbrs(size_t(info_.nfaces * n));
-    internal::check(hdd_local_fill(local_, nullptr, nbrs.data(), nullptr, nullptr, nullptr), "hdd_local_fill");
-    internal::check(hdd_dg_pattern_count(0, info_.nb, n, linfo_.own_begin, linfo_.own_end, nbrs.data(), &P->nnz),
-                    "hdd_dg_pattern_count");
-    P->rows = own * info_.nb;
-    P->cols = info_.n_elements * info_.nb;
-    P->row_ptr.resize(size_t(P->rows + 1));
-    P->col.resize(size_t(P->nnz));
-    P->elem_ptr.resize(size_t(own + 1));
-    internal::check(hdd_dg_pattern_fill(0, info_.nb, n, linfo_.own_begin, linfo_.own_end, nbrs.data(), nullptr,
-                                        P->row_ptr.data(), P->col.data(), P->elem_ptr.data()), "hdd_dg_pattern_fill");
-    P->d_row_ptr = internal::DeviceArray<int64_t>(P->row_ptr);
-    P->d_col = internal::DeviceArray<int32_t>(P->col);
-    P->d_elem_ptr = internal::DeviceArray<int64_t>(P->elem_ptr);
-    volume_pattern_ = P;
-    return P;
-  }
-
-  void build_pattern()
-  {
-    auto P = std::make_shared<Pattern>();
-    const int64_t n = linfo_.n_local;
-    std::vector<int32_t> nbrs(size_t(info_.nfaces * n));
-    internal::check(hdd_local_fill(local_, nullptr, nbrs.data(), nullptr, nullptr, nullptr), "hdd_local_fill");
-    internal::check(hdd_dg_pattern_count(info_.nfaces, info_.nb, n, linfo_.own_begin, linfo_.own_end, nbrs.data(),
-                                         &P->nnz), "hdd_dg_pattern_count");
-    const int64_t own = linfo_.own_end - linfo_.own_begin;
-    P->rows = own * info_.nb;
-    P->cols = info_.n_elements * info_.nb;
-    P->row_ptr.resize(size_t(P->rows + 1));
-    P->col.resize(size_t(P->nnz));
-    P->elem_ptr.resize(size_t(own + 1));
-    internal::check(hdd_dg_pattern_fill(info_.nfaces, info_.nb, n, linfo_.own_begin, linfo_.own_end, nbrs.data(),
-                                        nullptr, P->row_ptr.data(), P->col.data(), P->elem_ptr.data()),
-                    "hdd_dg_pattern_fill");
-    P->d_row_ptr = internal::DeviceArray<int64_t>(P->row_ptr);
-    P->d_col = internal::DeviceArray<int32_t>(P->col);
-    P->d_elem_ptr = internal::DeviceArray<int64_t>(P->elem_ptr);
-    pattern_ = P;
-  }
-
   const hdd_grid* grid_;
   Problems::Problem problem_;
+  Layer layer_ = Layer::leaf;
+  int subdomain_ = 0;
+  std::vector<std::string> only_these_products_;
+  int32_t boundary_code_ = HDD_NBR_DIRICHLET;
   hdd_grid_info info_{};
   hdd_local_info linfo_{};
   hdd_ctx* ctx_ = nullptr;
   hdd_local* local_ = nullptr;
+  std::vector<double> coords_, centers_;
+  std::vector<int32_t> nbrs_;
+  std::vector<uint32_t> finfo_;
+  std::vector<int64_t> gid_, cols_;
+  int64_t n_cols_ = 0;
+  detail::ElementView view_;
   std::shared_ptr<Pattern> pattern_;
   std::shared_ptr<const Pattern> volume_pattern_;
-  internal::DeviceArray<double> d_coords_, d_tensor_;
+  internal::DeviceArray<double> d_coords_;
   internal::DeviceArray<int32_t> d_nbrs_;
   internal::DeviceArray<uint32_t> d_finfo_;
+  detail::DeviceTensor tensor_;
   hdd_mesh mesh_{};
-  hdd_tensor_fn tensor_{};
   hdd_swipdg_params prm_{};
   int degree_ = 1;
+  bool purely_neumann_ = false;
   AffinelyDecomposedMatrix matrix_;
   AffinelyDecomposedVector rhs_;
+  std::map<std::string, std::shared_ptr<AffinelyDecomposedMatrix>> products_;
   bool initialized_ = false;
 };
 
-// BlockSWIPDG: the grid must carry the subdomain partition (hdd_grid_create_structured with px, py or
-// hdd_grid_create_from_connectivity with subdomains); its subdomain-major element order IS the block
-// numbering, so the global system matrix is assembled in one pass and the local / coupling operators
-// are its diagonal / off-diagonal blocks.
+namespace detail {
+// face-neighbour subdomains of every subdomain (MsGrid::neighborsOf), one pass over the grid
+inline std::vector<std::set<int>> subdomain_neighbours(const hdd_grid* g, const hdd_grid_info& gi)
+{
+  std::vector<std::set<int>> nb(size_t(gi.n_subdomains));
+  hdd_local* l = nullptr;
+  internal::check(hdd_local_create(g, 0, gi.n_subdomains, &l), "hdd_local_create");
+  hdd_local_info li{};
+  hdd_local_get_info(l, &li);
+  std::vector<int32_t> nbrs(size_t(gi.nfaces * li.n_local)), sd(size_t(li.n_local));
+  const int rc = hdd_local_fill(l, nullptr, nbrs.data(), nullptr, nullptr, sd.data());
+  hdd_local_destroy(l);
+  internal::check(rc, "hdd_local_fill");
+  for (int f = 0; f < gi.nfaces; ++f)
+    for (int64_t e = 0; e < li.n_local; ++e) {
+      const int32_t n = nbrs[size_t(f * li.n_local + e)];
+      if (n >= 0 && sd[size_t(n)] != sd[size_t(e)]) nb[size_t(sd[size_t(e)])].insert(sd[size_t(n)]);
+    }
+  return nb;
+}
+}  // namespace detail
+
+// ------------------------------------------------------------------------------------------------
+// BlockSWIPDG (block-swipdg.hh:177-846): the grid carries the subdomain partition; its subdomain-major
+// element order IS the block numbering, so the global system matrix is assembled in one pass and the local /
+// coupling operators are its diagonal / off-diagonal blocks.  As in the reference, the problem is replaced
+// by ZeroBoundary(problem) and the boundary info by AllDirichlet (block-swipdg.hh:172-176, 230-238).
+// ------------------------------------------------------------------------------------------------
 class BlockSWIPDG : public SWIPDG {
  public:
-  using SWIPDG::SWIPDG;
+  BlockSWIPDG(const grid::Multiscale::Providers::Cube& grid_provider, const Stuff::Common::Configuration& /*ignored*/,
+              const Problems::Problem& prob, const std::vector<std::string>& only_these_products = {},
+              int hip_device = 0)
+    : SWIPDG(grid_provider.grid(), Stuff::Grid::BoundaryInfos::AllDirichlet::default_config(),
+             Problems::ZeroBoundary(prob), Layer::leaf, 0, only_these_products, hip_device),
+      original_problem_(prob), device_(hip_device)
+  {
+    setup();
+  }
+  // convenience: raw grid handle, every product available
+  BlockSWIPDG(const hdd_grid* grid, const Problems::Problem& prob, int hip_device = 0)
+    : SWIPDG(grid, Stuff::Grid::BoundaryInfos::AllDirichlet::default_config(), Problems::ZeroBoundary(prob),
+             Layer::leaf, 0, detail::all_products(), hip_device),
+      original_problem_(prob), device_(hip_device)
+  {
+    setup();
+  }
+
+  static std::string static_id() { return "hdd.linearelliptic.discretizations.containerbased.block-swipdg"; }
+
+  // block-swipdg.hh:262-551 (the two subdomain walks collapse into the one-pass assembly of SWIPDG::init)
+  void init(std::ostream& out = Stuff::Common::devnull(), const std::string& prefix = "")
+  {
+    if (initialized_) return;
+    out << prefix << "walking subdomains for the first time... " << std::flush;
+    const auto t0 = internal::Timer::now();
+    out << "done (took " << internal::seconds_since(t0) << " sek)" << std::endl;
+    out << prefix << "walking subdomains for the second time... " << std::flush;
+    SWIPDG::init();
+    out << "done (took " << internal::seconds_since(t0) << " sek)" << std::endl;
+  }
 
   int num_subdomains() const { return info_.n_subdomains; }
 
+  // block-swipdg.hh:558-565 (MsGrid::neighborsOf, computed once at construction)
   std::vector<int> neighbouring_subdomains(int ss) const
   {
     range_check(ss);
-    std::vector<int> out;
-    for (int nn = 0; nn < num_subdomains(); ++nn) {
-      if (nn == ss) continue;
-      int64_t nnz = 0;
-      internal::check(hdd_block_operator_map(grid_, ss, nn, pattern_->row_ptr.data(), pattern_->col.data(), nullptr,
-                                             nullptr, nullptr, &nnz), "hdd_block_operator_map");
-      if (nnz) out.push_back(nn);
-    }
-    return out;
+    return std::vector<int>(neighbours_[size_t(ss)].begin(), neighbours_[size_t(ss)].end());
   }
 
   AffinelyDecomposedMatrix get_local_operator(int ss) const { return extract(ss, ss); }
 
   AffinelyDecomposedMatrix get_coupling_operator(int ss, int nn) const
   {
-    const auto nb = neighbouring_subdomains(ss);
-    if (std::find(nb.begin(), nb.end(), nn) == nb.end())
-      throw std::out_of_range("Subdomain " + std::to_string(nn) + " is not a neighbour of subdomain " + std::to_string(ss));
+    range_check(ss);
+    if (!neighbours_[size_t(ss)].count(nn))
+      throw Stuff::Exceptions::index_out_of_range("Subdomain " + std::to_string(nn) + " is not a neighbour of subdomain " +
+                                                  std::to_string(ss) + " (call neighbouring_subdomains(" +
+                                                  std::to_string(ss) + ") to find out)!");
     return extract(ss, nn);
+  }
+
+  // block-swipdg.hh:678-685: the local vector of ss (local discretization rhs + boundary contributions) =
+  // the rows of ss of the global rhs, component by component
+  AffinelyDecomposedVector get_local_functional(int ss) const
+  {
+    range_check(ss);
+    const auto& b = rhs();
+    int64_t a, e;
+    internal::check(hdd_grid_subdomain_range(grid_, ss, ss + 1, &a, &e), "hdd_grid_subdomain_range");
+    AffinelyDecomposedVector out;
+    out.size = (e - a) * info_.nb;
+    out.coefficients = b.coefficients;
+    auto slice = [&](const internal::DeviceArray<double>& v) {
+      auto o = std::make_shared<internal::DeviceArray<double>>(size_t(out.size) + 1);
+      internal::hip_check(hipMemcpy(o->get(), v.get() + a * info_.nb, size_t(out.size) * sizeof(double),
+                                    hipMemcpyDeviceToDevice), "get_local_functional");
+      return o;
+    };
+    if (b.affine) out.affine = slice(*b.affine);
+    for (const auto& c : b.comps) out.comps.push_back(slice(*c));
+    return out;
+  }
+
+  // block-swipdg.hh:761-768 / LocalDiscretizationsContainer (106-129): SWIPDG on the local grid part of ss,
+  // AllNeumann, ZeroBoundary(problem), the requested products; created and initialised on first use
+  const SWIPDG& get_local_discretization(int ss) const
+  {
+    if (ss < 0 || ss >= num_subdomains())
+      throw Stuff::Exceptions::index_out_of_range("Given subdomain " + std::to_string(ss) +
+                                                  " too large (has to be smaller than " +
+                                                  std::to_string(num_subdomains()) + "!");
+    auto& d = local_discretizations_[size_t(ss)];
+    if (!d) {
+      d = std::make_shared<SWIPDG>(grid_, Stuff::Grid::BoundaryInfos::AllNeumann::default_config(),
+                                   Problems::ZeroBoundary(original_problem_), Layer::local, ss, only_these_products_,
+                                   device_);
+      d->init();
+    }
+    return *d;
+  }
+
+  // block-swipdg.hh:612-618
+  const AffinelyDecomposedMatrix& get_local_product(int ss, const std::string& id) const
+  {
+    range_check(ss);
+    return get_local_discretization(ss).get_product(id);
   }
 
   std::vector<double> localize_vector(const std::vector<double>& global, int ss) const
   {
     range_check(ss);
-    if (int64_t(global.size()) != num_dofs()) throw std::out_of_range("localize_vector: wrong global size");
+    if (int64_t(global.size()) != num_dofs())
+      throw Stuff::Exceptions::index_out_of_range("The size() of global_vector does not match the ansatz space!");
     int64_t a, b;
     internal::check(hdd_grid_subdomain_range(grid_, ss, ss + 1, &a, &b), "hdd_grid_subdomain_range");
     return std::vector<double>(global.begin() + a * info_.nb, global.begin() + b * info_.nb);
@@ -499,23 +1148,31 @@ class BlockSWIPDG : public SWIPDG {
 
   std::vector<double> globalize_vectors(const std::vector<std::vector<double>>& locals) const
   {
-    if (int(locals.size()) != num_subdomains()) throw std::invalid_argument("globalize_vectors: wrong number of vectors");
+    if (int(locals.size()) != num_subdomains())
+      throw Stuff::Exceptions::wrong_input_given("Given local_vectors has wrong size!");
     std::vector<double> out;
     for (int ss = 0; ss < num_subdomains(); ++ss) {
       int64_t a, b;
       internal::check(hdd_grid_subdomain_range(grid_, ss, ss + 1, &a, &b), "hdd_grid_subdomain_range");
-      if (int64_t(locals[ss].size()) != (b - a) * info_.nb) throw std::invalid_argument("globalize_vectors: wrong local size");
-      out.insert(out.end(), locals[ss].begin(), locals[ss].end());
+      if (int64_t(locals[size_t(ss)].size()) != (b - a) * info_.nb)
+        throw Stuff::Exceptions::wrong_input_given("Given local_vectors[" + std::to_string(ss) + "] has wrong size!");
+      out.insert(out.end(), locals[size_t(ss)].begin(), locals[size_t(ss)].end());
     }
     return out;
   }
 
  private:
+  void setup()
+  {
+    neighbours_ = detail::subdomain_neighbours(grid_, info_);
+    local_discretizations_.resize(size_t(info_.n_subdomains));
+  }
+
   void range_check(int ss) const
   {
     if (ss < 0 || ss >= num_subdomains())
-      throw std::out_of_range("0 <= ss < num_subdomains() = " + std::to_string(num_subdomains()) + " is not true for ss = " +
-                              std::to_string(ss) + "!");
+      throw Stuff::Exceptions::index_out_of_range("0 <= ss < num_subdomains() = " + std::to_string(num_subdomains()) +
+                                                  " is not true for ss = " + std::to_string(ss) + "!");
   }
 
   AffinelyDecomposedMatrix extract(int ss, int nn) const
@@ -555,6 +1212,233 @@ class BlockSWIPDG : public SWIPDG {
     internal::hip_check(hipDeviceSynchronize(), "extract");
     return out;
   }
+
+  Problems::Problem original_problem_;
+  int device_ = 0;
+  std::vector<std::set<int>> neighbours_;
+  mutable std::vector<std::shared_ptr<SWIPDG>> local_discretizations_;
+};
+
+// ------------------------------------------------------------------------------------------------
+// ShardedBlockSWIPDG: BlockSWIPDG over one process / thread per GPU.  Rank r owns the subdomains
+// [n_sub r / nranks, n_sub (r+1) / nranks) and assembles their rows (owner-computes: A_ss and A_ss,nn are
+// written by the owner of ss, block-swipdg.hh:355-382) through hdd_block_assemble_sharded; the ghost columns
+// of the per-element coefficients arrive through the face halo of `comm`.  Host work and memory are
+// O(owned + ghost elements): the structured grid is implicit and coefficients are localized per rank.
+// ------------------------------------------------------------------------------------------------
+class ShardedBlockSWIPDG {
+ public:
+  ShardedBlockSWIPDG(const grid::Multiscale::Providers::Cube& grid_provider,
+                     const Stuff::Common::Configuration& /*ignored*/, const Problems::Problem& prob,
+                     Parallel::Communicator comm, int rank, int nranks, int hip_device = 0)
+    : ShardedBlockSWIPDG(grid_provider.grid(), prob, std::move(comm), rank, nranks, hip_device) {}
+
+  ShardedBlockSWIPDG(const hdd_grid* grid, const Problems::Problem& prob, Parallel::Communicator comm, int rank,
+                     int nranks, int hip_device = 0)
+    : grid_(grid), problem_(Problems::ZeroBoundary(prob)), comm_(std::move(comm)), device_(hip_device)
+  {
+    if (prob.diffusion_tensor_parametric) throw NotImplemented("The diffusion tensor must not be parametric!");
+    if (prob.diffusion_tensor_empty) throw Stuff::Exceptions::wrong_input_given("The diffusion tensor must not be empty!");
+    internal::check(hdd_grid_get_info(grid, &info_), "hdd_grid_get_info");
+    internal::check(hdd_ctx_create(hip_device, &ctx_), "hdd_ctx_create");
+    internal::check(hdd_shard_create(ctx_, grid, nranks, rank, nullptr, &shard_), "hdd_shard_create");
+    internal::check(hdd_shard_get_info(shard_, &sinfo_), "hdd_shard_get_info");
+    internal::check(hdd_shard_mesh(shard_, &mesh_), "hdd_shard_mesh");
+    if (sinfo_.n_peers > 0 && !comm_.get())
+      throw Stuff::Exceptions::wrong_input_given("ShardedBlockSWIPDG: this rank has halo peers, a Communicator is needed");
+  }
+  ~ShardedBlockSWIPDG()
+  {
+    if (shard_) hdd_shard_destroy(shard_);
+    if (ctx_) hdd_ctx_destroy(ctx_);
+  }
+  ShardedBlockSWIPDG(const ShardedBlockSWIPDG&) = delete;
+  ShardedBlockSWIPDG& operator=(const ShardedBlockSWIPDG&) = delete;
+
+  // block-swipdg.hh:262-551 for the owned subdomains: pattern of the owned rows (global columns), every
+  // diffusion-factor component through the sharded step (one halo exchange per call), the owned rows of the
+  // right-hand side (element-local)
+  void init(std::ostream& out = Stuff::Common::devnull(), const std::string& prefix = "")
+  {
+    if (initialized_) return;
+    out << prefix << "assembling subdomains [" << sinfo_.s_begin << ", " << sinfo_.s_end << ") of "
+        << info_.n_subdomains << " on rank " << sinfo_.rank << "... " << std::flush;
+    const auto t0 = internal::Timer::now();
+    const int64_t n = sinfo_.n_local;
+    centers_.assign(size_t(info_.dim * n), 0.0);
+    gid_.assign(size_t(n), 0);
+    internal::check(hdd_shard_centers(shard_, centers_.data()), "hdd_shard_centers");
+    internal::check(hdd_shard_global_ids(shard_, gid_.data()), "hdd_shard_global_ids");
+    view_ = detail::ElementView{n, sinfo_.own_begin, sinfo_.own_end, info_.dim, centers_.data(), gid_.data(),
+                                info_.n_elements, /*halo_ghosts=*/true};
+    auto P = std::make_shared<Pattern>();
+    P->rows = sinfo_.n_rows;
+    P->cols = sinfo_.n_cols;
+    P->nnz = sinfo_.nnz;
+    P->d_row_ptr = internal::DeviceArray<int64_t>(size_t(P->rows + 1));
+    P->d_col = internal::DeviceArray<int32_t>(size_t(P->nnz));
+    P->d_elem_ptr = internal::DeviceArray<int64_t>(size_t(sinfo_.own_end - sinfo_.own_begin + 1));
+    internal::check(hdd_shard_pattern_fill(ctx_, shard_, P->d_row_ptr.get(), P->d_col.get(), P->d_elem_ptr.get(),
+                                           nullptr), "hdd_shard_pattern_fill");
+    P->row_ptr = P->d_row_ptr.download();
+    P->col = P->d_col.download();
+    pattern_ = P;
+    tensor_ = detail::DeviceTensor(problem_.diffusion_tensor, view_);
+    prm_ = detail::swipdg_params(detail::degree_of(info_), info_.dim);
+    const auto& K = problem_.diffusion_factor;
+    kappas_.clear();
+    for (const auto& c : K.components) kappas_.emplace_back(c, view_);
+    if (K.has_affine_part) kappas_.emplace_back(K.affine_part, view_);
+    matrix_ = AffinelyDecomposedMatrix();
+    matrix_.pattern = pattern_;
+    matrix_.ctx = ctx_;
+    matrix_.coefficients = K.coefficients;
+    for (size_t q = 0; q < kappas_.size(); ++q) {
+      auto v = std::make_shared<internal::DeviceArray<double>>(size_t(P->nnz) + 1);
+      if (q < K.components.size()) matrix_.comps.push_back(v);
+      else matrix_.affine = v;
+    }
+    assemble();   // the halo fills every ghost column (NaN until then)
+    assemble_rhs();
+    internal::hip_check(hipDeviceSynchronize(), "init");
+    out << "done (took " << internal::seconds_since(t0) << "s)" << std::endl;
+    initialized_ = true;
+  }
+
+  // one sharded LHS step for every component: pack -> exchange -> interior tiles -> unpack -> boundary tiles
+  // (hdd_block_assemble_sharded); flags HDD_SHARD_* (NO_HALO once the ghost coefficients are current)
+  void assemble(uint32_t flags = 0, hipStream_t stream = nullptr)
+  {
+    std::vector<hdd_scalar_fn> k;
+    std::vector<double*> v;
+    for (size_t q = 0; q < kappas_.size(); ++q) {
+      k.push_back(kappas_[q].fn);
+      v.push_back(q < matrix_.comps.size() ? matrix_.comps[q]->get() : matrix_.affine->get());
+    }
+    const hdd_csr pat = pattern_->csr();
+    internal::check(hdd_block_assemble_sharded(ctx_, shard_, comm_.get(), k.data(), int32_t(k.size()), &tensor_.fn, &prm_,
+                                               &pat, v.data(), flags, stream), "hdd_block_assemble_sharded");
+  }
+
+  const AffinelyDecomposedMatrix& system_matrix() const { ready(); return matrix_; }   // owned rows, global columns
+  const AffinelyDecomposedVector& rhs() const { ready(); return rhs_; }                // owned rows
+  int num_subdomains() const { return info_.n_subdomains; }
+  std::pair<int, int> owned_subdomains() const { return {sinfo_.s_begin, sinfo_.s_end}; }
+  int64_t first_owned_dof() const { return sinfo_.global_first * info_.nb; }
+  int64_t num_dofs() const { return info_.n_elements * info_.nb; }
+  const hdd_shard_info& shard_info() const { return sinfo_; }
+  const Pattern& pattern() const { ready(); return *pattern_; }
+  hdd_ctx* context() const { return ctx_; }
+
+  // the rows of an owned subdomain ss restricted to the columns of subdomain nn (nn == ss: local operator),
+  // as AffinelyDecomposedMatrix in local numbering on both sides (block-swipdg.hh:625-676)
+  AffinelyDecomposedMatrix get_operator_block(int ss, int nn) const
+  {
+    ready();
+    if (ss < sinfo_.s_begin || ss >= sinfo_.s_end)
+      throw Stuff::Exceptions::index_out_of_range("subdomain " + std::to_string(ss) + " is not owned by this rank");
+    if (nn < 0 || nn >= info_.n_subdomains) throw Stuff::Exceptions::index_out_of_range("bad subdomain");
+    int64_t a, b, c, d;
+    internal::check(hdd_grid_subdomain_range(grid_, ss, ss + 1, &a, &b), "range");
+    internal::check(hdd_grid_subdomain_range(grid_, nn, nn + 1, &c, &d), "range");
+    const int nb = info_.nb;
+    const int64_t r0 = (a - sinfo_.global_first) * nb, r1 = (b - sinfo_.global_first) * nb;
+    auto P = std::make_shared<Pattern>();
+    P->rows = r1 - r0;
+    P->cols = (d - c) * nb;
+    P->row_ptr.assign(1, 0);
+    std::vector<int64_t> src;
+    for (int64_t r = r0; r < r1; ++r) {
+      for (int64_t q = pattern_->row_ptr[size_t(r)]; q < pattern_->row_ptr[size_t(r + 1)]; ++q) {
+        const int64_t col = pattern_->col[size_t(q)];
+        if (col < c * nb || col >= d * nb) continue;
+        P->col.push_back(int32_t(col - c * nb));
+        src.push_back(q);
+      }
+      P->row_ptr.push_back(int64_t(P->col.size()));
+    }
+    P->nnz = int64_t(P->col.size());
+    if (P->nnz == 0 && nn != ss)
+      throw Stuff::Exceptions::index_out_of_range("Subdomain " + std::to_string(nn) + " is not a neighbour of subdomain " +
+                                                  std::to_string(ss));
+    P->d_row_ptr = internal::DeviceArray<int64_t>(P->row_ptr);
+    P->d_col = internal::DeviceArray<int32_t>(P->col);
+    internal::DeviceArray<int64_t> d_src(src);
+    AffinelyDecomposedMatrix out;
+    out.pattern = P;
+    out.ctx = ctx_;
+    out.coefficients = matrix_.coefficients;
+    auto gather = [&](const internal::DeviceArray<double>& v) {
+      auto o = std::make_shared<internal::DeviceArray<double>>(size_t(P->nnz) + 1);
+      internal::check(hdd_gather_values(ctx_, v.get(), d_src.get(), P->nnz, o->get(), nullptr), "hdd_gather_values");
+      return o;
+    };
+    if (matrix_.affine) out.affine = gather(*matrix_.affine);
+    for (const auto& q : matrix_.comps) out.comps.push_back(gather(*q));
+    internal::hip_check(hipDeviceSynchronize(), "get_operator_block");
+    return out;
+  }
+  AffinelyDecomposedMatrix get_local_operator(int ss) const { return get_operator_block(ss, ss); }
+  AffinelyDecomposedMatrix get_coupling_operator(int ss, int nn) const
+  {
+    if (nn == ss) throw Stuff::Exceptions::index_out_of_range("a subdomain is not its own neighbour");
+    return get_operator_block(ss, nn);
+  }
+
+ private:
+  void ready() const
+  {
+    if (!initialized_)
+      throw Stuff::Exceptions::you_are_using_this_wrong("The user has to call init() before calling any other method!");
+  }
+
+  // owned rows of the block right-hand side (ZeroBoundary: L2Volume(force) only; element-local, no halo)
+  void assemble_rhs()
+  {
+    const auto& F = problem_.force;
+    rhs_ = AffinelyDecomposedVector();
+    rhs_.size = sinfo_.n_rows;
+    auto run = [&](const Problems::ScalarFunction* f, const Problems::ScalarFunction* kappa) {
+      auto b = std::make_shared<internal::DeviceArray<double>>(size_t(rhs_.size) + 1);
+      detail::DeviceFn fd, kd, dd;
+      if (f) fd = detail::DeviceFn(*f, view_);
+      const Problems::ScalarFunction zero = Problems::ScalarFunction::constant(0.0);
+      if (kappa) { kd = detail::DeviceFn(*kappa, view_); dd = detail::DeviceFn(zero, view_); }
+      internal::check(hdd_swipdg_rhs(ctx_, &mesh_, f ? &fd.fn : nullptr, kappa ? &kd.fn : nullptr, &tensor_.fn,
+                                     kappa ? &dd.fn : nullptr, nullptr, &prm_, b->get(), nullptr), "hdd_swipdg_rhs");
+      return b;
+    };
+    const auto& K = problem_.diffusion_factor;
+    for (int q = 0; q < F.num_components(); ++q) {
+      rhs_.comps.push_back(run(&F.components[size_t(q)], nullptr));
+      rhs_.coefficients.push_back(F.coefficients[size_t(q)]);
+    }
+    rhs_.affine = run(F.has_affine_part ? &F.affine_part : nullptr, K.has_affine_part ? &K.affine_part : nullptr);
+    for (int q = 0; q < K.num_components(); ++q) {   // kappa_q x (g_D = 0): registered as in swipdg.hh:300-311
+      rhs_.comps.push_back(run(nullptr, &K.components[size_t(q)]));
+      rhs_.coefficients.push_back(K.coefficients[size_t(q)]);
+    }
+  }
+
+  const hdd_grid* grid_;
+  Problems::Problem problem_;
+  Parallel::Communicator comm_;
+  int device_ = 0;
+  hdd_grid_info info_{};
+  hdd_ctx* ctx_ = nullptr;
+  hdd_shard* shard_ = nullptr;
+  hdd_shard_info sinfo_{};
+  hdd_mesh mesh_{};
+  std::vector<double> centers_;
+  std::vector<int64_t> gid_;
+  detail::ElementView view_;
+  std::shared_ptr<Pattern> pattern_;
+  detail::DeviceTensor tensor_;
+  std::vector<detail::DeviceFn> kappas_;
+  hdd_swipdg_params prm_{};
+  AffinelyDecomposedMatrix matrix_;
+  AffinelyDecomposedVector rhs_;
+  bool initialized_ = false;
 };
 
 }  // namespace Discretizations

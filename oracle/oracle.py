@@ -122,6 +122,30 @@ def checkerboard(centers, lower, upper, nxc, nyc, values):
     return values[cy * nxc + cx]
 
 
+def indicator(points, boxes):
+    """dune-stuff Indicator (playground/functions/indicator.hh, third-party: restated, unverifiable here) as
+    problems/spe10.hh:144, 157 use it: per entity, the value of the first closed box [lower, upper] that
+    contains the entity centre, 0 if none.  points [n][2], boxes [k][5] = lx, ly, ux, uy, value."""
+    out = np.zeros(points.shape[0])
+    done = np.zeros(points.shape[0], bool)
+    for lx, ly, ux, uy, v in np.asarray(boxes, np.float64).reshape(-1, 5):
+        m = ~done & (points[:, 0] >= lx) & (points[:, 0] <= ux) & (points[:, 1] >= ly) & (points[:, 1] <= uy)
+        out[m] = v
+        done |= m
+    return out
+
+
+def spe10_channel_boxes():
+    """The parametric SPE10 channel of testcases/spe10.hh:38-251 (105 boxes, channel_boundary_layer = 0, so
+    Indicator functions: problems/spe10.hh:213-218) and the three force boxes (testcases/spe10.hh:31-37),
+    from the committed fixture tests/golden/spe10_parametric_channel.json (make_spe10_channel.py).
+    Returned as (channel [105][5], force [3][5])."""
+    import json
+    path = os.path.join(os.path.dirname(_HERE), "tests", "golden", "spe10_parametric_channel.json")
+    d = json.load(open(path))
+    return np.array(d["channel"], np.float64), np.array(d["force"], np.float64)
+
+
 def spe10_synthetic_permeability(nxc=100, nyc=20, seed=10):
     """Stand-in for perm_case1.dat (absent): log10 k ~ U(-3, 3) on the 100x20 Model1 checkerboard."""
     rng = np.random.default_rng(seed)

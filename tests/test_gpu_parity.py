@@ -373,6 +373,21 @@ def test_affine_lincomb(ctx, nnz, n_comp, n_s, stride_pad):
     assert np.max(np.abs(got - ref)) <= 1e-14 * np.max(np.abs(ref)) * n_comp
 
 
+def test_affine_lincomb_odd_nnz_default_output(ctx):
+    """out=None with odd nnz: the front-end pads the row stride (the kernel stores 16-byte pairs) and
+    returns the (n_s, nnz) view."""
+    torch = _torch()
+    rng = np.random.default_rng(3)
+    nnz = 1001
+    comps = [torch.from_numpy(rng.standard_normal(nnz)).cuda() for _ in range(2)]
+    theta = rng.uniform(-1.0, 1.0, (5, 2))
+    out = H.affine_lincomb(ctx, comps, theta)
+    torch.cuda.synchronize()
+    assert tuple(out.shape) == (5, nnz)
+    ref = theta @ np.stack([c.cpu().numpy() for c in comps])
+    assert np.max(np.abs(out.cpu().numpy() - ref)) <= 1e-14 * np.max(np.abs(ref)) * 2
+
+
 @pytest.mark.parametrize("et,smooth", [(H.SIMPLEX, False), (H.SIMPLEX, True), (H.CUBE, False)])
 def test_penalty_exponent_beta(ctx, et, smooth):
     """beta != 1 (penalty |F|^-beta; 2d default 1/(d-1) = 1 is taken inline, other values through the

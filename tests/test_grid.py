@@ -143,3 +143,31 @@ def test_subdomain_range_errors():
         with pytest.raises(H.HddError, match="status 5"):
             g.local(s0, s1)
     assert g.local(1, 2).n_own == 32
+
+
+def test_connectivity_rejects_non_parallelogram_quads():
+    """HDD_CUBE meshes carry Q1 on parallelograms only (affine geometry from vertices 0, 1, 2): a
+    trapezoid must be refused, not assembled wrongly."""
+    coords = np.array([[0.0, 0.0], [1.0, 0.0], [0.0, 1.0], [1.0, 1.0]])
+    H.Grid.from_connectivity(H.CUBE, coords, np.array([[0, 1, 2, 3]]))          # square: accepted
+    sheared = coords + np.array([[0.0, 0.0], [0.0, 0.0], [0.3, 0.0], [0.3, 0.0]])
+    H.Grid.from_connectivity(H.CUBE, sheared, np.array([[0, 1, 2, 3]]))         # parallelogram: accepted
+    trapezoid = coords.copy()
+    trapezoid[3] = [0.8, 1.0]
+    with pytest.raises(H.HddError, match="parallelogram"):
+        H.Grid.from_connectivity(H.CUBE, trapezoid, np.array([[0, 1, 2, 3]]))
+
+
+def test_indicator_first_closed_box():
+    """hdd_indicator (dune-stuff Indicator at the element barycentre, problems/spe10.hh:144, 157) against the
+    oracle-side numpy twin: first closed box containing the point, 0 outside."""
+    rng = np.random.default_rng(5)
+    pts = rng.uniform(0.0, 5.0, (2, 1000))
+    pts[1] *= 0.2
+    boxes = np.array([[0.95, 0.30, 1.10, 0.45, 2000.0], [3.00, 0.75, 3.15, 0.90, -1000.0],
+                      [4.25, 0.25, 4.40, 0.40, -1000.0], [0.0, 0.0, 2.5, 0.5, 7.0]])
+    pts[:, :4] = [[1.0, 3.1, 4.3, 1.1], [0.4, 0.8, 0.3, 0.45]]     # inside / on the closed edge
+    got = H.indicator(pts, boxes)
+    ref = O.indicator(pts.T, boxes)
+    assert np.array_equal(got, ref)
+    assert got[0] == 2000.0 and got[1] == -1000.0 and got[2] == -1000.0 and got[3] == 2000.0
