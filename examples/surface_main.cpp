@@ -6,6 +6,7 @@
 #include <cmath>
 #include <cstdio>
 #include <fstream>
+#include <iostream>
 #include <string>
 #include <vector>
 
@@ -130,6 +131,123 @@ int main(int argc, char** argv)
     dump(out + "/hex_rhs.bin", sw.rhs().affine_part());
   }
   hdd_grid_destroy(g);
+
+  // 5. the reference's constructor / init surface (swipdg.hh:159-163, 206, 216-217, 486; base.hh:272-291)
+  namespace S = Dune::Stuff;
+  {
+    S::Grid::Providers::Cube provider(HDD_SIMPLEX, {-1.0, -1.0}, {1.0, 1.0}, {8, 8}, 1);   // levels 8^2, 16^2
+    Discretizations::SWIPDG sw(provider, S::Grid::BoundaryInfos::AllDirichlet::default_config(), Problems::ESV2007(),
+                               1, {"l2", "penalty"});
+    sw.init(std::cout, "  [swipdg] ");
+    std::string avail;
+    for (const auto& id : sw.available_products()) avail += id + " ";
+    std::printf("available products: %s\n", avail.c_str());
+    try {
+      sw.get_product("h1_semi");
+    } catch (const S::Exceptions::wrong_input_given& e) {
+      std::printf("not requested: %s\n", e.what());
+    }
+    dump(out + "/lvl1_row_ptr.bin", sw.pattern().row_ptr);
+    dump(out + "/lvl1_affine.bin", sw.system_matrix().affine_part());
+    dump(out + "/lvl1_rhs.bin", sw.rhs().affine_part());
+    Discretizations::SWIPDG bare(provider, S::Grid::BoundaryInfos::AllDirichlet::default_config(), Problems::ESV2007());
+    try {
+      bare.system_matrix();
+    } catch (const S::Exceptions::you_are_using_this_wrong& e) {
+      std::printf("before init: %s\n", e.what());
+    }
+    bare.init();
+    try {
+      bare.get_product("l2");
+    } catch (const S::Exceptions::you_are_using_this_wrong& e) {
+      std::printf("no products: %s\n", e.what());
+    }
+    try {
+      Discretizations::SWIPDG bad_level(provider, S::Grid::BoundaryInfos::AllDirichlet::default_config(),
+                                        Problems::ESV2007(), 5);
+    } catch (const S::Exceptions::index_out_of_range& e) {
+      std::printf("bad level: %s\n", e.what());
+    }
+  }
+
+  // 6. BlockSWIPDG on a multiscale provider: local discretization / product / functional (block-swipdg.hh:612-685, 761)
+  {
+    Dune::grid::Multiscale::Providers::Cube ms(HDD_SIMPLEX, {-1.0, -1.0}, {1.0, 1.0}, {16, 16}, {2, 2});
+    Discretizations::BlockSWIPDG block(ms, S::Common::Configuration(), Problems::ESV2007(), {"l2", "h1_semi"});
+    block.init(std::cout, "  [block] ");
+    const auto& L0 = block.get_local_discretization(0);
+    std::printf("local discretization 0: layer local %d, dofs %lld, purely neumann %d\n",
+                int(L0.layer() == Discretizations::SWIPDG::Layer::local), (long long)L0.num_dofs(),
+                int(L0.purely_neumann()));
+    dump(out + "/ld0_row_ptr.bin", L0.pattern().row_ptr);
+    dump(out + "/ld0_col.bin", L0.pattern().col);
+    dump(out + "/ld0_affine.bin", L0.system_matrix().affine_part());
+    const auto& P0 = block.get_local_product(0, "l2");
+    dump(out + "/lp0_row_ptr.bin", P0.pattern->row_ptr);
+    dump(out + "/lp0_l2.bin", P0.affine_part());
+    const auto F0 = block.get_local_functional(0);
+    dump(out + "/lf0.bin", F0.affine_part());
+    dump(out + "/lf0_from_ld.bin", L0.rhs().affine_part());
+    std::printf("local functional 0: size %lld components %d\n", (long long)F0.size, F0.num_components());
+    try {
+      block.get_local_discretization(4);
+    } catch (const S::Exceptions::index_out_of_range& e) {
+      std::printf("local discretization 4 rejected\n");
+    }
+  }
+
+  // 7. parametric SPE10 Model1 (problems/spe10.hh:160-172): A = checkerboard, kappa = (1 + channel) - mu channel,
+  //    force = Indicator; channel / force boxes read from <outdir>/spe10_boxes.bin when present
+  {
+    std::vector<double> perm(2000);
+    for (int i = 0; i < 2000; ++i) perm[size_t(i)] = std::pow(10.0, -3.0 + 6.0 * std::fmod(0.618033988749895 * i, 1.0));
+    std::vector<std::array<double, 5>> channel, forces;
+    std::ifstream bf(out + "/spe10_boxes.bin", std::ios::binary);
+    if (bf) {
+      double hdr[2];
+      bf.read(reinterpret_cast<char*>(hdr), sizeof(hdr));
+      for (int k = 0; k < int(hdr[0]) + int(hdr[1]); ++k) {
+        std::array<double, 5> b;
+        bf.read(reinterpret_cast<char*>(b.data()), sizeof(b));
+        (k < int(hdr[0]) ? channel : forces).push_back(b);
+      }
+    }
+    dump(out + "/spe10_perm.bin", perm);
+    S::Grid::Providers::Cube provider(HDD_SIMPLEX, {0.0, 0.0}, {5.0, 1.0}, {100, 20});
+    Discretizations::SWIPDG sw(provider, S::Grid::BoundaryInfos::AllDirichlet::default_config(),
+                               Problems::Spe10Model1(perm, channel, forces, true), 0, {"elliptic"});
+    sw.init();
+    const auto& A = sw.system_matrix();
+    std::printf("spe10 parametric %d components %d coefficient %s rhs components %d coefficient %s\n",
+                int(A.parametric()), A.num_components(), A.coefficient(0).expression().c_str(),
+                sw.rhs().num_components(), sw.rhs().coefficient(0).expression().c_str());
+    dump(out + "/spe10_affine.bin", A.affine_part());
+    dump(out + "/spe10_comp0.bin", A.component(0));
+    dump(out + "/spe10_frozen_0.5.bin", A.freeze_parameter(0.5));
+    dump(out + "/spe10_rhs.bin", sw.rhs().affine_part());
+    dump(out + "/spe10_rhs_comp0.bin", sw.rhs().component(0));
+    const auto& E = sw.get_product("elliptic");
+    dump(out + "/spe10_elliptic_comp0.bin", E.component(0));
+  }
+
+  // 8. parametric right-hand side with kappa_p x g_D,q cross terms (swipdg.hh:257-330): OS2014 kappa, g_D(mu) =
+  //    sin(..) + mu cos(..) cos(..), g_N = 0, f = 1 on 8x8 Kuhn with AllDirichlet
+  {
+    S::Grid::Providers::Cube provider(HDD_SIMPLEX, {-1.0, -1.0}, {1.0, 1.0}, {8, 8});
+    auto p = Problems::OS2014();
+    p.dirichlet = Problems::ScalarFunction::sinusoid(0.25, 0.5, 1.0, 2.0, 3);
+    p.dirichlet.register_component(Problems::ScalarFunction::cos_product(0.7, 1.5, 0.5, 0.0, 3),
+                                   Dune::HDD::LinearElliptic::Pymor::ParameterFunctional("mu", "mu", 1.0));
+    Discretizations::SWIPDG sw(provider, S::Grid::BoundaryInfos::AllDirichlet::default_config(), p);
+    sw.init();
+    const auto& b = sw.rhs();
+    std::string coefs;
+    for (int q = 0; q < b.num_components(); ++q) coefs += b.coefficient(q).expression() + ";";
+    std::printf("parametric rhs components %d coefficients %s\n", b.num_components(), coefs.c_str());
+    dump(out + "/prhs_affine.bin", b.affine_part());
+    for (int q = 0; q < b.num_components(); ++q) dump(out + "/prhs_comp" + std::to_string(q) + ".bin", b.component(q));
+    dump(out + "/prhs_frozen_0.7.bin", b.freeze_parameter(0.7));
+  }
   std::printf("surface ok\n");
   return 0;
 }

@@ -23,11 +23,23 @@ def test_surface_example_is_built():
     assert os.access(EXE, os.X_OK), "examples/bin/surface_main missing: run make -C dune-hdd_amd"
 
 
+@pytest.fixture(scope="module")
+def surface_run(tmp_path_factory):
+    """one run of examples/surface_main; the parametric SPE10 channel / force boxes (testcases/spe10.hh) are
+    handed over as a binary file"""
+    d = str(tmp_path_factory.mktemp("surface"))
+    ch, fo = O.spe10_channel_boxes()
+    np.concatenate([[len(ch), len(fo)], ch.ravel(), fo.ravel()]).astype(np.float64).tofile(
+        os.path.join(d, "spe10_boxes.bin"))
+    r = subprocess.run([EXE, d], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    return r, d
+
+
 @pytest.mark.gpu
-def test_cpp_surface_against_oracle():
-    with tempfile.TemporaryDirectory() as d:
-        r = subprocess.run([EXE, d], capture_output=True, text=True, timeout=300)
-        assert r.returncode == 0, r.stdout + r.stderr
+def test_cpp_surface_against_oracle(surface_run):
+    r, d = surface_run
+    if True:
         assert "roundtrip 1" in r.stdout and "coupling(0,3) rejected" in r.stdout
         assert "rejected: The diffusion tensor must not be parametric!" in r.stdout
         assert "os2014 parametric 1 components 1" in r.stdout
@@ -90,3 +102,119 @@ def test_cpp_surface_against_oracle():
     assert compare_rows(orp, hval, oval, 1e-12)[1]
     ob = O.qp_rhs_swipdg(q, force=O.esv2007_force(3))
     assert np.max(np.abs(hrhs - ob)) <= 1e-12 * np.max(np.abs(ob))
+
+
+def _ld(d, n, t=np.float64):
+    return np.fromfile(os.path.join(d, n + ".bin"), dtype=t)
+
+
+@pytest.mark.gpu
+def test_cpp_reference_ctor_init_products(surface_run):
+    """SWIPDG(grid_provider, boundary_cfg, problem, level, only_these_products) + init(out, prefix)
+    (swipdg.hh:159-163, 206-217, 486): level 1 of the provider, the timing line, only the requested products
+    available, the reference's error paths (base.hh:282-291, 370-377)."""
+    r, d = surface_run
+    out = r.stdout
+    assert "  [swipdg] assembling... done (took " in out
+    assert "available products: l2 penalty" in out
+    assert "not requested: Product 'h1_semi' not available!" in out
+    assert "before init: The user has to call init() before calling any other method!" in out
+    assert "no products: Do not call get_product() if available_products() is empty!" in out
+    assert "bad level: level 5 not in [0, 2)" in out
+    assert "  [block] walking subdomains for the first time... done" in out
+    og = O.Grid(*O.kuhn_grid(16, 16, (-1, -1), (1, 1)))
+    rp, col, val = O.assemble(og, O.scalar(), O.tensor(), O.params())
+    assert np.array_equal(_ld(d, "lvl1_row_ptr", np.int64), rp)
+    assert compare_rows(rp, _ld(d, "lvl1_affine"), val, 1e-12)[1]
+    b = O.rhs_swipdg(og, force=O.esv2007_force())
+    assert np.max(np.abs(_ld(d, "lvl1_rhs") - b)) <= 1e-12 * np.max(np.abs(b))
+
+
+@pytest.mark.gpu
+def test_cpp_block_local_discretization_product_functional(surface_run):
+    """BlockSWIPDG::get_local_discretization(0) (block-swipdg.hh:761-768: SWIPDG on the local grid part,
+    AllNeumann, ZeroBoundary), get_local_product(0, "l2") (612-618) and get_local_functional(0) (678-685)
+    against the oracle on the subdomain's elements with an all-Neumann boundary."""
+    r, d = surface_run
+    assert "local discretization 0: layer local 1, dofs 384, purely neumann 1" in r.stdout
+    assert "local functional 0: size 384 components 0" in r.stdout
+    assert "local discretization 4 rejected" in r.stdout
+    g = H.Grid.structured(H.SIMPLEX, 16, 16, (-1, -1), (1, 1), px=2, py=2)
+    pc, pev, psd = g.connectivity()
+    a0, b0 = g.subdomain_range(0, 1)
+    sg = O.Grid(O.SIMPLEX, pc, pev[a0:b0])
+    neu = O.params(boundary=O.BOUNDARY_NEUMANN)
+    rp, col, val = O.assemble(sg, O.scalar(), O.tensor(), neu)
+    assert np.array_equal(_ld(d, "ld0_row_ptr", np.int64), rp) and np.array_equal(_ld(d, "ld0_col", np.int32), col)
+    assert compare_rows(rp, _ld(d, "ld0_affine"), val, 1e-12)[1]
+    prp, _, pval = O.product(sg, O.PRODUCT_L2, prm=neu)
+    assert np.array_equal(_ld(d, "lp0_row_ptr", np.int64), prp)
+    assert compare_rows(prp, _ld(d, "lp0_l2"), pval, 1e-12)[1]
+    b = O.rhs_swipdg(sg, force=O.esv2007_force(), prm=neu)
+    lf = _ld(d, "lf0")
+    assert np.max(np.abs(lf - b)) <= 1e-12 * np.max(np.abs(b))
+    assert np.array_equal(lf, _ld(d, "lf0_from_ld"))     # the local discretization's rhs, bit for bit
+
+
+@pytest.mark.gpu
+def test_cpp_parametric_spe10(surface_run):
+    """Parametric SPE10 Model1 (problems/spe10.hh:160-172, channel / force boxes of testcases/spe10.hh:31-251):
+    affine part (1 + channel) and component channel with theta = -1.0*mu, the rhs with the kappa_1 x g_D,aff
+    component, the elliptic product; GPU vs oracle at 1e-12.  freeze_parameter(0.5) is the reference's
+    theta-lincomb; it equals a frozen-mu assembly exactly on rows whose element and neighbours lie outside the
+    channel (inside, the penalty's kappa^- kappa^+ is assembled per component, as the reference does)."""
+    r, d = surface_run
+    assert "spe10 parametric 1 components 1 coefficient -1.0*mu rhs components 1 coefficient -1.0*mu" in r.stdout
+    et, c, ev = O.kuhn_grid(100, 20, (0, 0), (5, 1))
+    og = O.Grid(et, c, ev)
+    cen = O.element_centers(c, ev)
+    ch, fo = O.spe10_channel_boxes()
+    chan = O.indicator(cen, ch)
+    k_aff, k_1 = 1.0 + chan, chan
+    perm = _ld(d, "spe10_perm")
+    A = O.tensor(O.TENSOR_ISO_PER_ELEM, per_elem=O.checkerboard(cen, (0, 0), (5, 1), 100, 20, perm))
+    pe = lambda v: O.scalar(O.FN_PER_ELEM, per_elem=np.ascontiguousarray(v))
+    rp, col, va = O.assemble(og, pe(k_aff), A, O.params())
+    _, _, v1 = O.assemble(og, pe(k_1), A, O.params())
+    assert (k_1 != 0).sum() > 100
+    assert compare_rows(rp, _ld(d, "spe10_affine"), va, 1e-12)[1]
+    assert compare_rows(rp, _ld(d, "spe10_comp0"), v1, 1e-12)[1]
+    fr = _ld(d, "spe10_frozen_0.5")
+    assert compare_rows(rp, fr, va - 0.5 * v1, 1e-12)[1]
+    _, _, vf = O.assemble(og, pe(k_aff - 0.5 * k_1), A, O.params())
+    nb, _ = og.neighbors()
+    quiet = (k_1 == 0) & np.all((nb < 0) | (k_1[np.maximum(nb, 0)] == 0), axis=1)
+    rows = np.repeat(quiet, 3)
+    for i in np.nonzero(rows)[0][::37]:
+        s = slice(rp[i], rp[i + 1])
+        assert np.array_equal(fr[s], vf[s]) or np.max(np.abs(fr[s] - vf[s])) <= 1e-12 * np.max(np.abs(vf[s]))
+    assert not np.allclose(fr, vf)        # the channel rows differ: component-wise penalty
+    b = O.rhs_swipdg(og, force=pe(O.indicator(cen, fo)), kappa=pe(k_aff), A=A, dirichlet=O.scalar(O.FN_CONST, 0.0))
+    assert np.max(np.abs(_ld(d, "spe10_rhs") - b)) <= 1e-12 * np.max(np.abs(b))
+    assert not _ld(d, "spe10_rhs_comp0").any()       # kappa_1 x (g_D = 0)
+    _, _, e1 = O.product(og, O.PRODUCT_ELLIPTIC, kappa=pe(k_1), A=A)
+    assert np.max(np.abs(_ld(d, "spe10_elliptic_comp0") - e1)) <= 1e-12 * np.max(np.abs(e1))
+
+
+@pytest.mark.gpu
+def test_cpp_parametric_rhs_cross_terms(surface_run):
+    """swipdg.hh:251-356 component structure: with kappa = kappa_aff + mu kappa_1 and g_D = g_aff + mu g_1 the
+    rhs holds affine = L2Volume(f) + Dirichlet(kappa_aff, g_aff) and the components Dirichlet(kappa_aff, g_1)
+    [mu], Dirichlet(kappa_1, g_aff) [mu], Dirichlet(kappa_1, g_1) [(mu)*(mu)]; b(0.7) = sum theta b."""
+    r, d = surface_run
+    assert "parametric rhs components 3 coefficients mu;mu;(mu)*(mu);" in r.stdout
+    og = O.Grid(*O.kuhn_grid(8, 8, (-1, -1), (1, 1)))
+    kx, ky = 4 * math.pi, 2 * math.pi
+    k_aff = O.scalar(O.FN_SINUSOID, 1.0, 0.75, kx, ky, order=3)
+    k_1 = O.scalar(O.FN_SINUSOID, 0.0, -0.75, kx, ky, order=3)
+    g_aff = O.scalar(O.FN_SINUSOID, 0.25, 0.5, 1.0, 2.0, order=3)
+    g_1 = O.scalar(O.FN_COS_PRODUCT, 0.7, 0.0, 1.5, 0.5, order=3)
+    ref = [O.rhs_swipdg(og, force=O.scalar(O.FN_CONST, 1.0), kappa=k_aff, dirichlet=g_aff),
+           O.rhs_swipdg(og, kappa=k_aff, dirichlet=g_1), O.rhs_swipdg(og, kappa=k_1, dirichlet=g_aff),
+           O.rhs_swipdg(og, kappa=k_1, dirichlet=g_1)]
+    got = [_ld(d, "prhs_affine")] + [_ld(d, "prhs_comp%d" % q) for q in range(3)]
+    for g_, r_ in zip(got, ref):
+        assert np.max(np.abs(g_ - r_)) <= 1e-12 * np.max(np.abs(r_))
+    mu = 0.7
+    frozen = ref[0] + mu * ref[1] + mu * ref[2] + mu * mu * ref[3]
+    assert np.max(np.abs(_ld(d, "prhs_frozen_0.7") - frozen)) <= 1e-12 * np.max(np.abs(frozen))
