@@ -81,7 +81,11 @@ def cpu_baseline(nx_full, ny, target_s, cube=False):
     import oracle as O
     perm = O.spe10_synthetic_permeability()
     lower = (0.0, 0.0)
-    threads = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()))
+    # The OpenMP leg uses this job's CPU share, not the node: the GPU box exports OMP_NUM_THREADS (16 = the
+    # host cores allotted to one GPU of the node; nproc / the affinity set show the whole machine's CPUs there,
+    # and the pool rules forbid sizing worker pools by them).  Without OMP_NUM_THREADS: the affinity set.
+    affinity = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    threads = max(1, int(os.environ.get("OMP_NUM_THREADS") or 0) or affinity)
 
     def run(nxs, reps=5, omp=0):
         upper = (5.0 * nxs / nx_full, 1.0)
@@ -111,8 +115,10 @@ def cpu_baseline(nx_full, ny, target_s, cube=False):
                        "workload = %d DoFs (%.3f s per assembly)"
                        % (nxs, ny, "Q1 quad" if cube else "Kuhn", "C4" if cube else "C2", dofs, t),
                 omp_value=dofs / t_omp, omp_cores=threads,
-                omp_sample="owner-computes OpenMP variant of the same integrands, %d threads, same strip, "
-                           "median of 5 (%.3f s per assembly)" % (threads, t_omp),
+                omp_sample="owner-computes OpenMP variant of the same integrands, %d threads (OMP_NUM_THREADS=%s: "
+                           "the job's host-core share; %d CPUs in the affinity set), same strip, median of 5 "
+                           "(%.3f s per assembly)" % (threads, os.environ.get("OMP_NUM_THREADS", "unset"), affinity,
+                                                      t_omp),
                 cpu_model=_cpu_model(), host_cpus=os.cpu_count())
 
 

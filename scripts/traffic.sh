@@ -14,4 +14,5 @@ for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 200 rocprofv3 --kernel-trace --pmc $c -d "$OUT/cal_$c" -o run --output-format csv -- "$ROOT/scripts/microbench/stream" > "$OUT/cal_$c.log" 2>&1 || exit $?
   timeout -k 10 300 rocprofv3 --kernel-trace --pmc $c -d "$OUT/bench_$c" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline > "$OUT/bench_$c.log" 2>&1 || exit $?
 done
+cd "$ROOT" && python3 scripts/traffic_summary.py "${1:-r01}" > "$OUT/summary.log" 2>&1 || exit $?
 echo traffic passes ok

@@ -2,9 +2,12 @@
 bench-readable profiles/traffic_<tag>.json: HBM bytes per launch of the hot kernel, corrected with the
 factors measured on calibration kernels of known byte counts (MI355X_MICROARCH.md HBM section: FETCH_SIZE
 reads 1/2 of wide coalesced reads on gfx950; other widths must be calibrated)."""
-import csv, glob, json, os, sys, collections
+import csv, glob, hashlib, json, os, sys, collections
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
+LIB = os.path.join(ROOT, "dune-hdd_amd", "lib", "libhdd_amd.so")
+# the build the counters were taken on (bench.py reports traffic only for the same build id)
+build_id = hashlib.sha256(open(LIB, "rb").read()).hexdigest()[:16]
 src = os.path.join(ROOT, "gpurun_out", "traffic_" + tag)
 
 def per_kernel(path, counter):
@@ -34,12 +37,12 @@ fetch_kb, write_kb = med(bf[kname]), med([v for k, vs in bw.items() if "swipdg" 
 # the kernel's reads are 8-byte lanes (coalesced SoA) + gathers; its writes are 16-byte lanes
 read_bytes = fetch_kb * KB * cal.get("read_8B_lane", 2.0)
 write_bytes = write_kb * KB * cal.get("write_16B_lane", 1.0)
-out = dict(workload="spe10_swipdg_p1_kuhn_3200x640", kernel=kname, fetch_size_kb=fetch_kb, write_size_kb=write_kb,
+out = dict(workload="spe10_swipdg_p1_kuhn_3200x640", build_id=build_id, kernel=kname, fetch_size_kb=fetch_kb, write_size_kb=write_kb,
            calibration_factors=cal, read_bytes=read_bytes, write_bytes=write_bytes,
            hbm_bytes_per_launch=read_bytes + write_bytes,
            note="FETCH_SIZE/WRITE_SIZE medians over the profiled launches; factors = known bytes / counter "
                 "bytes measured on stream.hip kernels of the same lane width")
 os.makedirs(os.path.join(ROOT, "profiles", tag), exist_ok=True)
 json.dump(out, open(os.path.join(ROOT, "profiles", tag, "traffic.json"), "w"), indent=1)
-json.dump(out, open(os.path.join(ROOT, "profiles", "traffic_%s.json" % tag), "w"), indent=1)
+json.dump(out, open(os.path.join(src, "traffic.json"), "w"), indent=1)   # gpurun_out travels back from the box
 print(json.dumps(out, indent=1))
