@@ -172,7 +172,8 @@ int main(int argc, char** argv)
 
   // 6. BlockSWIPDG on a multiscale provider: local discretization / product / functional (block-swipdg.hh:612-685, 761)
   {
-    Dune::grid::Multiscale::Providers::Cube ms(HDD_SIMPLEX, {-1.0, -1.0}, {1.0, 1.0}, {16, 16}, {2, 2});
+    Dune::grid::Multiscale::Providers::Cube ms(HDD_SIMPLEX, {-1.0, -1.0}, {1.0, 1.0}, {16, 16}, {2, 2},
+                                               /*oversampling_layers=*/1);
     Discretizations::BlockSWIPDG block(ms, S::Common::Configuration(), Problems::ESV2007(), {"l2", "h1_semi"});
     block.init(std::cout, "  [block] ");
     const auto& L0 = block.get_local_discretization(0);
@@ -193,6 +194,22 @@ int main(int argc, char** argv)
       block.get_local_discretization(4);
     } catch (const S::Exceptions::index_out_of_range& e) {
       std::printf("local discretization 4 rejected\n");
+    }
+    // block-swipdg.hh:783-817: subdomain 0 + one ring of face neighbours, Dirichlet / Neumann boundary
+    for (const char* bt : {"dirichlet", "neumann"}) {
+      const auto& O = block.get_oversampled_discretization(0, bt);
+      dump(out + "/os0_" + std::string(bt) + "_row_ptr.bin", O.pattern().row_ptr);
+      dump(out + "/os0_" + std::string(bt) + "_col.bin", O.pattern().col);
+      dump(out + "/os0_" + std::string(bt) + "_affine.bin", O.system_matrix().affine_part());
+      dump(out + "/os0_" + std::string(bt) + "_rhs.bin", O.rhs().affine_part());
+    }
+    const auto ids = block.oversampled_elements(0);
+    dump(out + "/os0_ids.bin", ids);
+    std::printf("oversampled 0: %zu elements (layers %d)\n", ids.size(), block.oversampling_layers());
+    try {
+      block.get_oversampled_discretization(0, "robin");
+    } catch (const S::Exceptions::wrong_input_given& e) {
+      std::printf("oversampled robin rejected\n");
     }
   }
 

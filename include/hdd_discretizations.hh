@@ -153,8 +153,11 @@ namespace Providers {
 // subdomain-major element order is the block numbering
 class Cube {
  public:
+  // oversampling_layers: the local_oversampled grid part of a subdomain is the subdomain plus this many
+  // rings of face-neighbour elements (testcases/base.hh:169, "oversampling_layers", default 0)
   Cube(int elem_type, std::array<double, 2> lower, std::array<double, 2> upper, std::array<int, 2> num_elements,
-       std::array<int, 2> num_partitions)
+       std::array<int, 2> num_partitions, int oversampling_layers = 0)
+    : layers_(oversampling_layers)
   {
     hdd_structured_desc d{elem_type, num_elements[0], num_elements[1], num_partitions[0], num_partitions[1],
                           HDD_BOUNDARY_ALL_DIRICHLET, 0, {lower[0], lower[1]}, {upper[0], upper[1]}};
@@ -172,9 +175,11 @@ class Cube {
     hdd_grid_get_info(g_.get(), &gi);
     return gi.n_subdomains;
   }
+  int oversampling_layers() const { return layers_; }
 
  private:
   std::shared_ptr<hdd_grid> g_;
+  int layers_ = 0;
 };
 }  // namespace Providers
 }  // namespace Multiscale
@@ -675,9 +680,20 @@ class SWIPDG {
     : SWIPDG(grid, Stuff::Common::Configuration(), problem, Layer::leaf, 0, detail::all_products(), hip_device,
              /*grid_boundary=*/true) {}
 
+  // a discretization on a grid of its own whose elements are a subset of a parent grid's (parent_ids: parent
+  // element id of every element; per-element functions given in the parent's numbering are read through it)
+  SWIPDG(std::shared_ptr<hdd_grid> subset_grid, std::vector<int64_t> parent_ids, int64_t n_parent,
+         const Stuff::Common::Configuration& bound_inf_cfg, const Problems::Problem& problem,
+         const std::vector<std::string>& only_these_products, int hip_device = 0)
+    : SWIPDG(subset_grid.get(), bound_inf_cfg, problem, Layer::leaf, 0, only_these_products, hip_device, false,
+             &parent_ids, n_parent)
+  {
+    owned_grid_ = std::move(subset_grid);
+  }
+
   SWIPDG(const hdd_grid* grid, const Stuff::Common::Configuration& bound_inf_cfg, const Problems::Problem& problem,
          Layer layer, int subdomain, const std::vector<std::string>& only_these_products, int hip_device = 0,
-         bool grid_boundary = false)
+         bool grid_boundary = false, const std::vector<int64_t>* parent_ids = nullptr, int64_t n_parent = 0)
     : grid_(grid), problem_(problem), layer_(layer), subdomain_(subdomain), only_these_products_(only_these_products)
   {
     // swipdg.hh:172-176
@@ -703,6 +719,14 @@ class SWIPDG {
     internal::check(hdd_local_get_info(local_, &linfo_), "hdd_local_get_info");
     degree_ = detail::degree_of(info_);
     build_view();
+    if (parent_ids) {   // per-element data of the parent grid: look it up through the parent ids
+      if (int64_t(parent_ids->size()) != info_.n_elements)
+        throw Stuff::Exceptions::wrong_input_given("parent_ids: one id per element expected");
+      parent_gid_.resize(gid_.size());
+      for (size_t e = 0; e < gid_.size(); ++e) parent_gid_[e] = (*parent_ids)[size_t(gid_[e])];
+      view_.gid = parent_gid_.data();
+      view_.n_global = n_parent;
+    }
     build_pattern();
   }
   virtual ~SWIPDG()
@@ -987,7 +1011,8 @@ class SWIPDG {
   std::vector<double> coords_, centers_;
   std::vector<int32_t> nbrs_;
   std::vector<uint32_t> finfo_;
-  std::vector<int64_t> gid_, cols_;
+  std::vector<int64_t> gid_, cols_, parent_gid_;
+  std::shared_ptr<hdd_grid> owned_grid_;   // subset grids (oversampled discretizations)
   int64_t n_cols_ = 0;
   detail::ElementView view_;
   std::shared_ptr<Pattern> pattern_;
@@ -1041,7 +1066,7 @@ class BlockSWIPDG : public SWIPDG {
               int hip_device = 0)
     : SWIPDG(grid_provider.grid(), Stuff::Grid::BoundaryInfos::AllDirichlet::default_config(),
              Problems::ZeroBoundary(prob), Layer::leaf, 0, only_these_products, hip_device),
-      original_problem_(prob), device_(hip_device)
+      original_problem_(prob), device_(hip_device), oversampling_layers_(grid_provider.oversampling_layers())
   {
     setup();
   }
@@ -1129,6 +1154,60 @@ class BlockSWIPDG : public SWIPDG {
     return *d;
   }
 
+  // block-swipdg.hh:783-817: SWIPDG on the local_oversampled grid part of ss (the subdomain plus
+  // oversampling_layers rings of face neighbours), boundary "dirichlet" or "neumann" on the whole boundary of
+  // that grid part, ZeroBoundary(problem), the requested products; created and initialised on first use
+  const SWIPDG& get_oversampled_discretization(int ss, const std::string& boundary_value_type) const
+  {
+    if (ss < 0 || ss >= num_subdomains())
+      throw Stuff::Exceptions::index_out_of_range("Given subdomain " + std::to_string(ss) +
+                                                  " too large (has to be smaller than " +
+                                                  std::to_string(num_subdomains()) + "!");
+    Stuff::Common::Configuration cfg;
+    if (boundary_value_type == "dirichlet") cfg = Stuff::Grid::BoundaryInfos::AllDirichlet::default_config();
+    else if (boundary_value_type == "neumann") cfg = Stuff::Grid::BoundaryInfos::AllNeumann::default_config();
+    else
+      throw Stuff::Exceptions::wrong_input_given(
+          "Unknown boundary_value_type given (has to be dirichlet or neumann): " + boundary_value_type);
+    auto& d = oversampled_[{ss, boundary_value_type}];
+    if (!d) {
+      std::vector<int64_t> ids = oversampled_elements(ss);
+      d = std::make_shared<SWIPDG>(subset_grid(ids), ids, info_.n_elements, cfg, Problems::ZeroBoundary(original_problem_),
+                                   only_these_products_, device_);
+      d->init();
+    }
+    return *d;
+  }
+  int oversampling_layers() const { return oversampling_layers_; }
+  void set_oversampling_layers(int layers)
+  {
+    oversampling_layers_ = layers;
+    oversampled_.clear();
+  }
+  // parent element ids of the local_oversampled grid part of ss, ascending
+  std::vector<int64_t> oversampled_elements(int ss) const
+  {
+    int64_t a, b;
+    internal::check(hdd_grid_subdomain_range(grid_, ss, ss + 1, &a, &b), "hdd_grid_subdomain_range");
+    std::vector<char> in(size_t(info_.n_elements), 0);
+    std::vector<int64_t> front;
+    for (int64_t e = a; e < b; ++e) { in[size_t(e)] = 1; front.push_back(e); }
+    const int64_t n = linfo_.n_local;   // the leaf view holds every element, local == global
+    for (int layer = 0; layer < oversampling_layers_; ++layer) {
+      std::vector<int64_t> next;
+      for (int64_t e : front)
+        for (int f = 0; f < info_.nfaces; ++f) {
+          const int32_t nb = nbrs_[size_t(f * n + e)];
+          if (nb >= 0 && !in[size_t(nb)]) { in[size_t(nb)] = 1; next.push_back(nb); }
+        }
+      front.swap(next);
+    }
+    std::vector<int64_t> ids;
+    for (int64_t e = 0; e < info_.n_elements; ++e)
+      if (in[size_t(e)]) ids.push_back(e);
+    return ids;
+  }
+
   // block-swipdg.hh:612-618
   const AffinelyDecomposedMatrix& get_local_product(int ss, const std::string& id) const
   {
@@ -1213,10 +1292,30 @@ class BlockSWIPDG : public SWIPDG {
     return out;
   }
 
+  // a standalone grid (vertex ids of the parent) of the given parent elements, in their order
+  std::shared_ptr<hdd_grid> subset_grid(const std::vector<int64_t>& ids) const
+  {
+    if (info_.dim != 2) throw NotImplemented("oversampled discretizations: 2d grids");
+    std::vector<double> vc(size_t(2 * info_.n_vertices));
+    std::vector<int32_t> ev(size_t(info_.nvpe * info_.n_elements)), sub;
+    internal::check(hdd_grid_connectivity(grid_, vc.data(), ev.data(), nullptr), "hdd_grid_connectivity");
+    std::vector<int32_t> sev;
+    sev.reserve(ids.size() * size_t(info_.nvpe));
+    for (int64_t e : ids)
+      for (int k = 0; k < info_.nvpe; ++k) sev.push_back(ev[size_t(e * info_.nvpe + k)]);
+    hdd_grid* g = nullptr;
+    internal::check(hdd_grid_create_from_connectivity(info_.elem_type, info_.n_vertices, vc.data(), int64_t(ids.size()),
+                                                      sev.data(), nullptr, 1, HDD_BOUNDARY_ALL_DIRICHLET, &g),
+                    "hdd_grid_create_from_connectivity");
+    return std::shared_ptr<hdd_grid>(g, hdd_grid_destroy);
+  }
+
   Problems::Problem original_problem_;
   int device_ = 0;
+  int oversampling_layers_ = 0;
   std::vector<std::set<int>> neighbours_;
   mutable std::vector<std::shared_ptr<SWIPDG>> local_discretizations_;
+  mutable std::map<std::pair<int, std::string>, std::shared_ptr<SWIPDG>> oversampled_;
 };
 
 // ------------------------------------------------------------------------------------------------

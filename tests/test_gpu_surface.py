@@ -218,3 +218,32 @@ def test_cpp_parametric_rhs_cross_terms(surface_run):
     mu = 0.7
     frozen = ref[0] + mu * ref[1] + mu * ref[2] + mu * mu * ref[3]
     assert np.max(np.abs(_ld(d, "prhs_frozen_0.7") - frozen)) <= 1e-12 * np.max(np.abs(frozen))
+
+
+@pytest.mark.gpu
+def test_cpp_block_oversampled_discretization(surface_run):
+    """BlockSWIPDG::get_oversampled_discretization(0, "dirichlet" / "neumann") (block-swipdg.hh:783-817) with
+    oversampling_layers = 1 (testcases/base.hh:169): SWIPDG on subdomain 0 plus one ring of face neighbours,
+    the whole boundary of that grid part Dirichlet / Neumann, ZeroBoundary(ESV2007) -- against the oracle on
+    the same element set."""
+    r, d = surface_run
+    ids = _ld(d, "os0_ids", np.int64)
+    assert "oversampled 0: %d elements (layers 1)" % ids.size in r.stdout and "oversampled robin rejected" in r.stdout
+    g = H.Grid.structured(H.SIMPLEX, 16, 16, (-1, -1), (1, 1), px=2, py=2)
+    pc, pev, psd = g.connectivity()
+    a0, b0 = g.subdomain_range(0, 1)
+    assert ids.size > b0 - a0 and np.array_equal(ids[ids < b0][:b0 - a0], np.arange(a0, b0))
+    # one ring: every added element shares a face with subdomain 0
+    loc = g.local()
+    nb = loc.neighbors.T
+    added = ids[(ids < a0) | (ids >= b0)]
+    assert all(np.any((nb[e] >= a0) & (nb[e] < b0)) for e in added)
+    sg = O.Grid(O.SIMPLEX, pc, pev[ids])
+    for bt, kind in (("dirichlet", O.BOUNDARY_DIRICHLET), ("neumann", O.BOUNDARY_NEUMANN)):
+        prm = O.params(boundary=kind)
+        rp, col, val = O.assemble(sg, O.scalar(), O.tensor(), prm)
+        assert np.array_equal(_ld(d, "os0_%s_row_ptr" % bt, np.int64), rp)
+        assert np.array_equal(_ld(d, "os0_%s_col" % bt, np.int32), col)
+        assert compare_rows(rp, _ld(d, "os0_%s_affine" % bt), val, 1e-12)[1]
+        b = O.rhs_swipdg(sg, force=O.esv2007_force(), prm=prm)
+        assert np.max(np.abs(_ld(d, "os0_%s_rhs" % bt) - b)) <= 1e-12 * np.max(np.abs(b))
