@@ -12,6 +12,7 @@
 #include <cstdint>
 #include <cstdlib>
 #include <string>
+#include <vector>
 
 #include "hdd.h"
 #include "../host/hdd_internal.hh"
@@ -25,6 +26,8 @@ struct hdd_ctx {
   int n_cu = 256;           // hipDeviceAttributeMultiprocessorCount
   int debug_flags = 0;      // HDD_DEBUG_FLAGS: profiling ablations only (0 in production)
   int wgcu = 0;             // HDD_P1_WGCU: tiles-per-CU sweep override (0: the policy's measured value)
+  int q3g_reps = 0;         // HDD_Q3G_REPS: workgroups per (XCD, row quad) of the p=3 GEMM kernel (0: by CU count)
+  double* q3g_tab = nullptr;   // p=3 reference matrices [Q3G_K][4096], uploaded on first use
 };
 
 int hdd::ctx_device(const hdd_ctx* ctx) { return ctx ? ctx->device : 0; }
@@ -69,6 +72,7 @@ extern "C" int hdd_ctx_create(int hip_device, hdd_ctx** out)
     c->n_cu = cus;
   if (const char* df = getenv("HDD_DEBUG_FLAGS")) c->debug_flags = atoi(df);
   if (const char* w = getenv("HDD_P1_WGCU")) c->wgcu = std::max(0, atoi(w));
+  if (const char* r = getenv("HDD_Q3G_REPS")) c->q3g_reps = std::max(0, atoi(r));
   *out = c;
   return HDD_OK;
 }
@@ -76,6 +80,7 @@ extern "C" int hdd_ctx_create(int hip_device, hdd_ctx** out)
 extern "C" void hdd_ctx_destroy(hdd_ctx* ctx)
 {
   if (ctx && ctx->ws) (void)hipFree(ctx->ws);
+  if (ctx && ctx->q3g_tab) (void)hipFree(ctx->q3g_tab);
   delete ctx;
 }
 
@@ -193,10 +198,24 @@ static int assemble_hex(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_fn* ka
       for (int q = 0; q < 2; ++q) lagrange_1d(deg, r, double(q), &a.tab.Le[r][q], &a.tab.De[r][q]);
     }
     if (hex_uses_records(a, deg, nq1v, nq1f)) {
+      const int64_t n_own = std::max<int64_t>(1, m->own_end - m->own_begin);
       void* ws = nullptr;
-      e = ctx_workspace(ctx, size_t(std::max<int64_t>(1, m->own_end - m->own_begin)) * HEX_REC * sizeof(double), &ws);
+      e = ctx_workspace(ctx, hex_q3_workspace_doubles(n_own) * sizeof(double), &ws);
       if (e != hipSuccess) return hip_fail(e, "hdd_swipdg_assemble: workspace");
       a.ws = static_cast<double*>(ws);
+      a.q3g_coef = a.ws + n_own * HEX_REC;
+      a.q3g_meta = reinterpret_cast<int64_t*>(a.q3g_coef + (n_own + 15) / 16 * 16 * Q3G_K);
+      if (!ctx->q3g_tab) {   // element-independent: the 1D tables are fixed for (p, nq1v, nq1f) = (3, 3, 4)
+        std::vector<double> tab(size_t(Q3G_K) * 4096);
+        hex_q3g_reference_tables(a.tab, tab.data());
+        e = hipMalloc(&ctx->q3g_tab, tab.size() * sizeof(double));
+        if (e != hipSuccess) return hip_fail(e, "hdd_swipdg_assemble: reference matrices");
+        e = hipMemcpy(ctx->q3g_tab, tab.data(), tab.size() * sizeof(double), hipMemcpyHostToDevice);
+        if (e != hipSuccess) return hip_fail(e, "hdd_swipdg_assemble: reference matrices");
+      }
+      a.q3g_tab = ctx->q3g_tab;
+      // 4 row waves per workgroup, 128 workgroups per replica: 2 replicas per 128 CUs (8 waves per CU)
+      a.q3g_reps = ctx->q3g_reps > 0 ? ctx->q3g_reps : std::max(1, ctx->n_cu / 64);
     }
     bool supported = false;
     e = launch_hex(a, deg, nq1v, nq1f, static_cast<hipStream_t>(stream), &supported);

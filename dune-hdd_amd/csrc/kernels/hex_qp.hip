@@ -750,13 +750,237 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   }
 }
 
+// ---------------------------------------------------------------------------------------------------
+// p = 3, piecewise-constant data: the local matrices as a dense GEMM over reference matrices.
+//
+// With kappa and A constant on an affine hexahedron, every integrand is a coefficient (element data) times a
+// product of 1D factors, and the reference's tensor Gauss rules factorise the same way, so each block is a
+// linear combination of element-independent 64 x 64 reference matrices (sums over the SAME quadrature
+// points the reference uses: 3^3 volume, 4^2 face points):
+//   self block  S = sum_ab M_ab V_ab                                (M = |det J| kappa J^-1 A J^-T, 6 terms)
+//                 + sum_f [ ce_f I_V^f - ca_f sum_a cm_f,a (I_N^{f,a} + I_N^{f,a}^T) ]   (4 terms per face)
+//   face block  E_f = -ce_f J_V^f - cb_f sum_a cp_f,a J_N^{f,a} + ca_f sum_a cm_f,a J_N'^{f,a}   (7 terms)
+// (cm = J^-1 A^- n, cp = J_+^-1 A^+ n, ca / cb / ce = |F| omega^- kappa^- / |F| omega^+ kappa^+ / the
+// penalty, as in the p=3 records; V_ab, I_V, I_N, J_V, J_N, J_N' = Kronecker products of the 1D Gauss sums
+// of L L, L' L', L L', L' L and the trace values L(0|1), L'(0|1)).  So, for 16 elements at once,
+//   [16 elements x 32 terms] x [32 terms x 4096 entries]  (self)    [16 x 8] x [8 x 4096] per face block,
+// a dense f64 GEMM on v_mfma_f64_16x16x4_f64 with the reference matrices as the B operand.  A wave owns one
+// matrix row i: its B fragments (row i of every reference matrix, 80 values per lane) stay in registers for
+// the whole launch; it walks 16-element groups, reading each group's coefficient fragments (A) and writing
+// row i of the 7 blocks of its 16 elements (16 lanes = 128 contiguous bytes per element row).  320 MFMAs per
+// element instead of 1200, no operand generation on the VALU: the kernel is bound by the 229 KB per
+// element of value stores.  XCD-aware: the 64 row waves of a group run on one XCD (its L2 holds the
+// group's coefficients).
+// ---------------------------------------------------------------------------------------------------
+size_t hex_q3_workspace_doubles(int64_t n_own)
+{
+  const int64_t groups = (n_own + 15) / 16;
+  return size_t(n_own) * HEX_REC + size_t(groups) * 16 * Q3G_K + size_t(n_own) * 2;
+}
+
+void hex_q3g_reference_tables(const HexTables& t, double* out)
+{
+  const int nv = 3, nf = 4;   // the reference's Gauss points per direction at p = 3 (orders 4 and 6)
+  double Mm[4][4], Dd[4][4], Ca[4][4], Cb[4][4], Mf[4][4], Cfa[4][4], Cfb[4][4];
+  for (int x = 0; x < 4; ++x)
+    for (int y = 0; y < 4; ++y) {
+      Mm[x][y] = Dd[x][y] = Ca[x][y] = Cb[x][y] = Mf[x][y] = Cfa[x][y] = Cfb[x][y] = 0.0;
+      for (int q = 0; q < nv; ++q) {
+        Mm[x][y] += t.wv[q] * t.Lv[x][q] * t.Lv[y][q];
+        Dd[x][y] += t.wv[q] * t.Dv[x][q] * t.Dv[y][q];
+        Ca[x][y] += t.wv[q] * t.Lv[x][q] * t.Dv[y][q];   // derivative on the ansatz function
+        Cb[x][y] += t.wv[q] * t.Dv[x][q] * t.Lv[y][q];   // derivative on the test function
+      }
+      for (int q = 0; q < nf; ++q) {
+        Mf[x][y] += t.wf[q] * t.Lf[x][q] * t.Lf[y][q];
+        Cfa[x][y] += t.wf[q] * t.Lf[x][q] * t.Df[y][q];
+        Cfb[x][y] += t.wf[q] * t.Df[x][q] * t.Lf[y][q];
+      }
+    }
+  for (int i = 0; i < 64; ++i)
+    for (int j = 0; j < 64; ++j) {
+      const int ii[3] = {i & 3, (i >> 2) & 3, i >> 4}, jj[3] = {j & 3, (j >> 2) & 3, j >> 4};
+      auto T = [&](int k) -> double& { return out[size_t(k) * 4096 + size_t(i) * 64 + j]; };
+      auto mm = [&](int d) { return Mm[ii[d]][jj[d]]; };
+      auto ca = [&](int d) { return Ca[ii[d]][jj[d]]; };
+      auto cb = [&](int d) { return Cb[ii[d]][jj[d]]; };
+      T(0) = Dd[ii[0]][jj[0]] * mm(1) * mm(2);
+      T(1) = mm(0) * Dd[ii[1]][jj[1]] * mm(2);
+      T(2) = mm(0) * mm(1) * Dd[ii[2]][jj[2]];
+      T(3) = (cb(0) * ca(1) + ca(0) * cb(1)) * mm(2);
+      T(4) = (cb(0) * ca(2) + ca(0) * cb(2)) * mm(1);
+      T(5) = mm(0) * (cb(1) * ca(2) + ca(1) * cb(2));
+      for (int f = 0; f < 6; ++f) {
+        const int af = f >> 1, sd = f & 1;
+        const int t1 = af == 0 ? 1 : 0, t2 = af == 2 ? 1 : 2;
+        auto mf = [&](int d) { return Mf[ii[d]][jj[d]]; };
+        const double mt = mf(t1) * mf(t2);
+        // trace factors on my side (sd) and on the neighbour's (1 - sd)
+        const double Lti = t.Le[ii[af]][sd], Ltj = t.Le[jj[af]][sd], Dti = t.De[ii[af]][sd];
+        const double Lnj = t.Le[jj[af]][1 - sd], Dnj = t.De[jj[af]][1 - sd];
+        // I_N^{f,a}(x, y) = sum phi_x d_a phi_y over the face (x, y basis indices)
+        auto IN = [&](int a, const int* xi, const int* yi) {
+          const double Lx = t.Le[xi[af]][sd], Ly = t.Le[yi[af]][sd], Dy = t.De[yi[af]][sd];
+          if (a == af) return Lx * Dy * Mf[xi[t1]][yi[t1]] * Mf[xi[t2]][yi[t2]];
+          const int o = a == t1 ? t2 : t1;
+          return Lx * Ly * Cfa[xi[a]][yi[a]] * Mf[xi[o]][yi[o]];
+        };
+        T(6 + 4 * f) = Lti * Ltj * mt;
+        for (int a = 0; a < 3; ++a) T(7 + 4 * f + a) = IN(a, ii, jj) + IN(a, jj, ii);
+        const int kb = 32 + 8 * f;
+        T(kb) = Lti * Lnj * mt;
+        for (int a = 0; a < 3; ++a) {
+          if (a == af) {
+            T(kb + 1 + a) = Lti * Dnj * mt;
+            T(kb + 4 + a) = Dti * Lnj * mt;
+          } else {
+            const int o = a == t1 ? t2 : t1;
+            T(kb + 1 + a) = Lti * Lnj * Cfa[ii[a]][jj[a]] * mf(o);
+            T(kb + 4 + a) = Lti * Lnj * Cfb[ii[a]][jj[a]] * mf(o);
+          }
+        }
+        T(kb + 7) = 0.0;
+      }
+      T(30) = T(31) = 0.0;
+    }
+}
+
+// element records -> the GEMM's coefficient fragments [group][term][16] and row-block layout per element
+__global__ __launch_bounds__(256) void hex_q3g_coef_kernel(HexArgs a, int64_t n_groups)
+{
+  const int64_t n_own = a.own_end - a.own_begin;
+  const int64_t k = blockIdx.x * int64_t(blockDim.x) + threadIdx.x;   // element slot (groups padded to 16)
+  if (k >= n_groups * 16) return;
+  double* C = a.q3g_coef + (k >> 4) * (Q3G_K * 16) + (k & 15);
+  auto put = [&](int t, double v) { C[t * 16] = v; };
+  if (k >= n_own) {
+    for (int t = 0; t < Q3G_K; ++t) put(t, 0.0);
+    return;
+  }
+  const double* R = a.ws + k * HEX_REC;
+  put(0, R[2]); put(1, R[5]); put(2, R[7]); put(3, R[3]); put(4, R[4]); put(5, R[6]);   // M00 M11 M22 M01 M02 M12
+  put(30, 0.0); put(31, 0.0);
+  const int64_t hdr = d2i(R[1]);
+  uint64_t info = uint64_t(hdr & 0xff) | (uint64_t((hdr >> 32) & 0xff) << 8);   // nblk | self position
+#pragma unroll
+  for (int f = 0; f < 6; ++f) {
+    const double* F = R + 8 + 10 * f;
+    const int64_t fk = d2i(F[9]);
+    const int kind = int32_t(fk & 0xffffffff);
+    const bool inner = kind > 0, neu = kind == HDD_NBR_NEUMANN;
+    const double ca = F[6], cb = F[7], ce = F[8];
+    put(6 + 4 * f, neu ? 0.0 : ce);
+    for (int d = 0; d < 3; ++d) put(7 + 4 * f + d, neu ? 0.0 : -ca * F[d]);
+    const int kb = 32 + 8 * f;
+    put(kb, inner ? -ce : 0.0);
+    for (int d = 0; d < 3; ++d) {
+      put(kb + 1 + d, inner ? -cb * F[3 + d] : 0.0);
+      put(kb + 4 + d, inner ? ca * F[d] : 0.0);
+    }
+    put(kb + 7, 0.0);
+    info |= uint64_t(inner ? ((fk >> 32) & 0xff) : 0xff) << (16 + 8 * f);
+  }
+  a.q3g_meta[2 * k] = d2i(R[0]);
+  a.q3g_meta[2 * k + 1] = int64_t(info);
+}
+
+__global__ __launch_bounds__(256) void hex_q3g_kernel(HexArgs a, int64_t n_groups)
+{
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int b = blockIdx.x;
+  const int x = b & 7, kq = b >> 3, rq = kq & 15, rep = kq >> 4;   // XCD, row quad, replica
+  const int row = rq * 4 + wv;                                       // matrix row i of every block
+  const int kl = lane >> 4, cl = lane & 15;
+  const int64_t n_own = a.own_end - a.own_begin;
+  // B fragments: row `row` of every reference matrix (k = 4 kk + kl, entry = 64 row + 16 tc + cl)
+  double bS[8][4], bE[6][2][4];
+  {
+    const double* T = a.q3g_tab + row * 64 + cl;
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk)
+#pragma unroll
+      for (int tc = 0; tc < 4; ++tc) bS[kk][tc] = T[(4 * kk + kl) * 4096 + 16 * tc];
+#pragma unroll
+    for (int f = 0; f < 6; ++f)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int tc = 0; tc < 4; ++tc) bE[f][kk][tc] = T[(32 + 8 * f + 4 * kk + kl) * 4096 + 16 * tc];
+  }
+  double* const vals = a.vals;
+  for (int64_t g = x + 8 * int64_t(rep); g < n_groups; g += 8 * int64_t(a.q3g_reps)) {
+    const double* C = a.q3g_coef + g * (Q3G_K * 16) + cl;   // A fragments: element cl, term 4 kk + kl
+    double aS[8], aE[6][2];
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) aS[kk] = C[(4 * kk + kl) * 16];
+#pragma unroll
+    for (int f = 0; f < 6; ++f)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) aE[f][kk] = C[(32 + 8 * f + 4 * kk + kl) * 16];
+    // the 4 output elements of this lane: D register r holds element kl + 4 r, entry 16 tc + cl
+    double* rowp[4];
+    uint64_t info[4];
+    bool ok[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t k = g * 16 + kl + 4 * r;
+      ok[r] = k < n_own;
+      const int64_t kk = ok[r] ? k : 0;
+      const int64_t off = a.q3g_meta[2 * kk];
+      info[r] = uint64_t(a.q3g_meta[2 * kk + 1]);
+      rowp[r] = vals + off + int64_t(row) * 64 * int64_t(info[r] & 0xff) + cl;
+    }
+    // self block
+    dbl4 acc[4];
+#pragma unroll
+    for (int tc = 0; tc < 4; ++tc) acc[tc] = dbl4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk)
+#pragma unroll
+      for (int tc = 0; tc < 4; ++tc) acc[tc] = mfma(aS[kk], bS[kk][tc], acc[tc]);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int pos = int((info[r] >> 8) & 0xff);
+      if (ok[r]) {
+#pragma unroll
+        for (int tc = 0; tc < 4; ++tc) __builtin_nontemporal_store(acc[tc][r], rowp[r] + pos * 64 + 16 * tc);
+      }
+    }
+    // face blocks
+#pragma unroll
+    for (int f = 0; f < 6; ++f) {
+#pragma unroll
+      for (int tc = 0; tc < 4; ++tc) {
+        acc[tc] = mfma(aE[f][0], bE[f][0][tc], dbl4{0.0, 0.0, 0.0, 0.0});
+        acc[tc] = mfma(aE[f][1], bE[f][1][tc], acc[tc]);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int pos = int((info[r] >> (16 + 8 * f)) & 0xff);
+        if (ok[r] && pos != 0xff) {
+#pragma unroll
+          for (int tc = 0; tc < 4; ++tc) __builtin_nontemporal_store(acc[tc][r], rowp[r] + pos * 64 + 16 * tc);
+        }
+      }
+    }
+  }
+}
+
 static hipError_t launch_hex_q3(const HexArgs& a, hipStream_t s)
 {
   const int64_t n_own = a.own_end - a.own_begin;
   if (n_own <= 0) return hipSuccess;
   hipLaunchKernelGGL(hex_q3_setup_kernel, dim3(unsigned((n_own + 255) / 256)), dim3(256), 0, s, a);
-  const int64_t grid = std::min<int64_t>(n_own, 1 << 20);
-  hipLaunchKernelGGL(hex_q3_kernel, dim3(unsigned(grid)), dim3(256), 0, s, a);
+  if (a.debug_flags & 512) {   // A/B: the register-fragment MFMA kernel (operands generated per element)
+    const int64_t grid = std::min<int64_t>(n_own, 1 << 20);
+    hipLaunchKernelGGL(hex_q3_kernel, dim3(unsigned(grid)), dim3(256), 0, s, a);
+    return hipGetLastError();
+  }
+  const int64_t n_groups = (n_own + 15) / 16;
+  hipLaunchKernelGGL(hex_q3g_coef_kernel, dim3(unsigned((n_groups * 16 + 255) / 256)), dim3(256), 0, s, a, n_groups);
+  // 16 row quads x 8 XCDs x reps workgroups of 4 row waves
+  hipLaunchKernelGGL(hex_q3g_kernel, dim3(unsigned(128 * a.q3g_reps)), dim3(256), 0, s, a, n_groups);
   return hipGetLastError();
 }
 

@@ -58,12 +58,24 @@ struct HexArgs {
   double* vals;
   double sigma_inner, sigma_boundary, beta;
   double* ws;                   // p=3 register kernel: per-element coefficient records [n_own][HEX_REC]
-  int32_t debug_flags, pad;     // ablations (HDD_ABLATION builds only)
+  int32_t debug_flags, pad;     // ablations (HDD_ABLATION builds only); bit 512: the register-MFMA q3 kernel
   HexTables tab;
+  // p=3 reference-matrix GEMM path (hex_q3g_kernel): per 16-element group the coefficient vectors
+  // [n_groups][Q3G_K][16], per element {value offset, packed row-block layout} [n_own][2], and the
+  // element-independent reference matrices [Q3G_K][4096] (Q3G_K = 32 self-block + 6 x 8 face-block terms)
+  double* q3g_coef;
+  int64_t* q3g_meta;
+  const double* q3g_tab;
+  int32_t q3g_reps, pad3;
 };
 
 constexpr int HEX_REC = 72;     // doubles per element record (see hex_qp.hip)
+constexpr int Q3G_K = 80;       // coefficient / reference-matrix terms of the p=3 GEMM path
 bool hex_uses_records(const HexArgs& a, int degree, int nq1v, int nq1f);
+// doubles of workspace the p=3 path needs for n_own elements (records + GEMM coefficients + layout)
+size_t hex_q3_workspace_doubles(int64_t n_own);
+// the reference matrices of the p=3 GEMM path from the 1D tables (host): out [Q3G_K][4096]
+void hex_q3g_reference_tables(const HexTables& t, double* out);
 
 // degree p in 1..3; (nq1v, nq1f) Gauss points per direction; *supported = false if no kernel matches
 hipError_t launch_hex(const HexArgs& a, int degree, int nq1v, int nq1f, hipStream_t s, bool* supported);

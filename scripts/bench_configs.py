@@ -214,7 +214,7 @@ def c5(args):
     nq, nqf = nq1v ** 3, nq1f ** 2
     # F = ne 2 nb^2 nq d + nif 24 nb^2 nqf + nbf 6 nb^2 nqf (reference quadrature)
     alg_flops = loc.n_own * 2 * nb * nb * nq * 3 + nif * 24 * nb * nb * nqf + nbf * 6 * nb * nb * nqf
-    # executed MFMA work of hex_q3_kernel (v_mfma_f64_16x16x4: 2048 flop), whole element = 4 waves:
+    # executed MFMA work (v_mfma_f64_16x16x4: 2048 flop).  hex_q3_kernel (HDD_DEBUG_FLAGS=512), whole element = 4 waves:
     # volume 27 k-steps x 4 row tiles per wave; every face runs its rows in the layout rotated to its normal,
     # so the [V] part takes 1 row tile (4 k-steps) per wave; the [N] part 4 tiles x 4 k-steps in every wave
     # on x / y faces and in one wave only on z faces (column skip) -> x/y: 80 (S) + 80 (E, inner) per face,
@@ -222,8 +222,16 @@ def c5(args):
     nbr_own = nbr[:, loc.own_begin:loc.own_end]
     xy_inner = int((nbr_own[:4] >= 0).sum()); xy_dir = int((nbr_own[:4] == H.NBR_DIRICHLET).sum())
     z_inner = int((nbr_own[4:] >= 0).sum()); z_dir = int((nbr_own[4:] == H.NBR_DIRICHLET).sum())
-    n_mfma = (loc.n_own * 4 * 108 + (xy_inner + xy_dir) * 80 + xy_inner * 80 + (z_inner + z_dir) * 32
-              + z_inner * 32) if deg == 3 else 0
+    legacy = int(os.environ.get("HDD_DEBUG_FLAGS", "0") or 0) & 512
+    if deg != 3:
+        n_mfma = 0
+    elif legacy:
+        n_mfma = (loc.n_own * 4 * 108 + (xy_inner + xy_dir) * 80 + xy_inner * 80 + (z_inner + z_dir) * 32
+                  + z_inner * 32)
+    else:
+        # hex_q3g_kernel: per 16-element group, each of the 64 row waves runs 8 x 4 (self, 32 terms) +
+        # 6 x 2 x 4 (face blocks, 8 terms) MFMAs, boundary faces included (zero coefficients)
+        n_mfma = (loc.n_own + 15) // 16 * 64 * 80
     mfma_flops = 2048 * n_mfma
     alg_bytes = 8 * dp.nnz + loc.n_own * (24 * 8 + 8 + 6 * 4)
     dofs = nb * loc.n_own

@@ -84,8 +84,8 @@ def test_hex_smooth_kappa_sym_tensor(ctx, deg):
         assert ok, worst
 
 
-def test_hex_neumann_boundary(ctx):
-    deg = 2
+@pytest.mark.parametrize("deg", [2, 3])
+def test_hex_neumann_boundary(ctx, deg):
     g, ei, q = _setup((3, 3, 3), (1, 1, 1), deg, boundary=H.BOUNDARY_ALL_NEUMANN)
     loc = g.local()
     dm = H.DeviceMesh(loc)
@@ -95,6 +95,44 @@ def test_hex_neumann_boundary(ctx):
     prm = O.qp_params(q, boundary=O.BOUNDARY_NEUMANN)
     _, _, oval = O.qp_assemble(q, O.scalar(O.FN_CONST, 2.0), O.qp_tensor(), prm, elem_index=ei)
     worst, ok = compare_rows(dp.host[0], val.cpu().numpy(), oval, RTOL)
+    assert ok, worst
+
+
+def test_hex_q3_gemm_equals_register_kernel():
+    """p = 3 with per-element data: the reference-matrix GEMM kernel (hex_q3g_kernel, default) against the
+    register-fragment MFMA kernel (HDD_DEBUG_FLAGS bit 512) on 10 x 9 x 7 elements in 2 slabs (ragged last
+    16-element group, every workgroup walking several groups, Dirichlet faces), both through the C ABI; and the
+    oracle on the same input at the parity tolerance."""
+    import os
+    torch = _torch()
+    deg, n = 3, (10, 9, 7)
+    g, ei, q = _setup(n, (2, 1, 1), deg)
+    loc = g.local()
+    dm, dp = H.DeviceMesh(loc), H.DevicePattern(loc)
+    T = _spd_tensors(g.ne, 11)
+    kel = np.random.default_rng(12).uniform(0.2, 4.0, g.ne)
+    ten = H.tensor_fn(H.TENSOR_SYM_PER_ELEM, per_elem=torch.from_numpy(np.ascontiguousarray(T.T)).cuda(), dim=3)
+    kap = H.scalar_fn(H.FN_PER_ELEM, per_elem=torch.from_numpy(kel).cuda())
+    old = os.environ.get("HDD_DEBUG_FLAGS")
+    vals = []
+    for flags in ("0", "512"):
+        os.environ["HDD_DEBUG_FLAGS"] = flags
+        c = H.Context(0)
+        (v,) = H.assemble(c, dm, dp, [kap], ten, H.params_for(deg, 3))
+        torch.cuda.synchronize()
+        vals.append(v.cpu().numpy())
+        del c
+    if old is None:
+        del os.environ["HDD_DEBUG_FLAGS"]
+    else:
+        os.environ["HDD_DEBUG_FLAGS"] = old
+    rp = dp.host[0]
+    worst, ok = compare_rows(rp, vals[0], vals[1], RTOL)
+    assert ok, worst
+    _, _, oval = O.qp_assemble(q, O.scalar(O.FN_PER_ELEM, per_elem=np.ascontiguousarray(kel[ei])),
+                               O.qp_tensor(O.TENSOR_SYM_PER_ELEM, per_elem=np.ascontiguousarray(T[ei])),
+                               O.qp_params(q), elem_index=ei)
+    worst, ok = compare_rows(rp, vals[0], oval, RTOL)
     assert ok, worst
 
 
