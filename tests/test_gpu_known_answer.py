@@ -13,7 +13,8 @@ These tests fix their structure by exact answers instead of fixtures:
    g_N = A grad u . n on y = 0, 1 (L2Face): nonzero for the symmetric tensor.  With the GPU matrix and rhs
    the exact nodal values satisfy the discrete equations to rounding (relative residual <= 1e-13, which a
    sign or weight error in the consistency terms would break by orders of magnitude), and a direct host solve
-   returns them to 1e-8 (the solve is conditioned like contrast / h^2 ~ 1e8-1e9).
+   returns them to 1e-7 (the solve is conditioned like contrast / h^2 ~ 1e8-1e9, so its forward error is
+   cond * eps ~ 1e-8..1e-7 whatever the last bits of the matrix; observed 0.3-1.4e-8).
 2. BlockSWIPDG == monolithic SWIPDG at the full C4 size (3520 x 1200 Q1, SPE10 synthetic checkerboard) for the
    2x2, 4x4 and 8x8 partitions: the block matrix is the monolithic one under the element permutation, entry for
    entry and bit for bit (block-swipdg.hh:1292-1294, 1328-1379; compared on the GPU by sorted global keys).
@@ -91,7 +92,7 @@ def test_piecewise_linear_solution_across_1e6_jump(ctx, et, tensor_kind):
     assert res <= 1e-13, "consistency residual %.3g (contrast %g, %s, %s)" % (res, contrast, et, tensor_kind)
     uh = spla.spsolve(Am.tocsc(), bh)
     err = np.max(np.abs(uh - ue)) / np.max(np.abs(ue))
-    assert err <= 1e-8, "nodal error %.3g (contrast %g, %s, %s)" % (err, contrast, et, tensor_kind)
+    assert err <= 1e-7, "nodal error %.3g (contrast %g, %s, %s)" % (err, contrast, et, tensor_kind)
 
 
 def _keys(torch, row_ptr, col, nb, perm):

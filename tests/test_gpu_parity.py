@@ -171,6 +171,53 @@ def test_rank_local_rows_equal_global_slice(ctx):
         assert np.allclose(val, gval[lo:hi], rtol=0, atol=1e-13 * np.max(np.abs(gval)))
 
 
+@pytest.mark.parametrize("tk,bnd", [("iso", "dirichlet"), ("sym", "dirichlet"), ("sym", "neumann")])
+def test_q1_ragged_tiles_and_tile_lists(ctx, tk, bnd):
+    """Q1 closed form (the C4 kernel) on 203 x 91 quads over 4 x 3 subdomains -- uniform and non-uniform
+    tiles, a ragged last tile -- with per-element diffusion factor and tensor, Dirichlet or Neumann boundary,
+    against the oracle on the grid's own (subdomain-major) element order; and a rank-local slice assembled
+    through the sharded path's interior / halo tile lists == its one-shot assembly, bit for bit."""
+    torch = _torch()
+    rng = np.random.default_rng(21)
+    nx, ny = 203, 91
+    boundary = H.BOUNDARY_ALL_NEUMANN if bnd == "neumann" else H.BOUNDARY_ALL_DIRICHLET
+    grid = H.Grid.structured(H.CUBE, nx, ny, (0, 0), (5, 1), px=4, py=3, boundary=boundary)
+    ne = grid.ne
+    a = rng.uniform(0.5, 2.0, ne); c = rng.uniform(0.5, 2.0, ne); b = rng.uniform(-0.3, 0.3, ne)
+    kap = rng.uniform(0.1, 10.0, ne)
+    t_np = np.stack([a, b, c], 0) if tk == "sym" else a
+    tkind = H.TENSOR_SYM_PER_ELEM if tk == "sym" else H.TENSOR_ISO_PER_ELEM
+
+    def run(s0=0, s1=None):
+        loc = grid.local(s0, s1)
+        idx = loc.global_id
+        ten = H.tensor_fn(tkind, per_elem=torch.from_numpy(np.ascontiguousarray(t_np[..., idx])).cuda())
+        kf = [H.scalar_fn(H.FN_PER_ELEM, per_elem=torch.from_numpy(np.ascontiguousarray(kap[idx])).cuda())]
+        dm, dp = H.DeviceMesh(loc), H.DevicePattern(loc)
+        (v,) = H.assemble(ctx, dm, dp, kf, ten)
+        tiles = None
+        if s1 is not None:   # the sharded path's interior / halo tile lists, assembled in two launches
+            t_in, t_bd = H.halo_tiles(loc)
+            tiles = torch.full_like(v, float("nan"))
+            for tl in (t_in, t_bd):
+                H.assemble_tiles(ctx, dm, dp, kf, ten, torch.from_numpy(tl).cuda(), [tiles])
+        torch.cuda.synchronize()
+        return dp.host[0], v.cpu().numpy(), (None if tiles is None else tiles.cpu().numpy())
+
+    rp, val, _ = run()
+    pc, pev, _ = grid.connectivity()
+    og = O.Grid(_oracle_mesh(H.CUBE, 1, 1, (0, 0), (1, 1))[0], pc, pev)
+    okind = O.TENSOR_SYM_PER_ELEM if tk == "sym" else O.TENSOR_ISO_PER_ELEM
+    oper = np.ascontiguousarray(t_np.T) if tk == "sym" else t_np
+    orp, _, oval = O.assemble(og, O.scalar(O.FN_PER_ELEM, per_elem=kap), O.tensor(okind, per_elem=oper),
+                              O.params(O.BOUNDARY_NEUMANN if bnd == "neumann" else O.BOUNDARY_DIRICHLET))
+    assert np.array_equal(rp, orp)
+    worst, ok = compare_rows(rp, val, oval, RTOL)
+    assert ok, worst
+    _, lv, lt = run(5, 9)
+    assert np.array_equal(lv, lt)
+
+
 @pytest.mark.parametrize("et,smooth", [(H.SIMPLEX, False), (H.SIMPLEX, True), (H.CUBE, False), (H.CUBE, True)])
 def test_tile_split_overlap(ctx, et, smooth):
     """hdd_swipdg_assemble_tiles: interior tiles assembled while the ghost records are garbage (NaN), then
