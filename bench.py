@@ -122,6 +122,26 @@ def cpu_baseline(nx_full, ny, target_s, cube=False):
                 cpu_model=_cpu_model(), host_cpus=os.cpu_count())
 
 
+def attainable_hbm(torch, nbytes=1 << 30, reps=10):
+    """Attainable HBM bandwidth on this box, measured in the same run ('also report attainable
+    BW from a device copy kernel'): a device-to-device copy (reads + writes) and a fill (writes only) of a
+    1 GiB buffer, HIP events around `reps` back-to-back launches after one warm-up; GB/s of bytes moved."""
+    a = torch.empty(nbytes // 8, dtype=torch.float64, device="cuda").fill_(1.0)
+    b = torch.empty_like(a)
+    out = {}
+    for name, fn, moved in (("copy", lambda: b.copy_(a), 2 * nbytes), ("fill", lambda: b.fill_(2.0), nbytes)):
+        fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        out[name + "_gbs"] = moved * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    del a, b
+    return out
+
+
 def lib_build_id():
     """sha256 prefix of the timed libhdd_amd.so: PMC traffic files are stamped with it, and a traffic figure
     measured on another build is not reported."""
@@ -261,6 +281,7 @@ def main():
         elif world > 1:
             halo_desc = ", %s face halo%s" % ("RCCL" if args.backend == "nccl" else "gloo host-staged (rehearsal)",
                                               " overlapped with interior tiles" if not args.no_overlap else "")
+        att = attainable_hbm(torch)
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(nx // world, ny, args.cpu_seconds, cube=c4)
@@ -293,7 +314,10 @@ def main():
                          "kernel": "swipdg_persistent_kernel<%s<1, 0, false>, %s>"
                                    % ("Q1PwcPolicy" if c4 else "P1PwcPolicy", "true" if per_step else "false"),
                          "kernel_ms_avg": kernel_ms, "kernel_ms_avg_max_rank": kernel_ms_max,
-                         "algorithmic_bytes_per_launch": alg_bytes},
+                         "algorithmic_bytes_per_launch": alg_bytes,
+                         # measured on this box in this run: device copy (read + write) and fill (write)
+                         "attainable": dict(att, source="torch copy_ / fill_ of 1 GiB, HIP events"),
+                         "frac_of_torch_copy": achieved / att["copy_gbs"]},
             "cpu_baseline": cpu,
         }
         out["config"]["entry"] = "hdd_block_assemble_sharded (C ABI)"
