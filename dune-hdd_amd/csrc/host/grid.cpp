@@ -613,6 +613,39 @@ extern "C" int hdd_local_centers(const hdd_local* l, double* centers)
   return HDD_OK;
 }
 
+extern "C" int hdd_local_vertices(const hdd_local* l, int64_t* n_vertices, int32_t* elem_vertices,
+                                  double* vertex_coords)
+{
+  if (!l || !n_vertices) return set_error(HDD_ERR_INVALID, "hdd_local_vertices: null argument");
+  const Local& L = l->impl;
+  const Grid& G = *L.g;
+  const int64_t nl = L.n_local();
+  const int nv = G.nvpe;
+  // local vertex set = sorted distinct global ids of the local elements' vertices (elements in local
+  // order = global order, so neighbouring elements get neighbouring vertex ids)
+  std::vector<int64_t> ids(size_t(nl) * nv);
+  int64_t vv[8];
+  for (int64_t e = 0; e < nl; ++e) {
+    G.vertices(L.global_of(e), vv);
+    for (int k = 0; k < nv; ++k) ids[size_t(e) * nv + k] = vv[k];
+  }
+  std::vector<int64_t> uniq(ids);
+  std::sort(uniq.begin(), uniq.end());
+  uniq.erase(std::unique(uniq.begin(), uniq.end()), uniq.end());
+  if (int64_t(uniq.size()) > int64_t(INT32_MAX))
+    return set_error(HDD_ERR_RANGE, "hdd_local_vertices: too many local vertices for int32 ids");
+  *n_vertices = int64_t(uniq.size());
+  if (elem_vertices)
+    for (int64_t e = 0; e < nl; ++e)
+      for (int k = 0; k < nv; ++k) {
+        const int64_t g = ids[size_t(e) * nv + k];
+        elem_vertices[k * nl + e] = int32_t(std::lower_bound(uniq.begin(), uniq.end(), g) - uniq.begin());
+      }
+  if (vertex_coords)
+    for (size_t v = 0; v < uniq.size(); ++v) G.vertex_coord(uniq[v], vertex_coords + G.dim * v);
+  return HDD_OK;
+}
+
 static int ghost_owner(const Local& L, const int32_t* owner, int64_t gid)
 {
   return owner[L.g->subdomain(gid)];

@@ -281,6 +281,13 @@ static int assemble_impl(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_fn* k
   a.beta = p->beta;
   a.tile_list = d_tiles;
   a.n_tile_list = n_tiles;
+  if (!m->elem_vertices != !m->vertex_coords)
+    return set_error(HDD_ERR_INVALID, "hdd_swipdg_assemble: mesh elem_vertices / vertex_coords: both or neither");
+  // vertex-indexed geometry (bit 16384 of HDD_DEBUG_FLAGS: A/B against the element-major coords)
+  if (m->elem_vertices && !(ctx->debug_flags & 16384)) {
+    a.ev = m->elem_vertices;
+    a.vxy = m->vertex_coords;
+  }
   a.n_cu = ctx->n_cu;
   a.debug_flags = ctx->debug_flags;   // profiling ablations only
   a.wgcu = ctx->wgcu;

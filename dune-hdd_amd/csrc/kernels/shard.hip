@@ -385,6 +385,8 @@ struct hdd_shard {
   int32_t* d_nbrs = nullptr;
   uint32_t* d_finfo = nullptr;
   int64_t* d_gid = nullptr;
+  int32_t* d_ev = nullptr;             // vertex-indexed geometry (2d): element -> local vertex ids
+  double* d_vxy = nullptr;             //   and the rank-local vertex coordinates (owned + ghost elements')
   // halo
   std::vector<int32_t> peers;
   std::vector<int64_t> send_prefix, recv_prefix, recv_col0;
@@ -406,7 +408,7 @@ extern "C" void hdd_shard_destroy(hdd_shard* sh)
   for (void* p : {static_cast<void*>(sh->d_coords), static_cast<void*>(sh->d_nbrs), static_cast<void*>(sh->d_finfo),
                   static_cast<void*>(sh->d_gid), static_cast<void*>(sh->d_send_idx), static_cast<void*>(sh->d_sbuf),
                   static_cast<void*>(sh->d_rbuf), static_cast<void*>(sh->d_tiles_in),
-                  static_cast<void*>(sh->d_tiles_bd)})
+                  static_cast<void*>(sh->d_tiles_bd), static_cast<void*>(sh->d_ev), static_cast<void*>(sh->d_vxy)})
     if (p) (void)hipFree(p);
   if (sh->local) hdd_local_destroy(sh->local);
   delete sh;
@@ -466,6 +468,18 @@ extern "C" int hdd_shard_create(hdd_ctx* ctx, const hdd_grid* g, int32_t nranks,
   if (rc) return fail(rc);
   rc = hdd_dg_pattern_count(gi.nfaces, gi.nb, nl, ob, oe, nbrs.data(), &sh->nnz);
   if (rc) return fail(rc);
+  // vertex-indexed geometry of the local elements (2d): what the P1 / Q1 kernels read
+  std::vector<int32_t> ev;
+  std::vector<double> vxy;
+  if (gi.dim == 2) {
+    int64_t nvl = 0;
+    rc = hdd_local_vertices(sh->local, &nvl, nullptr, nullptr);
+    if (rc) return fail(rc);
+    ev.resize(size_t(gi.nvpe) * nl);
+    vxy.resize(size_t(2) * nvl);
+    rc = hdd_local_vertices(sh->local, &nvl, ev.data(), vxy.data());
+    if (rc) return fail(rc);
+  }
 
   // halo plan: peers ascending, send lists concatenated in peer order
   int32_t np = 0;
@@ -514,6 +528,8 @@ extern "C" int hdd_shard_create(hdd_ctx* ctx, const hdd_grid* g, int32_t nranks,
   if (e == hipSuccess) e = upload(&sh->d_nbrs, nbrs);
   if (e == hipSuccess) e = upload(&sh->d_finfo, finfo);
   if (e == hipSuccess) e = upload(&sh->d_gid, sh->gid);
+  if (e == hipSuccess && !ev.empty()) e = upload(&sh->d_ev, ev);
+  if (e == hipSuccess && !vxy.empty()) e = upload(&sh->d_vxy, vxy);
   if (e == hipSuccess) e = upload(&sh->d_send_idx, send_idx);
   if (e == hipSuccess) e = upload(&sh->d_tiles_in, tin);
   if (e == hipSuccess) e = upload(&sh->d_tiles_bd, tbd);
@@ -558,7 +574,7 @@ extern "C" int hdd_shard_mesh(const hdd_shard* sh, hdd_mesh* m)
 {
   if (!sh || !m) return set_error(HDD_ERR_INVALID, "hdd_shard_mesh: null argument");
   *m = hdd_mesh{sh->gi.elem_type, sh->gi.elem_type == HDD_HEX ? sh->degree : 1, sh->li.n_local, sh->li.own_begin,
-                sh->li.own_end, sh->d_coords, sh->d_nbrs, sh->d_finfo};
+                sh->li.own_end, sh->d_coords, sh->d_nbrs, sh->d_finfo, sh->d_ev, sh->d_vxy};
   return HDD_OK;
 }
 
@@ -615,6 +631,10 @@ extern "C" int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm*
     return set_error(HDD_ERR_INVALID, "hdd_block_assemble_sharded: pattern does not belong to this shard");
   hdd_mesh m;
   hdd_shard_mesh(sh, &m);
+  if (flags & HDD_SHARD_HALO_GEOMETRY) {   // ghost geometry arrives through the halo: element-major coords
+    m.elem_vertices = nullptr;
+    m.vertex_coords = nullptr;
+  }
   const hipStream_t s = static_cast<hipStream_t>(stream);
 
   // halo rows: [coordinates] [tensor] [per-element diffusion factors (each distinct array once)]

@@ -643,12 +643,22 @@ struct P1Own {
   uint32_t finfo;
   Tensor A;
   double ke;
+  int32_t vid[3];   // vertex-indexed geometry (VX): local vertex ids; X / Y then arrive with the gathers
 };
 struct P1Gat {
   double Ox[3], Oy[3];
   Tensor Ap[3];
   double kn[3];
+  int32_t ov[3];    // VX: the neighbour's off-face vertex id; Ox / Oy arrive in the second gather stage
 };
+
+// vertex (x, y) of the vertex-indexed geometry: one 16-byte load
+__device__ __forceinline__ void vertex_xy(const AssembleArgs& a, int32_t v, double& x, double& y)
+{
+  const dvec2 p = *reinterpret_cast<const dvec2*>(a.vxy + 2 * int64_t(v));
+  x = p.x;
+  y = p.y;
+}
 
 template <int TK>
 __device__ __forceinline__ Tensor tensor_k(const AssembleArgs& a, int64_t e)
@@ -671,14 +681,21 @@ __device__ __forceinline__ double kappa_k(const AssembleArgs& a, int64_t e)
   else return a.kappa[0].c;
 }
 
-template <int TK, int KK>
+// Own-data loads of a tile (coalesced SoA).  VX: vertex ids instead of coordinates -- the vertex
+// coordinates are then gathered with the neighbour data (p1_load_gat), the neighbour's off-face vertex in a
+// second stage (p1_load_gat2) that the persistent driver issues after the tile's stores.
+template <int TK, int KK, bool VX = false>
 __device__ __forceinline__ void p1_load_own(const AssembleArgs& a, int64_t e, P1Own& o)
 {
   const int64_t ne = a.n_local;
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
-    o.X[k] = a.coords[(2 * k) * ne + e];
-    o.Y[k] = a.coords[(2 * k + 1) * ne + e];
+    if constexpr (VX) {
+      o.vid[k] = a.ev[k * ne + e];
+    } else {
+      o.X[k] = a.coords[(2 * k) * ne + e];
+      o.Y[k] = a.coords[(2 * k + 1) * ne + e];
+    }
   }
 #pragma unroll
   for (int f = 0; f < 3; ++f) o.nbr[f] = a.nbrs[f * ne + e];
@@ -687,20 +704,36 @@ __device__ __forceinline__ void p1_load_own(const AssembleArgs& a, int64_t e, P1
   o.ke = kappa_k<KK>(a, e);
 }
 
-template <int TK, int KK>
-__device__ __forceinline__ void p1_load_gat(const AssembleArgs& a, int64_t e, const P1Own& o, P1Gat& g)
+template <int TK, int KK, bool VX = false>
+__device__ __forceinline__ void p1_load_gat(const AssembleArgs& a, int64_t e, P1Own& o, P1Gat& g)
 {
   const int64_t ne = a.n_local;
+  if constexpr (VX) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) vertex_xy(a, o.vid[k], o.X[k], o.Y[k]);
+  }
 #pragma unroll
   for (int f = 0; f < 3; ++f) {
     const int64_t n = o.nbr[f] >= 0 ? int64_t(o.nbr[f]) : e;   // boundary faces: harmless own reload
     const uint32_t inf = (o.finfo >> (4 * f)) & 15u;
     const int tw = int(inf & 7u);
     const int to = 3 - Simplex::fv(tw, 0) - Simplex::fv(tw, 1);
-    g.Ox[f] = a.coords[(2 * to) * ne + n];
-    g.Oy[f] = a.coords[(2 * to + 1) * ne + n];
+    if constexpr (VX) {
+      g.ov[f] = a.ev[to * ne + n];
+    } else {
+      g.Ox[f] = a.coords[(2 * to) * ne + n];
+      g.Oy[f] = a.coords[(2 * to + 1) * ne + n];
+    }
     g.Ap[f] = tensor_k<TK>(a, n);
     g.kn[f] = kappa_k<KK>(a, n);
+  }
+}
+template <bool VX>
+__device__ __forceinline__ void p1_load_gat2(const AssembleArgs& a, P1Gat& g)
+{
+  if constexpr (VX) {
+#pragma unroll
+    for (int f = 0; f < 3; ++f) vertex_xy(a, g.ov[f], g.Ox[f], g.Oy[f]);
   }
 }
 
@@ -841,12 +874,14 @@ struct GOwn {
   uint32_t finfo;
   Tensor A;
   double ke;
+  int32_t vid[E::NV];   // VX: local vertex ids (as P1Own)
 };
 template <class E>
 struct GGat {
   double Cx[E::NF], Cy[E::NF];
   Tensor Ap[E::NF];
   double kn[E::NF];
+  int32_t ov[E::NF];    // VX: the neighbour's third-role vertex id
 };
 
 template <class E>
@@ -875,7 +910,7 @@ struct RotImg {
   }
 };
 
-template <class E, int NQV, int NQF, int TK, int KK>
+template <class E, int NQV, int NQF, int TK, int KK, bool VX = false>
 struct GenericPolicy {
   static constexpr int NB = E::NB, NF = E::NF, NV = E::NV;
   static constexpr int RB = (NF + 1) * NB * NB;
@@ -894,8 +929,12 @@ struct GenericPolicy {
     const int64_t ne = a.n_local;
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
-      o.X[k] = a.coords[(2 * k) * ne + e];
-      o.Y[k] = a.coords[(2 * k + 1) * ne + e];
+      if constexpr (VX) {
+        o.vid[k] = a.ev[k * ne + e];
+      } else {
+        o.X[k] = a.coords[(2 * k) * ne + e];
+        o.Y[k] = a.coords[(2 * k + 1) * ne + e];
+      }
     }
 #pragma unroll
     for (int f = 0; f < NF; ++f) o.nbr[f] = a.nbrs[f * ne + e];
@@ -904,17 +943,33 @@ struct GenericPolicy {
     o.ke = KK == HDD_FN_SINUSOID ? 0.0 : kappa_k<KK == HDD_FN_PER_ELEM ? HDD_FN_PER_ELEM : HDD_FN_CONST>(a, e);
   }
 
-  __device__ static void load_gat(const AssembleArgs& a, int64_t e, const Own& o, Gat& g)
+  __device__ static void load_gat(const AssembleArgs& a, int64_t e, Own& o, Gat& g)
   {
     const int64_t ne = a.n_local;
+    if constexpr (VX) {
+#pragma unroll
+      for (int k = 0; k < NV; ++k) vertex_xy(a, o.vid[k], o.X[k], o.Y[k]);
+    }
 #pragma unroll
     for (int f = 0; f < NF; ++f) {
       const int64_t n = o.nbr[f] >= 0 ? int64_t(o.nbr[f]) : e;
       const int c = role_slot<E>(o.finfo, f, 2);
-      g.Cx[f] = a.coords[(2 * c) * ne + n];
-      g.Cy[f] = a.coords[(2 * c + 1) * ne + n];
+      if constexpr (VX) {
+        g.ov[f] = a.ev[c * ne + n];
+      } else {
+        g.Cx[f] = a.coords[(2 * c) * ne + n];
+        g.Cy[f] = a.coords[(2 * c + 1) * ne + n];
+      }
       g.Ap[f] = tensor_k<TK>(a, n);
       g.kn[f] = KK == HDD_FN_SINUSOID ? 0.0 : kappa_k<KK == HDD_FN_PER_ELEM ? HDD_FN_PER_ELEM : HDD_FN_CONST>(a, n);
+    }
+  }
+
+  __device__ static void load_gat2(const AssembleArgs& a, Gat& g)
+  {
+    if constexpr (VX) {
+#pragma unroll
+      for (int f = 0; f < NF; ++f) vertex_xy(a, g.ov[f], g.Cx[f], g.Cy[f]);
     }
   }
 
@@ -1090,9 +1145,9 @@ struct GenericPolicy {
 // maximum).  Neighbour quantities are in role coordinates (A = my face vertex a, B = b, C = the
 // neighbour vertex next to A), as in GenericPolicy.
 // ------------------------------------------------------------------------------------------------
-template <int TK, int KK, bool PEN = false>   // PEN: penalty terms only (the SWIPDG penalty product)
-struct Q1PwcPolicy : GenericPolicy<Cube, 1, 2, TK, KK> {
-  using Base = GenericPolicy<Cube, 1, 2, TK, KK>;
+template <int TK, int KK, bool PEN = false, bool VX = false>   // PEN: penalty terms only (the SWIPDG penalty product)
+struct Q1PwcPolicy : GenericPolicy<Cube, 1, 2, TK, KK, VX> {
+  using Base = GenericPolicy<Cube, 1, 2, TK, KK, VX>;
   using E = Cube;
   static constexpr int NB = 4, NF = 4;
   using Own = typename Base::Own;
@@ -1227,7 +1282,7 @@ struct Q1PwcPolicy : GenericPolicy<Cube, 1, 2, TK, KK> {
 };
 
 // P1 simplex, piecewise-constant coefficients: the closed-form policy (p1_compute above)
-template <int TK, int KK, bool PEN = false>
+template <int TK, int KK, bool PEN = false, bool VX = false>
 struct P1PwcPolicy {
   static constexpr int NB = 3, NF = 3;
   static constexpr int RB = 36;
@@ -1237,8 +1292,9 @@ struct P1PwcPolicy {
   static constexpr bool PAD = false;          // store-bound: its 4-way write conflicts stay hidden
   using Own = P1Own;
   using Gat = P1Gat;
-  __device__ static void load_own(const AssembleArgs& a, int64_t e, Own& o) { p1_load_own<TK, KK>(a, e, o); }
-  __device__ static void load_gat(const AssembleArgs& a, int64_t e, const Own& o, Gat& g) { p1_load_gat<TK, KK>(a, e, o, g); }
+  __device__ static void load_own(const AssembleArgs& a, int64_t e, Own& o) { p1_load_own<TK, KK, VX>(a, e, o); }
+  __device__ static void load_gat(const AssembleArgs& a, int64_t e, Own& o, Gat& g) { p1_load_gat<TK, KK, VX>(a, e, o, g); }
+  __device__ static void load_gat2(const AssembleArgs& a, Gat& g) { p1_load_gat2<VX>(a, g); }
   __device__ static int n_interior(const Own& o) { return int(o.nbr[0] >= 0) + int(o.nbr[1] >= 0) + int(o.nbr[2] >= 0); }
   __device__ static void compute(const AssembleArgs& a, int64_t e, const Own& o, const Gat& g, double* img)
   {
@@ -1258,7 +1314,7 @@ struct P1PwcPolicy {
 // ord kappa + 0 / ord kappa + 2 with ord kappa = 3), so the entries equal the quadrature form up to
 // rounding, at 15 kappa evaluations and the P1 closed-form entry count per element.
 // ------------------------------------------------------------------------------------------------
-template <int TK>
+template <int TK, bool VX = false>
 struct P1SmoothPolicy {
   static constexpr int NB = 3, NF = 3;
   static constexpr int RB = 36;
@@ -1268,11 +1324,12 @@ struct P1SmoothPolicy {
   static constexpr bool PAD = false;
   using Own = P1Own;
   using Gat = P1Gat;
-  __device__ static void load_own(const AssembleArgs& a, int64_t e, Own& o) { p1_load_own<TK, HDD_FN_CONST>(a, e, o); }
-  __device__ static void load_gat(const AssembleArgs& a, int64_t e, const Own& o, Gat& g)
+  __device__ static void load_own(const AssembleArgs& a, int64_t e, Own& o) { p1_load_own<TK, HDD_FN_CONST, VX>(a, e, o); }
+  __device__ static void load_gat(const AssembleArgs& a, int64_t e, Own& o, Gat& g)
   {
-    p1_load_gat<TK, HDD_FN_CONST>(a, e, o, g);
+    p1_load_gat<TK, HDD_FN_CONST, VX>(a, e, o, g);
   }
+  __device__ static void load_gat2(const AssembleArgs& a, Gat& g) { p1_load_gat2<VX>(a, g); }
   __device__ static int n_interior(const Own& o) { return int(o.nbr[0] >= 0) + int(o.nbr[1] >= 0) + int(o.nbr[2] >= 0); }
 
   __device__ static void compute(const AssembleArgs& a, int64_t e, const Own& o, const Gat& gt, double* img)
@@ -1448,6 +1505,7 @@ struct VolProductPolicy {
     }
   }
   __device__ static void load_gat(const AssembleArgs&, int64_t, const Own&, Gat&) {}
+  __device__ static void load_gat2(const AssembleArgs&, Gat&) {}
   __device__ static int n_interior(const Own&) { return 0; }
 
   __host__ __device__ static constexpr double m1(int i, int j) { return i == j ? 1.0 / 3.0 : 1.0 / 6.0; }
@@ -1589,6 +1647,7 @@ swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
   typename P::Gat gat;
   P::load_own(a, e, own);
   P::load_gat(a, e, own, gat);
+  P::load_gat2(a, gat);
   int64_t base, tile_end;
   bounds(t, base, tile_end);
   double* out = a.vals[0];
@@ -1668,6 +1727,10 @@ swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ivec4, v), rsrc, idx * 8, 0, 2);
       }
     }
+    // second gather stage of tile t+1 (vertex-indexed geometry: the neighbours' off-face vertices by the
+    // ids the first stage brought): its wait covers the first stage only, which was issued before the
+    // stores of tile t (vmcnt is in order), so it never waits for those stores
+    P::load_gat2(a, gat_n);
     if (!has_next) break;
     t = tn;
     e = en;
@@ -1743,34 +1806,52 @@ static hipError_t dispatch_pwc(const AssembleArgs& a, hipStream_t s)
   return pe ? launch_persistent<PT<HDD_TENSOR_SYM_PER_ELEM, HDD_FN_PER_ELEM>>(a, s) : launch_persistent<PT<HDD_TENSOR_SYM_PER_ELEM, HDD_FN_CONST>>(a, s);
 }
 
-// instantiate a policy for the runtime (tensor kind, kappa kind) pair
-template <template <int, int> class PT>
-static hipError_t dispatch_kinds(const AssembleArgs& a, hipStream_t s, bool smooth)
+// instantiate a policy for the runtime (tensor kind, kappa kind) pair; VX: vertex-indexed geometry
+template <template <int, int, bool> class PT, bool VX>
+static hipError_t dispatch_kinds_vx(const AssembleArgs& a, hipStream_t s, bool smooth)
 {
   const int tk = a.tkind, kk = a.kappa[0].kind;
   if (smooth) {
-    if (tk == HDD_TENSOR_CONST) return launch_persistent<PT<HDD_TENSOR_CONST, HDD_FN_SINUSOID>>(a, s);
-    if (tk == HDD_TENSOR_ISO_PER_ELEM) return launch_persistent<PT<HDD_TENSOR_ISO_PER_ELEM, HDD_FN_SINUSOID>>(a, s);
-    return launch_persistent<PT<HDD_TENSOR_SYM_PER_ELEM, HDD_FN_SINUSOID>>(a, s);
+    if (tk == HDD_TENSOR_CONST) return launch_persistent<PT<HDD_TENSOR_CONST, HDD_FN_SINUSOID, VX>>(a, s);
+    if (tk == HDD_TENSOR_ISO_PER_ELEM) return launch_persistent<PT<HDD_TENSOR_ISO_PER_ELEM, HDD_FN_SINUSOID, VX>>(a, s);
+    return launch_persistent<PT<HDD_TENSOR_SYM_PER_ELEM, HDD_FN_SINUSOID, VX>>(a, s);
   }
   const bool pe = kk == HDD_FN_PER_ELEM;
   if (tk == HDD_TENSOR_CONST)
-    return pe ? launch_persistent<PT<HDD_TENSOR_CONST, HDD_FN_PER_ELEM>>(a, s) : launch_persistent<PT<HDD_TENSOR_CONST, HDD_FN_CONST>>(a, s);
+    return pe ? launch_persistent<PT<HDD_TENSOR_CONST, HDD_FN_PER_ELEM, VX>>(a, s)
+              : launch_persistent<PT<HDD_TENSOR_CONST, HDD_FN_CONST, VX>>(a, s);
   if (tk == HDD_TENSOR_ISO_PER_ELEM)
-    return pe ? launch_persistent<PT<HDD_TENSOR_ISO_PER_ELEM, HDD_FN_PER_ELEM>>(a, s) : launch_persistent<PT<HDD_TENSOR_ISO_PER_ELEM, HDD_FN_CONST>>(a, s);
-  return pe ? launch_persistent<PT<HDD_TENSOR_SYM_PER_ELEM, HDD_FN_PER_ELEM>>(a, s) : launch_persistent<PT<HDD_TENSOR_SYM_PER_ELEM, HDD_FN_CONST>>(a, s);
+    return pe ? launch_persistent<PT<HDD_TENSOR_ISO_PER_ELEM, HDD_FN_PER_ELEM, VX>>(a, s)
+              : launch_persistent<PT<HDD_TENSOR_ISO_PER_ELEM, HDD_FN_CONST, VX>>(a, s);
+  return pe ? launch_persistent<PT<HDD_TENSOR_SYM_PER_ELEM, HDD_FN_PER_ELEM, VX>>(a, s)
+            : launch_persistent<PT<HDD_TENSOR_SYM_PER_ELEM, HDD_FN_CONST, VX>>(a, s);
+}
+// Vertex-indexed geometry pays on triangles (C2 0.323 -> 0.245 ms, same box: 2 waves per SIMD hide the
+// second gather stage); the Q1 tiles run one wave per SIMD (40 KB image), where that stage's latency is
+// exposed (C4 0.600 -> 0.690 ms), so quads keep the element-major coords.
+template <template <int, int, bool> class PT>
+static hipError_t dispatch_kinds(const AssembleArgs& a, hipStream_t s, bool smooth)
+{
+  return a.ev && a.elem_type == HDD_SIMPLEX ? dispatch_kinds_vx<PT, true>(a, s, smooth)
+                                            : dispatch_kinds_vx<PT, false>(a, s, smooth);
 }
 
-template <int TK, int KK> using P1Pwc = P1PwcPolicy<TK, KK>;
-template <int TK, int KK> using Q1Pwc = Q1PwcPolicy<TK, KK>;
-template <int TK, int KK> using Q1Smooth3 = GenericPolicy<Cube, 4, 3, TK, KK>;
-template <int TK, int KK> using P1Smooth3 = GenericPolicy<Simplex, 6, 3, TK, KK>;
+template <int TK, int KK, bool VX> using P1Pwc = P1PwcPolicy<TK, KK, false, VX>;
+template <int TK, int KK, bool VX> using Q1Pwc = Q1PwcPolicy<TK, KK, false, VX>;
+template <int TK, int KK, bool VX> using Q1Smooth3 = GenericPolicy<Cube, 4, 3, TK, KK, VX>;
+template <int TK, int KK, bool VX> using P1Smooth3 = GenericPolicy<Simplex, 6, 3, TK, KK, VX>;
 
 static hipError_t dispatch_smooth_p1(const AssembleArgs& a, hipStream_t s)
 {
   if (a.debug_flags & 256) return dispatch_kinds<P1Smooth3>(a, s, true);   // A/B: the quadrature policy
-  if (a.tkind == HDD_TENSOR_CONST) return launch_persistent<P1SmoothPolicy<HDD_TENSOR_CONST>>(a, s);
-  if (a.tkind == HDD_TENSOR_ISO_PER_ELEM) return launch_persistent<P1SmoothPolicy<HDD_TENSOR_ISO_PER_ELEM>>(a, s);
+  const int tk = a.tkind;
+  if (a.ev) {
+    if (tk == HDD_TENSOR_CONST) return launch_persistent<P1SmoothPolicy<HDD_TENSOR_CONST, true>>(a, s);
+    if (tk == HDD_TENSOR_ISO_PER_ELEM) return launch_persistent<P1SmoothPolicy<HDD_TENSOR_ISO_PER_ELEM, true>>(a, s);
+    return launch_persistent<P1SmoothPolicy<HDD_TENSOR_SYM_PER_ELEM, true>>(a, s);
+  }
+  if (tk == HDD_TENSOR_CONST) return launch_persistent<P1SmoothPolicy<HDD_TENSOR_CONST>>(a, s);
+  if (tk == HDD_TENSOR_ISO_PER_ELEM) return launch_persistent<P1SmoothPolicy<HDD_TENSOR_ISO_PER_ELEM>>(a, s);
   return launch_persistent<P1SmoothPolicy<HDD_TENSOR_SYM_PER_ELEM>>(a, s);
 }
 

@@ -69,7 +69,7 @@ class LocalInfo(C.Structure):
 class MeshT(C.Structure):
     _fields_ = [("elem_type", C.c_int32), ("degree", C.c_int32), ("n_local", C.c_int64), ("own_begin", C.c_int64),
                 ("own_end", C.c_int64), ("coords", C.c_void_p), ("neighbors", C.c_void_p),
-                ("face_info", C.c_void_p)]
+                ("face_info", C.c_void_p), ("elem_vertices", C.c_void_p), ("vertex_coords", C.c_void_p)]
 
 
 class ScalarFn(C.Structure):
@@ -142,6 +142,7 @@ def lib():
         "hdd_local_get_info": (_I32, [_VP, C.POINTER(LocalInfo)]),
         "hdd_local_fill": (_I32, [_VP, _VP, _VP, _VP, _VP, _VP]),
         "hdd_local_centers": (_I32, [_VP, _VP]),
+        "hdd_local_vertices": (_I32, [_VP, C.POINTER(_I64), _VP, _VP]),
         "hdd_local_halo_plan": (_I32, [_VP, _VP, _I32, C.POINTER(_I32), _VP, _VP, _VP, _VP]),
         "hdd_local_send_list": (_I32, [_VP, _VP, _I32, _I32, _VP]),
         "hdd_checkerboard": (_I32, [_I64, _VP, _VP, _VP, _I32, _I32, _VP, _VP]),
@@ -335,6 +336,16 @@ class LocalMesh:
         _check(lib().hdd_local_centers(self.h, _p(c)), "hdd_local_centers")
         return c
 
+    def vertices(self):
+        """Vertex-indexed geometry (hdd_local_vertices): elem_vertices [nvpe][n_local] int32 local vertex ids,
+        vertex_coords [n_vertices][dim] (distinct vertices of the local elements, ascending global id)."""
+        nv = C.c_int64()
+        _check(lib().hdd_local_vertices(self.h, C.byref(nv), None, None), "hdd_local_vertices")
+        ev = np.empty((self.nvpe, self.n_local), np.int32)
+        xy = np.empty((nv.value, self.dim))
+        _check(lib().hdd_local_vertices(self.h, C.byref(nv), _p(ev), _p(xy)), "hdd_local_vertices")
+        return ev, xy
+
     def checkerboard(self, lower, upper, ncx, ncy, values):
         """dune-stuff Checkerboard at the element barycentres (problems/spe10.hh:151-156 tensor field)."""
         c = self.centers()
@@ -432,9 +443,11 @@ def params_for(degree, dim, vol_order=-1, face_order=-1):
 
 
 class DeviceMesh:
-    """Device copy of a LocalMesh (SoA arrays in HBM)."""
+    """Device copy of a LocalMesh (SoA arrays in HBM).  2d meshes also carry the vertex-indexed geometry
+    (elem_vertices, vertex_coords: what the P1 / Q1 stiffness kernels read) unless vertex_indexed=False or
+    zero_ghosts (ghost geometry then comes only from the halo exchange, into the element-major coords)."""
 
-    def __init__(self, local, device=0, zero_ghosts=False):
+    def __init__(self, local, device=0, zero_ghosts=False, vertex_indexed=True):
         torch = _torch()
         dev = torch.device("cuda", device)
         coords = torch.from_numpy(local.coords).to(dev)
@@ -445,8 +458,15 @@ class DeviceMesh:
         self.neighbors = torch.from_numpy(local.neighbors).to(dev).contiguous()
         self.face_info = torch.from_numpy(local.face_info.view(np.int32)).to(dev).contiguous()
         self.local = local
+        self.elem_vertices = self.vertex_coords = None
+        if vertex_indexed and not zero_ghosts and local.dim == 2:
+            ev, xy = local.vertices()
+            self.elem_vertices = torch.from_numpy(ev).to(dev).contiguous()
+            self.vertex_coords = torch.from_numpy(xy).to(dev).contiguous()
+        vx = self.elem_vertices is not None
         self.t = MeshT(local.elem_type, local.degree, local.n_local, local.own_begin, local.own_end, self.coords.data_ptr(),
-                       self.neighbors.data_ptr(), self.face_info.data_ptr())
+                       self.neighbors.data_ptr(), self.face_info.data_ptr(),
+                       self.elem_vertices.data_ptr() if vx else None, self.vertex_coords.data_ptr() if vx else None)
 
 
 class DevicePattern:

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define HDD_ABI_VERSION 2
+#define HDD_ABI_VERSION 3   /* 3: hdd_mesh vertex-indexed geometry, hdd_local_vertices */
 #define HDD_MAX_COMP 8
 
 typedef enum {
@@ -134,6 +134,13 @@ int hdd_local_fill(const hdd_local* l, double* coords, int32_t* neighbors, uint3
                    int64_t* global_id, int32_t* subdomain);
 /* element barycentres [dim][n_local] (coefficient lookup, e.g. the Spe10 checkerboard) */
 int hdd_local_centers(const hdd_local* l, double* centers);
+/* vertex-indexed geometry of the local elements (owned + ghosts), the grid's own representation (a Dune
+ * grid's vertex set + element -> vertex map): the distinct vertices of the local elements, numbered in
+ * ascending global vertex id, *n_vertices of them;
+ *   elem_vertices [nvpe][n_local]   : local vertex id of vertex k of element e at k*n_local + e
+ *   vertex_coords [n_vertices][dim] : coordinates, interleaved
+ * Call with elem_vertices == vertex_coords == NULL to query *n_vertices. */
+int hdd_local_vertices(const hdd_local* l, int64_t* n_vertices, int32_t* elem_vertices, double* vertex_coords);
 /* halo plan with the subdomain -> rank map `owner` [n_subdomains]:
  *   peers[n_peers] ranks this rank exchanges with (ascending); for peer p: send_count[p] owned elements
  *   whose local ids are listed by hdd_local_send_list(l, p, ...), and recv_count[p] ghost slots starting
@@ -187,6 +194,13 @@ typedef struct hdd_mesh_s {
   const double* coords;       /* device, layout of hdd_local_fill */
   const int32_t* neighbors;   /* device */
   const uint32_t* face_info;  /* device */
+  /* optional vertex-indexed geometry (hdd_local_vertices; both or neither, device): when present, the 2d
+   * P1 / Q1 stiffness kernels read each element's vertices through elem_vertices from vertex_coords and
+   * the neighbour's off-face vertex through its vertex id, instead of the element-major coords (4 B per
+   * element vertex instead of 16; the shared vertex rows stay cache resident).  coords stays required
+   * (right-hand sides, products, 3d, halo geometry). */
+  const int32_t* elem_vertices;  /* [nvpe][n_local] */
+  const double* vertex_coords;   /* [n_vertices][dim] */
 } hdd_mesh;
 
 typedef struct {              /* one diffusion-factor component kappa_q (a Stuff::LocalizableFunction) */

@@ -877,9 +877,18 @@ class SWIPDG {
     d_coords_ = internal::DeviceArray<double>(coords_);
     d_nbrs_ = internal::DeviceArray<int32_t>(nbrs_);
     d_finfo_ = internal::DeviceArray<uint32_t>(finfo_);
+    if (info_.dim == 2) {   // vertex-indexed geometry: what the P1 / Q1 stiffness kernels read
+      int64_t nv = 0;
+      internal::check(hdd_local_vertices(local_, &nv, nullptr, nullptr), "hdd_local_vertices");
+      std::vector<int32_t> ev(size_t(info_.nvpe * linfo_.n_local));
+      std::vector<double> vxy(size_t(2 * nv));
+      internal::check(hdd_local_vertices(local_, &nv, ev.data(), vxy.data()), "hdd_local_vertices");
+      d_ev_ = internal::DeviceArray<int32_t>(ev);
+      d_vxy_ = internal::DeviceArray<double>(vxy);
+    }
     tensor_ = detail::DeviceTensor(problem_.diffusion_tensor, view_);
     mesh_ = hdd_mesh{info_.elem_type, degree_, linfo_.n_local, linfo_.own_begin, linfo_.own_end, d_coords_.get(),
-                     d_nbrs_.get(), d_finfo_.get()};
+                     d_nbrs_.get(), d_finfo_.get(), d_ev_.get(), d_vxy_.get()};
     prm_ = detail::swipdg_params(degree_, info_.dim);
     purely_neumann_ = true;
     for (int f = 0; f < info_.nfaces; ++f)
@@ -1018,6 +1027,8 @@ class SWIPDG {
   std::shared_ptr<Pattern> pattern_;
   std::shared_ptr<const Pattern> volume_pattern_;
   internal::DeviceArray<double> d_coords_;
+  internal::DeviceArray<int32_t> d_ev_;
+  internal::DeviceArray<double> d_vxy_;
   internal::DeviceArray<int32_t> d_nbrs_;
   internal::DeviceArray<uint32_t> d_finfo_;
   detail::DeviceTensor tensor_;

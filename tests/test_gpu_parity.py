@@ -239,8 +239,18 @@ def test_tile_split_overlap(ctx, et, smooth):
     ghosts = torch.ones(local.n_local, dtype=torch.bool, device="cuda")
     ghosts[local.own_begin:local.own_end] = False
     dm.coords[:, ghosts] = float("nan")
+    # the vertex-indexed geometry the kernels read: poison the vertices only ghost elements touch
+    assert dm.elem_vertices is not None
+    ev = dm.elem_vertices.cpu().numpy()
+    own_v = np.zeros(dm.vertex_coords.shape[0], bool)
+    own_v[ev[:, local.own_begin:local.own_end].ravel()] = True
+    ghost_only = torch.from_numpy(~own_v).cuda()
+    assert bool(ghost_only.any())
+    saved_v = dm.vertex_coords.clone()
+    dm.vertex_coords[ghost_only] = float("nan")
     H.assemble_tiles(ctx, dm, dp, kap, ten, torch.from_numpy(t_in).cuda(), [val])
     dm.coords.copy_(saved)
+    dm.vertex_coords.copy_(saved_v)
     H.assemble_tiles(ctx, dm, dp, kap, ten, torch.from_numpy(t_bd).cuda(), [val])
     torch.cuda.synchronize()
     assert torch.equal(val, ref)
@@ -401,6 +411,47 @@ def test_scrambled_quad_orientations(ctx, smooth):
     assert np.array_equal(col, ocol)
     worst, ok = compare_rows(rp, val, oval, RTOL)
     assert ok, worst
+
+
+@pytest.mark.parametrize("case", ["kuhn_spe10", "quad_spe10", "kuhn_sinusoid_sym", "quad_sinusoid", "nvb", "scrambled"])
+def test_vertex_indexed_geometry_equals_element_major(ctx, case):
+    """hdd_mesh elem_vertices / vertex_coords (the default of DeviceMesh and of the shards): the P1 / Q1
+    kernels read the element and neighbour vertices through vertex ids.  Same arithmetic on the same
+    coordinates, so the values must equal those of the element-major coords path bit for bit -- on
+    structured Kuhn / quad meshes (ragged tiles, 2 subdomains), the bisection mesh (reversed faces) and the
+    scrambled quad mesh (every twin face id), piecewise-constant and sinusoid (C3) diffusion factors."""
+    torch = _torch()
+    rng = np.random.default_rng(17)
+    if case in ("nvb", "scrambled"):
+        if case == "nvb":
+            from mesh_tools import nvb_mesh
+            et, coords, ev = nvb_mesh(4, 3)
+        else:
+            et, coords, ev = _scrambled_quad_mesh(130, 20, 5)
+        grid = H.Grid.from_connectivity(et, coords, ev)
+    else:
+        et = H.SIMPLEX if case.startswith("kuhn") else H.CUBE
+        grid = H.Grid.structured(et, 157, 43, (0, 0), (5, 1), px=2, py=1)
+    local = grid.local()
+    ne = local.n_local
+    if "sym" in case:
+        t = np.stack([rng.uniform(0.5, 2.0, ne), rng.uniform(-0.3, 0.3, ne), rng.uniform(0.5, 2.0, ne)], 0)
+        ten = H.tensor_fn(H.TENSOR_SYM_PER_ELEM, per_elem=torch.from_numpy(np.ascontiguousarray(t)).cuda())
+    else:
+        ten = H.tensor_fn(H.TENSOR_ISO_PER_ELEM, per_elem=torch.from_numpy(10.0 ** rng.uniform(-3, 3, ne)).cuda())
+    if "sinusoid" in case:
+        fns = [H.scalar_fn(H.FN_SINUSOID, 1.0, 0.75, 4 * np.pi, 2 * np.pi, order=3)]
+    else:
+        fns = [H.scalar_fn(H.FN_PER_ELEM, per_elem=torch.from_numpy(rng.uniform(0.2, 5.0, ne)).cuda())]
+    dp = H.DevicePattern(local)
+    vals = []
+    for vx in (True, False):
+        dm = H.DeviceMesh(local, vertex_indexed=vx)
+        assert (dm.elem_vertices is not None) == vx
+        (v,) = H.assemble(ctx, dm, dp, fns, ten)
+        torch.cuda.synchronize()
+        vals.append(v)
+    assert torch.equal(vals[0], vals[1])
 
 
 @pytest.mark.parametrize("nnz,n_comp,n_s,stride_pad", [(1001, 3, 40, 6), (75460608 // 64, 2, 33, 0), (7, 1, 1, 2)])
