@@ -60,12 +60,19 @@ __device__ __forceinline__ void compute(const Args& a, const double* ov, const d
   for (int j = 0; j < RB; ++j) img[j] = acc[j % NO] + double(j);
 }
 
+__device__ int g_sched;   // 0: XCD eighths (production); 1: global round robin; 2: per-window XCD slices
 __device__ __forceinline__ void sched(long ntiles, long& t, long& t_end, long& step)
 {
   const long G = gridDim.x, b = blockIdx.x, x = b & 7, w = b >> 3, gx = G >> 3;
-  t = (ntiles * x) / 8 + w;
-  t_end = (ntiles * (x + 1)) / 8;
-  step = gx;
+  if (g_sched == 1) {
+    t = b; t_end = ntiles; step = G;
+  } else if (g_sched == 2) {   // window k = tiles [k G, (k+1) G); XCD x takes slice [x G/8, (x+1) G/8) of it
+    t = x * gx + w; t_end = ntiles; step = G;
+  } else {
+    t = (ntiles * x) / 8 + w;
+    t_end = (ntiles * (x + 1)) / 8;
+    step = gx;
+  }
 }
 
 template <int AUX>
@@ -161,6 +168,21 @@ __global__ void __launch_bounds__(128, 1) split(const Args a)
 }
 
 template <int AUX>
+__global__ void fillchunks(const Args a)
+{
+  const int lane = threadIdx.x;
+  const long G = gridDim.x, nchunks = a.ntiles * IMG / 128;   // 1 KB = 128 doubles per wave instruction
+  __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(a.out, (short)0, 0x7fffffff, 0x00020000);
+  for (long c = blockIdx.x; c < nchunks; c += G) {
+    const dvec2 v = {double(c), 1.0};
+    const long off = (c * 128 + 2 * lane) * 8;
+    double* p = a.out + c * 128 + 2 * lane;
+    __builtin_nontemporal_store(v, reinterpret_cast<dvec2*>(p));
+    (void)off; (void)r;
+  }
+}
+
+template <int AUX>
 __global__ void storeonly(const Args a)
 {
   __shared__ __attribute__((aligned(16))) double lds[IMG];
@@ -207,26 +229,19 @@ int main()
     fflush(stdout);
   };
   char nm[128];
-  auto sweep = [&](auto aux) {
-    constexpr int AUX = decltype(aux)::value;
-    snprintf(nm, sizeof nm, "storeonly aux=%d wg/cu=4", AUX);
-    time(nm, [&] { hipLaunchKernelGGL(storeonly<AUX>, dim3(cus * 4), dim3(64), 0, 0, a); });
+  for (int sc : {0, 1, 2}) {
+    hipMemcpyToSymbol(HIP_SYMBOL(g_sched), &sc, sizeof(int));
     for (int wg : {4, 8}) {
-      snprintf(nm, sizeof nm, "mono  aux=%d wg/cu=%d", AUX, wg);
-      time(nm, [&] { hipLaunchKernelGGL(mono<AUX>, dim3(cus * wg), dim3(64), 0, 0, a); });
+      snprintf(nm, sizeof nm, "storeonly sched=%d wg/cu=%d", sc, wg);
+      time(nm, [&] { hipLaunchKernelGGL(storeonly<2>, dim3(cus * wg), dim3(64), 0, 0, a); });
+      snprintf(nm, sizeof nm, "mono      sched=%d wg/cu=%d", sc, wg);
+      time(nm, [&] { hipLaunchKernelGGL(mono<2>, dim3(cus * wg), dim3(64), 0, 0, a); });
     }
-    snprintf(nm, sizeof nm, "split aux=%d wg/cu=4", AUX);
-    time(nm, [&] { hipLaunchKernelGGL(split<AUX>, dim3(cus * 4), dim3(128), 0, 0, a); });
-  };
-  // cache-policy bits of the store (gfx950): sc0 = 1, nt = 2, sc1 = 16
-  a.work = 0;
-  sweep(std::integral_constant<int, 2>());
-  sweep(std::integral_constant<int, 0>());
-  sweep(std::integral_constant<int, 16>());
-  sweep(std::integral_constant<int, 17>());
-  sweep(std::integral_constant<int, 18>());
-  sweep(std::integral_constant<int, 19>());
-  sweep(std::integral_constant<int, 1>());
+  }
+  for (int wg : {4, 8, 16}) {
+    snprintf(nm, sizeof nm, "fillchunks 1KB nt wg/cu=%d", wg);
+    time(nm, [&] { hipLaunchKernelGGL(fillchunks<2>, dim3(cus * wg), dim3(64), 0, 0, a); });
+  }
   // correctness of the split image: tile 5, element 3, value 7
   std::vector<double> o(IMG);
   hipMemcpy(o.data(), out + 5 * IMG, IMG * 8, hipMemcpyDeviceToHost);
