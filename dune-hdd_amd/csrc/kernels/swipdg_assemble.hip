@@ -1730,7 +1730,7 @@ swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
     // second gather stage of tile t+1 (vertex-indexed geometry: the neighbours' off-face vertices by the
     // ids the first stage brought): its wait covers the first stage only, which was issued before the
     // stores of tile t (vmcnt is in order), so it never waits for those stores
-    P::load_gat2(a, gat_n);
+    if (!HDD_ABL(a, 4)) P::load_gat2(a, gat_n);   // (ablation 4: no stage-1 ids to follow)
     if (!has_next) break;
     t = tn;
     e = en;

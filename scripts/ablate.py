@@ -34,16 +34,21 @@ def workload(cfg, ctx):
 
 def main():
     groups = sys.argv[1:] or ["c2:0", "c4:0"]
-    ctx = H.Context(0)
+    # the debug flags are read once per context (hdd_ctx_create): one context per flag value
+    ctxs = {}
     runs = []
     for g in groups:
         cfg, fl = g.split(":")
-        fn = workload(cfg, ctx)
-        runs += [(cfg, int(f), fn) for f in fl.split(",")]
+        for f in fl.split(","):
+            f = int(f)
+            if f not in ctxs:
+                os.environ["HDD_DEBUG_FLAGS"] = str(f)
+                ctxs[f] = H.Context(0)
+            runs.append((cfg, f, workload(cfg, ctxs[f])))
+    os.environ["HDD_DEBUG_FLAGS"] = "0"
     res = {(c, f): [] for c, f, _ in runs}
     for rnd in range(6):
         for cfg, f, fn in runs:
-            os.environ["HDD_DEBUG_FLAGS"] = str(f)
             for _ in range(3):
                 fn()
             ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
@@ -53,7 +58,6 @@ def main():
             ev[1].record()
             torch.cuda.synchronize()
             res[(cfg, f)].append(ev[0].elapsed_time(ev[1]) / 10)
-    os.environ["HDD_DEBUG_FLAGS"] = "0"
     for cfg, f, _ in runs:
         r = res[(cfg, f)]
         print("%s flags=%-3d median %.4f ms  min %.4f ms" % (cfg, f, np.median(r), np.min(r)), flush=True)
