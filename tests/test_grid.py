@@ -171,3 +171,31 @@ def test_indicator_first_closed_box():
     ref = O.indicator(pts.T, boxes)
     assert np.array_equal(got, ref)
     assert got[0] == 2000.0 and got[1] == -1000.0 and got[2] == -1000.0 and got[3] == 2000.0
+
+
+@pytest.mark.parametrize("case", ["kuhn", "quad", "nvb", "kuhn_slice"])
+def test_local_vertices_reproduce_element_coords(case):
+    """hdd_local_vertices (ABI v3, the vertex-indexed geometry the P1 kernels read): every element's vertices
+    through elem_vertices -> vertex_coords equal the element-major coords exactly, owned and ghost columns;
+    the local vertex set is the distinct vertices of the local elements in ascending global id."""
+    if case == "nvb":
+        et, coords, ev = nvb_mesh(3, 2)
+        g = H.Grid.from_connectivity(et, coords, ev)
+        loc = g.local()
+    else:
+        et = H.CUBE if case == "quad" else H.SIMPLEX
+        g = H.Grid.structured(et, 23, 9, (0, 0), (5, 1), px=3, py=1)
+        loc = g.local(1, 2) if case == "kuhn_slice" else g.local()
+    lev, lxy = loc.vertices()
+    assert lev.shape == (loc.nvpe, loc.n_local) and lxy.shape[1] == 2
+    for k in range(loc.nvpe):
+        assert np.array_equal(lxy[lev[k], 0], loc.coords[2 * k])
+        assert np.array_equal(lxy[lev[k], 1], loc.coords[2 * k + 1])
+    used = np.zeros(lxy.shape[0], bool)
+    used[lev.ravel()] = True
+    assert used.all()                                                  # no unused vertex rows
+    gcoords, gev, _ = g.connectivity()
+    gids = np.unique(gev[loc.global_id].ravel())                       # ascending global ids
+    assert np.array_equal(lxy, gcoords[gids])
+    if case == "kuhn_slice":
+        assert loc.n_ghost > 0
