@@ -1286,9 +1286,11 @@ template <int TK, int KK, bool PEN = false, bool VX = false>
 struct P1PwcPolicy {
   static constexpr int NB = 3, NF = 3;
   static constexpr int RB = 36;
-  // store-bound: 8 tiles per CU since the out-of-line pow (191 VGPRs, 2 waves per SIMD): C2 0.310 / 0.305
-  // vs 0.312 / 0.314 ms at 4 (profiles/r01/s3/sweep_wgcu_s3.log; 4 was best at 226 VGPRs)
-  static constexpr int WGCU = 8, MINW = 1;
+  // store-bound.  Element-major geometry: 8 tiles per CU since the out-of-line pow (191 VGPRs, 2 waves per
+  // SIMD): C2 0.310 / 0.305 vs 0.312 / 0.314 ms at 4 (profiles/r01/s3/sweep_wgcu_s3.log).  Vertex-indexed
+  // geometry: 4 (one wave per SIMD): C2 0.230-0.237 ms vs 0.246-0.247 at 8, 0.242 at 6, 0.256 at 3
+  // (same box, profiles/r02/s2/ab_wgcu_vx*)
+  static constexpr int WGCU = VX ? 4 : 8, MINW = 1;
   static constexpr bool PAD = false;          // store-bound: its 4-way write conflicts stay hidden
   using Own = P1Own;
   using Gat = P1Gat;

@@ -13,6 +13,8 @@ typedef int ivec4 __attribute__((ext_vector_type(4)));
 constexpr int RB = 36, IMG = 64 * RB, STORES = (IMG / 2 + 63) / 64;
 
 struct Args {
+  const ivec4* vf4;       // [n] (v0, v1, v2, finfo)
+  const ivec4* nb4;       // [n] (nb0, nb1, nb2, 0)
   const double* tiled;    // [ntiles][7][64] doubles: X0 Y0 X1 Y1 X2 Y2 k
   const int* tiledi;      // [ntiles][4][64] ints: nb0 nb1 nb2 finfo
   const double* coords;   // [6][n] element-major
@@ -182,6 +184,46 @@ __global__ void __launch_bounds__(64, 1) vertex_indexed(const Args a)
   }
 }
 
+// ---- vertex-indexed, packed per-element ints (AoS int4): vid + finfo in one 16-B load, nbr in another ----
+template <bool NB4>
+__device__ __forceinline__ void own_p(const Args& a, long e, OwnV& o)
+{
+  const ivec4 vf = a.vf4[e];
+  o.v[0] = vf.x; o.v[1] = vf.y; o.v[2] = vf.z; o.fi = unsigned(vf.w);
+  if constexpr (NB4) {
+    const ivec4 nb = a.nb4[e];
+    o.nb[0] = nb.x; o.nb[1] = nb.y; o.nb[2] = nb.z;
+  } else {
+#pragma unroll
+    for (int f = 0; f < 3; ++f) o.nb[f] = a.nbr[f * a.n + e];
+  }
+  o.k = a.tper[e];
+}
+template <bool NB4>
+__global__ void __launch_bounds__(64, 1) vertex_packed(const Args a)
+{
+  __shared__ __attribute__((aligned(16))) double lds[IMG];
+  const int lane = threadIdx.x;
+  long t, t_end, step; sched(a.ntiles, t, t_end, step);
+  if (t >= t_end) return;
+  OwnV o; Gat1 g1; Gat2 g2;
+  own_p<NB4>(a, t * 64 + lane, o); gat1(a, t * 64 + lane, o, g1); gat2(a, g1, g2);
+  for (;;) {
+    const bool more = t + step < t_end; const long tn = more ? t + step : t;
+    OwnV on; own_p<NB4>(a, tn * 64 + lane, on);
+    double X[3], Y[3], Ox[3], Oy[3];
+#pragma unroll
+    for (int v = 0; v < 3; ++v) { X[v] = g1.P[v].x; Y[v] = g1.P[v].y; Ox[v] = g2.O[v].x; Oy[v] = g2.O[v].y; }
+    comp(X, Y, o.k, Ox, Oy, g1.kn, lds + lane * RB);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); __builtin_amdgcn_wave_barrier(); __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    Gat1 g1n; gat1(a, tn * 64 + lane, on, g1n);
+    store_tile(a, t, lds, lane);
+    Gat2 g2n; gat2(a, g1n, g2n);
+    if (!more) break;
+    t = tn; o = on; g1 = g1n; g2 = g2n;
+  }
+}
+
 int main()
 {
   const long nx = 3200, ny = 640, n = nx * ny * 2, ntiles = n / 64, nv = (nx + 1) * (ny + 1);
@@ -228,6 +270,15 @@ int main()
   hipMemcpy(dtl, tiled.data(), tiled.size() * 8, hipMemcpyHostToDevice);
   hipMemcpy(dti, tiledi.data(), tiledi.size() * 4, hipMemcpyHostToDevice);
   a.tiled = dtl; a.tiledi = dti;
+  std::vector<ivec4> vf4(n), nb4(n);
+  for (long e = 0; e < n; ++e) {
+    vf4[e] = ivec4{vid[e], vid[n + e], vid[2 * n + e], int(fi[e])};
+    nb4[e] = ivec4{nbr[e], nbr[n + e], nbr[2 * n + e], 0};
+  }
+  ivec4 *dvf4, *dnb4;
+  hipMalloc(&dvf4, n * 16); hipMalloc(&dnb4, n * 16);
+  hipMemcpy(dvf4, vf4.data(), n * 16, hipMemcpyHostToDevice); hipMemcpy(dnb4, nb4.data(), n * 16, hipMemcpyHostToDevice);
+  a.vf4 = dvf4; a.nb4 = dnb4;
   a.coords = dc; a.tper = dt; a.vid = dv; a.nbr = dn; a.finfo = df; a.xy = dxy; a.out = dout;
   int cus = 0; hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
   hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
@@ -243,15 +294,17 @@ int main()
   std::vector<double> o1(ntiles * IMG), o2(ntiles * IMG);
   hipLaunchKernelGGL(elem_major, dim3(cus * 8), dim3(64), 0, 0, a); hipDeviceSynchronize();
   hipMemcpy(o1.data(), dout, o1.size() * 8, hipMemcpyDeviceToHost);
-  for (int v = 0; v < 2; ++v) {
+  for (int v = 0; v < 4; ++v) {
     hipMemset(dout, 0, o2.size() * 8);
     if (v == 0) hipLaunchKernelGGL(vertex_indexed, dim3(cus * 8), dim3(64), 0, 0, a);
-    else hipLaunchKernelGGL(elem_tiled, dim3(cus * 8), dim3(64), 0, 0, a);
+    else if (v == 1) hipLaunchKernelGGL(elem_tiled, dim3(cus * 8), dim3(64), 0, 0, a);
+    else if (v == 2) hipLaunchKernelGGL(vertex_packed<false>, dim3(cus * 8), dim3(64), 0, 0, a);
+    else hipLaunchKernelGGL(vertex_packed<true>, dim3(cus * 8), dim3(64), 0, 0, a);
     hipDeviceSynchronize();
     hipMemcpy(o2.data(), dout, o2.size() * 8, hipMemcpyDeviceToHost);
     long diff = 0;
     for (size_t i = 0; i < o1.size(); ++i) diff += o1[i] != o2[i];
-    printf("%s outputs differing from element-major: %ld of %zu\n", v == 0 ? "vertex-indexed" : "tile-blocked", diff, o1.size());
+    printf("variant %d outputs differing from element-major: %ld of %zu\n", v, diff, o1.size());
   }
   for (int rep = 0; rep < 3; ++rep)
     for (int wg : {4, 8}) {
@@ -260,6 +313,10 @@ int main()
       time(nm, [&] { hipLaunchKernelGGL(elem_major, dim3(cus * wg), dim3(64), 0, 0, a); });
       snprintf(nm, sizeof nm, "tile-blocked wg/cu=%d", wg);
       time(nm, [&] { hipLaunchKernelGGL(elem_tiled, dim3(cus * wg), dim3(64), 0, 0, a); });
+      snprintf(nm, sizeof nm, "vx packed vid+fi wg/cu=%d", wg);
+      time(nm, [&] { hipLaunchKernelGGL(vertex_packed<false>, dim3(cus * wg), dim3(64), 0, 0, a); });
+      snprintf(nm, sizeof nm, "vx packed vid+fi, nb wg/cu=%d", wg);
+      time(nm, [&] { hipLaunchKernelGGL(vertex_packed<true>, dim3(cus * wg), dim3(64), 0, 0, a); });
       snprintf(nm, sizeof nm, "vertex-indexed wg/cu=%d", wg);
       time(nm, [&] { hipLaunchKernelGGL(vertex_indexed, dim3(cus * wg), dim3(64), 0, 0, a); });
     }
