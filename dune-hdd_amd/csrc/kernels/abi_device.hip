@@ -28,6 +28,8 @@ struct hdd_ctx {
   int wgcu = 0;             // HDD_P1_WGCU: tiles-per-CU sweep override (0: the policy's measured value)
   int q3g_reps = 0;         // HDD_Q3G_REPS: workgroups per (XCD, row quad) of the p=3 GEMM kernel (0: by CU count)
   double* q3g_tab = nullptr;   // p=3 reference matrices [Q3G_K][4096], uploaded on first use
+  void* scan_ws = nullptr;     // device-pattern row-length scan scratch (kept: no allocation per build)
+  size_t scan_ws_bytes = 0;
 };
 
 int hdd::ctx_device(const hdd_ctx* ctx) { return ctx ? ctx->device : 0; }
@@ -81,6 +83,7 @@ extern "C" void hdd_ctx_destroy(hdd_ctx* ctx)
 {
   if (ctx && ctx->ws) (void)hipFree(ctx->ws);
   if (ctx && ctx->q3g_tab) (void)hipFree(ctx->q3g_tab);
+  if (ctx && ctx->scan_ws) (void)hipFree(ctx->scan_ws);
   delete ctx;
 }
 
@@ -570,12 +573,17 @@ extern "C" int hdd_pattern_elem_ptr_device(hdd_ctx* ctx, const hdd_mesh* m, int3
     size_t tmp_bytes = 0;
     e = hipcub::DeviceScan::InclusiveSum(nullptr, tmp_bytes, d_elem_ptr + 1, d_elem_ptr + 1, n_own, s);
     if (e != hipSuccess) return hip_fail(e, "hdd_pattern_elem_ptr_device: scan size");
-    void* tmp = nullptr;
-    e = hipMalloc(&tmp, tmp_bytes);
-    if (e != hipSuccess) return hip_fail(e, "hdd_pattern_elem_ptr_device: scan scratch");
-    e = hipcub::DeviceScan::InclusiveSum(tmp, tmp_bytes, d_elem_ptr + 1, d_elem_ptr + 1, n_own, s);
+    if (tmp_bytes > ctx->scan_ws_bytes) {   // the context keeps the scratch (one stream at a time per context)
+      (void)hipStreamSynchronize(s);
+      if (ctx->scan_ws) (void)hipFree(ctx->scan_ws);
+      ctx->scan_ws = nullptr;
+      ctx->scan_ws_bytes = 0;
+      e = hipMalloc(&ctx->scan_ws, tmp_bytes);
+      if (e != hipSuccess) return hip_fail(e, "hdd_pattern_elem_ptr_device: scan scratch");
+      ctx->scan_ws_bytes = tmp_bytes;
+    }
+    e = hipcub::DeviceScan::InclusiveSum(ctx->scan_ws, tmp_bytes, d_elem_ptr + 1, d_elem_ptr + 1, n_own, s);
     const hipError_t e2 = hipStreamSynchronize(s);
-    (void)hipFree(tmp);
     if (e != hipSuccess) return hip_fail(e, "hdd_pattern_elem_ptr_device: scan");
     if (e2 != hipSuccess) return hip_fail(e2, "hdd_pattern_elem_ptr_device: synchronize");
   }
@@ -838,6 +846,12 @@ extern "C" int hdd_product_assemble(hdd_ctx* ctx, const hdd_mesh* m, int32_t pro
     f.n_cu = ctx->n_cu;
     f.debug_flags = ctx->debug_flags;
     f.wgcu = ctx->wgcu;
+    if (!m->elem_vertices != !m->vertex_coords)
+      return set_error(HDD_ERR_INVALID, "hdd_product_assemble: mesh elem_vertices / vertex_coords: both or neither");
+    if (m->elem_vertices && m->elem_type == HDD_SIMPLEX && !(ctx->debug_flags & 16384)) {
+      f.ev = m->elem_vertices;   // vertex-indexed geometry, as hdd_swipdg_assemble
+      f.vxy = m->vertex_coords;
+    }
     bool fast = false;
     e = launch_product_fast(f, product, static_cast<hipStream_t>(stream), &fast);
     if (fast) return e == hipSuccess ? HDD_OK : hip_fail(e, "hdd_product_assemble: launch");

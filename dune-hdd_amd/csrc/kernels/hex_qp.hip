@@ -1093,6 +1093,19 @@ __device__ __forceinline__ int lanes_below(uint64_t m)
 }
 
 template <int NB, int NF>
+struct PatTile {
+  int32_t nb[NF];   // local neighbour ids (< 0: boundary)
+  int64_t own;      // global id of the element
+};
+
+// Software-pipelined like swipdg_persistent_kernel (gfx950's vmcnt is in order and counts stores): per
+// wave a sequence of tiles, memory order [own data of tile t+1][sort + LDS image of t][neighbour global ids
+// of t+1][stores of t].  The tile's row_ptr entries are staged in LDS and written with coalesced 8-byte
+// stores (a lane's three or four consecutive entries would be 24 / 32 bytes apart); the column range goes
+// out as aligned 16-byte non-temporal buffer stores (head / tail ints separately, so no store straddles
+// the range); uniform tiles (64 elements with NF interior faces: 16-byte aligned row blocks) are staged with
+// 16-byte LDS writes.
+template <int NB, int NF>
 __global__ void __launch_bounds__(64) pattern_fill_tile_kernel(const int32_t* __restrict__ nbrs, int64_t n_local,
                                                                int64_t own_begin, int64_t n_own,
                                                                const int64_t* __restrict__ gid,
@@ -1101,21 +1114,52 @@ __global__ void __launch_bounds__(64) pattern_fill_tile_kernel(const int32_t* __
                                                                int64_t n_tiles)
 {
   constexpr int RB = (NF + 1) * NB * NB;
+  constexpr int CH = (64 * RB + 3) / 4;           // 16-byte chunks of a full tile image
+  constexpr int CPL = (CH + 63) / 64;             // chunk stores per lane
   __shared__ __attribute__((aligned(16))) int32_t img[64 * RB + 8 + RB];
+  __shared__ int64_t rps[64 * NB];
   typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
   const int lane = threadIdx.x;
-  for (int64_t t = blockIdx.x; t < n_tiles; t += gridDim.x) {
+  int64_t t = blockIdx.x;
+  if (t >= n_tiles) return;
+  const int64_t step = gridDim.x;
+  auto load_own = [&](int64_t tt, PatTile<NB, NF>& p) {
+    const int64_t k = tt * 64 + lane;
+    const int64_t e = own_begin + (k < n_own ? k : tt * 64);
+#pragma unroll
+    for (int f = 0; f < NF; ++f) p.nb[f] = nbrs[f * n_local + e];
+    p.own = gid ? gid[e] : e;
+  };
+  auto load_keys = [&](const PatTile<NB, NF>& p, int64_t* nk) {
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+      const int32_t n = p.nb[f];
+      nk[f] = n >= 0 ? (gid ? gid[n] : int64_t(n)) : INT64_MAX;
+    }
+  };
+  PatTile<NB, NF> cur;
+  int64_t nk[NF];
+  load_own(t, cur);
+  load_keys(cur, nk);
+  for (;;) {
+    const bool has_next = t + step < n_tiles;
+    const int64_t tn = has_next ? t + step : t;
+    PatTile<NB, NF> nxt;
+    load_own(tn, nxt);
+
     const int64_t k0 = t * 64, k = k0 + lane;
     const bool active = k < n_own;
-    const int64_t e = own_begin + (active ? k : k0);
+    const int64_t kend = k0 + 64 < n_own ? k0 + 64 : n_own;
+    const int nact = int(kend - k0);
+    const int64_t base = __builtin_amdgcn_readfirstlane(elem_ptr[k0]);
+    const int64_t tend = __builtin_amdgcn_readfirstlane(elem_ptr[kend]);
     int64_t key[NF + 1];
-    key[0] = gid ? gid[e] : e;
+    key[0] = cur.own;
     int nblk = 1;
 #pragma unroll
     for (int f = 0; f < NF; ++f) {
-      const int32_t nf = nbrs[f * n_local + e];
-      key[f + 1] = nf >= 0 ? (gid ? gid[nf] : int64_t(nf)) : INT64_MAX;
-      nblk += nf >= 0;
+      key[f + 1] = nk[f];
+      nblk += cur.nb[f] >= 0;
     }
 #pragma unroll
     for (int i = 0; i < NF; ++i)   // sorting network (bubble, compile-time)
@@ -1126,9 +1170,6 @@ __global__ void __launch_bounds__(64) pattern_fill_tile_kernel(const int32_t* __
         key[j] = lo;
         key[j + 1] = hi;
       }
-    const int64_t kend = k0 + 64 < n_own ? k0 + 64 : n_own;
-    const int64_t base = __builtin_amdgcn_readfirstlane(elem_ptr[k0]);
-    const int64_t tend = __builtin_amdgcn_readfirstlane(elem_ptr[kend]);
     const int64_t al = base & ~int64_t(3);
     const int c = nblk - 1;
     int sum = lanes_below(__ballot(active));
@@ -1139,34 +1180,71 @@ __global__ void __launch_bounds__(64) pattern_fill_tile_kernel(const int32_t* __
     const int rl = NB * nblk;
     if (active) {
 #pragma unroll
-      for (int i = 0; i < NB; ++i) row_ptr[k * NB + i] = base + off + i * rl;
-      if (k == n_own - 1) row_ptr[n_own * NB] = base + off + NB * rl;
+      for (int i = 0; i < NB; ++i) rps[lane * NB + i] = base + off + i * rl;
     }
-    int32_t* my = active ? img + (base - al) + off : img + 64 * RB + 8;
+    const bool uni = nact == 64 && tend - base == int64_t(64) * RB && base == al;   // wave-uniform
+    if (uni) {   // row block of lane = 16-byte aligned at lane * RB: NB rows x (NF + 1) blocks x NB ints
+      i32x4* my = reinterpret_cast<i32x4*>(img + lane * RB);
 #pragma unroll
-    for (int i = 0; i < NB; ++i)
+      for (int q = 0; q < RB / 4; ++q) {
+        i32x4 v;
 #pragma unroll
-      for (int b = 0; b <= NF; ++b)
-        if (b < nblk)
+        for (int u = 0; u < 4; ++u) {
+          const int m = 4 * q + u, j = m % NB, b = (m / NB) % (NF + 1);
+          v[u] = int32_t(key[b] * NB + j);
+        }
+        my[q] = v;
+      }
+    } else {
+      int32_t* my = active ? img + (base - al) + off : img + 64 * RB + 8;
 #pragma unroll
-          for (int j = 0; j < NB; ++j) my[i * rl + b * NB + j] = int32_t(key[b] * NB + j);
+      for (int i = 0; i < NB; ++i)
+#pragma unroll
+        for (int b = 0; b <= NF; ++b)
+          if (b < nblk)
+#pragma unroll
+            for (int j = 0; j < NB; ++j) my[i * rl + b * NB + j] = int32_t(key[b] * NB + j);
+    }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const int64_t n16 = (tend - al + 3) >> 2;
-    for (int64_t q = lane; q < n16; q += 64) {
-      const int64_t g0 = al + 4 * q;
-      if (g0 >= base && g0 + 4 <= tend) {
-        __builtin_nontemporal_store(*reinterpret_cast<const i32x4*>(img + 4 * q), reinterpret_cast<i32x4*>(col + g0));
-      } else {
+
+    int64_t nk_n[NF];
+    load_keys(nxt, nk_n);
+
+    // row_ptr of the tile's rows: contiguous, coalesced
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
-          if (g0 + u >= base && g0 + u < tend) col[g0 + u] = img[4 * q + u];
+    for (int m = 0; m < NB; ++m) {
+      const int idx = lane + 64 * m;
+      if (idx < nact * NB) row_ptr[k0 * NB + idx] = rps[idx];
+    }
+    if (k == n_own - 1) row_ptr[n_own * NB] = tend;
+    // columns: head ints [base, a0), aligned middle [a0, a1) in 16-byte chunks, tail [a1, tend)
+    const int64_t a0 = (base + 3) & ~int64_t(3), a1 = tend & ~int64_t(3);
+    if (a0 >= a1) {   // short range (tiny tiles): plain ints
+      for (int64_t g = base + lane; g < tend; g += 64) col[g] = img[g - al];
+    } else {
+      if (lane < a0 - base) col[base + lane] = img[base - al + lane];
+      if (lane < tend - a1) col[a1 + lane] = img[a1 - al + lane];
+      const int nbytes = int(a1 - a0) * 4;
+      __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(col + a0, (short)0, nbytes, 0x00020000);
+      const int32_t* src = img + (a0 - al);
+#pragma unroll
+      for (int u = 0; u < CPL; ++u) {
+        const int m = lane + 64 * u;
+        const int li = 4 * m < 64 * RB + 4 ? 4 * m : 0;
+        const i32x4 v = *reinterpret_cast<const i32x4*>(src + li);
+        __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, m * 16, 0, 2);   // out-of-range chunks dropped
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (!has_next) break;
+    t = tn;
+    cur = nxt;
+#pragma unroll
+    for (int f = 0; f < NF; ++f) nk[f] = nk_n[f];
   }
 }
 

@@ -1471,7 +1471,7 @@ struct P1SmoothPolicy {
 //   boundary l2: sum over boundary faces of |F| (1/3, 1/6) on the face vertices.
 // Row block = nb x nb (no neighbour blocks), so tiles are 64 nb^2 doubles and no gathers are needed.
 // ------------------------------------------------------------------------------------------------
-template <class E, int KIND, int TK, int KK>
+template <class E, int KIND, int TK, int KK, int VX = 0>   // VX: vertex-indexed geometry (P1 / Q1 kernels' VX)
 struct VolProductPolicy {
   static constexpr int NB = E::NB, NF = E::NF, NV = E::NV;
   static constexpr int RB = NB * NB;
@@ -1482,22 +1482,23 @@ struct VolProductPolicy {
     int32_t nbr[NF];
     Tensor A;
     double ke;
+    int32_t vid[NV];
   };
   struct Gat {};
+  static constexpr int NVL = KIND == HDD_PRODUCT_BOUNDARY_L2 ? NV : 3;   // vertices read (0, 1, 2 span the map)
   __device__ static void load_own(const AssembleArgs& a, int64_t e, Own& o)
   {
     const int64_t ne = a.n_local;
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {   // vertices 0, 1, 2 span the affine map
-      o.X[k] = a.coords[(2 * k) * ne + e];
-      o.Y[k] = a.coords[(2 * k + 1) * ne + e];
-    }
-    if constexpr (KIND == HDD_PRODUCT_BOUNDARY_L2) {
-#pragma unroll
-      for (int k = 3; k < NV; ++k) {
+    for (int k = 0; k < NVL; ++k) {
+      if constexpr (VX != 0) {
+        o.vid[k] = a.ev[k * ne + e];
+      } else {
         o.X[k] = a.coords[(2 * k) * ne + e];
         o.Y[k] = a.coords[(2 * k + 1) * ne + e];
       }
+    }
+    if constexpr (KIND == HDD_PRODUCT_BOUNDARY_L2) {
 #pragma unroll
       for (int f = 0; f < NF; ++f) o.nbr[f] = a.nbrs[f * ne + e];
     }
@@ -1506,7 +1507,13 @@ struct VolProductPolicy {
       o.ke = kappa_k<KK>(a, e);
     }
   }
-  __device__ static void load_gat(const AssembleArgs&, int64_t, const Own&, Gat&) {}
+  __device__ static void load_gat(const AssembleArgs& a, int64_t, Own& o, Gat&)
+  {
+    if constexpr (VX != 0) {
+#pragma unroll
+      for (int k = 0; k < NVL; ++k) vertex_xy(a, o.vid[k], o.X[k], o.Y[k]);
+    }
+  }
   __device__ static void load_gat2(const AssembleArgs&, Gat&) {}
   __device__ static int n_interior(const Own&) { return 0; }
 
@@ -1885,25 +1892,34 @@ static hipError_t launch_components(const AssembleArgs& a, int nqv, int nqf, hip
 // products (hdd_product_assemble) on the persistent driver: P1 / Q1 with piecewise-constant kappa; the
 // caller falls back to the generic product kernel (rhs.hip) for smooth kappa and hexahedra
 // ------------------------------------------------------------------------------------------------
-template <class E, int KIND>
-static hipError_t launch_vol_product(const AssembleArgs& a, hipStream_t s)
+template <class E, int KIND, int VX>
+static hipError_t launch_vol_product_vx(const AssembleArgs& a, hipStream_t s)
 {
   if constexpr (KIND != HDD_PRODUCT_ELLIPTIC) {
-    return launch_persistent<VolProductPolicy<E, KIND, HDD_TENSOR_CONST, HDD_FN_CONST>>(a, s);
+    return launch_persistent<VolProductPolicy<E, KIND, HDD_TENSOR_CONST, HDD_FN_CONST, VX>>(a, s);
   } else {
     const bool pe = a.kappa[0].kind == HDD_FN_PER_ELEM;
     if (a.tkind == HDD_TENSOR_CONST)
-      return pe ? launch_persistent<VolProductPolicy<E, KIND, HDD_TENSOR_CONST, HDD_FN_PER_ELEM>>(a, s)
-                : launch_persistent<VolProductPolicy<E, KIND, HDD_TENSOR_CONST, HDD_FN_CONST>>(a, s);
+      return pe ? launch_persistent<VolProductPolicy<E, KIND, HDD_TENSOR_CONST, HDD_FN_PER_ELEM, VX>>(a, s)
+                : launch_persistent<VolProductPolicy<E, KIND, HDD_TENSOR_CONST, HDD_FN_CONST, VX>>(a, s);
     if (a.tkind == HDD_TENSOR_ISO_PER_ELEM)
-      return pe ? launch_persistent<VolProductPolicy<E, KIND, HDD_TENSOR_ISO_PER_ELEM, HDD_FN_PER_ELEM>>(a, s)
-                : launch_persistent<VolProductPolicy<E, KIND, HDD_TENSOR_ISO_PER_ELEM, HDD_FN_CONST>>(a, s);
-    return pe ? launch_persistent<VolProductPolicy<E, KIND, HDD_TENSOR_SYM_PER_ELEM, HDD_FN_PER_ELEM>>(a, s)
-              : launch_persistent<VolProductPolicy<E, KIND, HDD_TENSOR_SYM_PER_ELEM, HDD_FN_CONST>>(a, s);
+      return pe ? launch_persistent<VolProductPolicy<E, KIND, HDD_TENSOR_ISO_PER_ELEM, HDD_FN_PER_ELEM, VX>>(a, s)
+                : launch_persistent<VolProductPolicy<E, KIND, HDD_TENSOR_ISO_PER_ELEM, HDD_FN_CONST, VX>>(a, s);
+    return pe ? launch_persistent<VolProductPolicy<E, KIND, HDD_TENSOR_SYM_PER_ELEM, HDD_FN_PER_ELEM, VX>>(a, s)
+              : launch_persistent<VolProductPolicy<E, KIND, HDD_TENSOR_SYM_PER_ELEM, HDD_FN_CONST, VX>>(a, s);
   }
 }
 
+template <class E, int KIND>
+static hipError_t launch_vol_product(const AssembleArgs& a, hipStream_t s)
+{
+  if constexpr (std::is_same_v<E, Simplex>)
+    if (a.ev) return launch_vol_product_vx<E, KIND, 1>(a, s);
+  return launch_vol_product_vx<E, KIND, 0>(a, s);
+}
+
 template <int TK, int KK> using P1Pen = P1PwcPolicy<TK, KK, true>;
+template <int TK, int KK> using P1PenVX = P1PwcPolicy<TK, KK, true, 1>;
 template <int TK, int KK> using Q1Pen = Q1PwcPolicy<TK, KK, true>;
 
 hipError_t launch_product_fast(const AssembleArgs& a, int product, hipStream_t s, bool* supported)
@@ -1930,6 +1946,7 @@ hipError_t launch_product_fast(const AssembleArgs& a, int product, hipStream_t s
       return tri ? launch_vol_product<Simplex, HDD_PRODUCT_BOUNDARY_L2>(a, s)
                  : launch_vol_product<Cube, HDD_PRODUCT_BOUNDARY_L2>(a, s);
     default:
+      if (tri && a.ev) return dispatch_pwc<P1PenVX>(a, s);   // vertex-indexed geometry (triangles, as the stiffness)
       return tri ? dispatch_pwc<P1Pen>(a, s) : dispatch_pwc<Q1Pen>(a, s);
   }
 }

@@ -138,13 +138,20 @@ def f(args):
     # products
     dpv = H.DevicePattern(loc, volume=True)
     dpf = H.DevicePattern(loc)
+    # products read the vertex-indexed geometry (12 B of vertex ids per triangle + each 16-byte vertex row
+    # once); the elliptic / penalty products the tensor (8 B), the penalty product the neighbour ids + face
+    # info (16 B); values written once
+    nv = dm.vertex_coords.shape[0] if dm.vertex_coords is not None else 0
     for name, kind, dp in (("l2", H.PRODUCT_L2, dpv), ("h1_semi", H.PRODUCT_H1_SEMI, dpv),
                            ("elliptic", H.PRODUCT_ELLIPTIC, dpv), ("penalty", H.PRODUCT_PENALTY, dpf)):
         o = torch.empty(dp.nnz, dtype=torch.float64, device="cuda")
         fn = lambda: H.product(ctx, dm, kind, dp, kappa=H.scalar_fn(H.FN_CONST, 1.0), tensor=ten, out=o)
         t = timed(fn, args.steps, args.warmup)
-        b = 8 * dp.nnz + ne * (48 + 12 + 8)
-        res.update({name + "_ms": t * 1e3, name + "_GBps": b / t / 1e9, name + "_nnz": dp.nnz})
+        per_elem = 12 + (8 if kind in (H.PRODUCT_ELLIPTIC, H.PRODUCT_PENALTY) else 0) + \
+            (16 if kind == H.PRODUCT_PENALTY else 0)
+        b = 8 * dp.nnz + ne * per_elem + 16 * nv
+        res.update({name + "_ms": t * 1e3, name + "_GBps": b / t / 1e9, name + "_values_GBps": 8 * dp.nnz / t / 1e9,
+                    name + "_nnz": dp.nnz})
     return res
 
 

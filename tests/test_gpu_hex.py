@@ -188,3 +188,21 @@ def test_device_pattern_tiles_equal_host(ctx, et):
     assert np.array_equal(dpat.row_ptr.cpu().numpy(), host[0])
     assert np.array_equal(dpat.col.cpu().numpy(), host[1])
     assert np.array_equal(dpat.elem_ptr.cpu().numpy(), host[2])
+
+
+@pytest.mark.parametrize("et,px", [(H.SIMPLEX, 1), (H.CUBE, 1), (H.SIMPLEX, 3)])
+def test_device_pattern_uniform_tiles_equal_host(ctx, et, px):
+    """Large single- and multi-subdomain meshes, where most tiles are uniform (every element with all faces
+    interior: the 16-byte staged path of pattern_fill_tile_kernel) next to boundary tiles, with and without
+    global ids (a rank-local slice maps local to global ids through the gid gathers)."""
+    torch = _torch()
+    g = H.Grid.structured(et, 400, 83, px=px, py=1)
+    for s0, s1 in ((0, px), (px - 1, px)):
+        loc = g.local(s0, s1)
+        host = loc.pattern()
+        dpat = H.DevicePattern(loc, ctx=ctx, on_device=True)
+        torch.cuda.synchronize()
+        assert dpat.nnz == host[1].shape[0]
+        assert np.array_equal(dpat.row_ptr.cpu().numpy(), host[0])
+        assert np.array_equal(dpat.col.cpu().numpy(), host[1])
+        assert np.array_equal(dpat.elem_ptr.cpu().numpy(), host[2])

@@ -454,6 +454,30 @@ def test_vertex_indexed_geometry_equals_element_major(ctx, case):
     assert torch.equal(vals[0], vals[1])
 
 
+@pytest.mark.parametrize("kind", ["l2", "h1_semi", "elliptic", "boundary_l2", "penalty"])
+def test_vertex_indexed_products_equal_element_major(ctx, kind):
+    """The products (swipdg.hh:358-508) on the vertex-indexed geometry equal the element-major ones bit for
+    bit (bisection mesh: reversed faces; per-element tensor and diffusion factor)."""
+    torch = _torch()
+    from mesh_tools import nvb_mesh
+    et, coords, ev = nvb_mesh(5, 3)
+    grid = H.Grid.from_connectivity(et, coords, ev)
+    local = grid.local()
+    rng = np.random.default_rng(5)
+    ne = local.n_local
+    ten = H.tensor_fn(H.TENSOR_ISO_PER_ELEM, per_elem=torch.from_numpy(10.0 ** rng.uniform(-2, 2, ne)).cuda())
+    kap = H.scalar_fn(H.FN_PER_ELEM, per_elem=torch.from_numpy(rng.uniform(0.5, 2.0, ne)).cuda())
+    k = {"l2": H.PRODUCT_L2, "h1_semi": H.PRODUCT_H1_SEMI, "elliptic": H.PRODUCT_ELLIPTIC,
+         "boundary_l2": H.PRODUCT_BOUNDARY_L2, "penalty": H.PRODUCT_PENALTY}[kind]
+    dp = H.DevicePattern(local, volume=kind != "penalty")
+    vals = []
+    for vx in (True, False):
+        dm = H.DeviceMesh(local, vertex_indexed=vx)
+        vals.append(H.product(ctx, dm, k, dp, kappa=kap, tensor=ten))
+    torch.cuda.synchronize()
+    assert torch.equal(vals[0], vals[1])
+
+
 @pytest.mark.parametrize("nnz,n_comp,n_s,stride_pad", [(1001, 3, 40, 6), (75460608 // 64, 2, 33, 0), (7, 1, 1, 2)])
 def test_affine_lincomb(ctx, nnz, n_comp, n_s, stride_pad):
     """theta-lincomb A(mu_s) = sum_q theta_q(mu_s) A_q (freeze_parameter, base.hh:338-361): several passes of
