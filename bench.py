@@ -317,7 +317,12 @@ def main():
                          "algorithmic_bytes_per_launch": alg_bytes,
                          # measured on this box in this run: device copy (read + write) and fill (write)
                          "attainable": dict(att, source="torch copy_ / fill_ of 1 GiB, HIP events"),
-                         "frac_of_torch_copy": achieved / att["copy_gbs"]},
+                         "frac_of_torch_copy": achieved / att["copy_gbs"],
+                         # the algorithmic count prices element-major coordinates (48 B per
+                         # triangle); the kernel reads the vertex-indexed geometry instead, so its measured HBM
+                         # traffic (PMC, same build) is below it -- the rate of that traffic:
+                         "traffic_gbs": (traffic / (kernel_ms * 1e-3) / 1e9) if traffic else None,
+                         "traffic_frac": (traffic / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if traffic else None},
             "cpu_baseline": cpu,
         }
         out["config"]["entry"] = "hdd_block_assemble_sharded (C ABI)"
