@@ -713,6 +713,12 @@ extern "C" int hdd_swipdg_rhs(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_
   a.own_begin = m->own_begin;
   a.own_end = m->own_end;
   a.coords = m->coords;
+  if (!m->elem_vertices != !m->vertex_coords)
+    return set_error(HDD_ERR_INVALID, "hdd_swipdg_rhs: mesh elem_vertices / vertex_coords: both or neither");
+  if (m->elem_vertices && m->elem_type != HDD_HEX && !(ctx->debug_flags & 16384)) {
+    a.ev = m->elem_vertices;   // vertex-indexed geometry
+    a.vxy = m->vertex_coords;
+  }
   a.nbrs = m->neighbors;
   a.tkind = tensor ? tensor->kind : HDD_TENSOR_CONST;
   for (int r = 0; r < 6; ++r) a.tc[r] = tensor ? tensor->c[r] : 0.0;

@@ -232,7 +232,11 @@ __device__ __forceinline__ void rhs2d_shape(double x, double y, double* v, doubl
   }
 }
 
-template <bool TRI>
+// Thread per element (VALU-bound: the force's cos products at the quadrature points).  VX: the vertex-indexed
+// geometry (vertex ids + 16-byte vertex rows) instead of the element-major coordinates -- neutral here (same
+// box 0.1345 ms both), kept so that one mesh serves every kernel.  (Staging the chunk's values in LDS for
+// 16-byte stores was slower: 0.102 -> 0.135 ms.)
+template <bool TRI, bool VX>
 __global__ __launch_bounds__(256) void rhs2d_kernel(RhsArgs a)
 {
   constexpr int NB = TRI ? 3 : 4, NF = TRI ? 3 : 4;
@@ -240,9 +244,19 @@ __global__ __launch_bounds__(256) void rhs2d_kernel(RhsArgs a)
   const int64_t n = a.n_local;
   for (int64_t k = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; k < n_own; k += int64_t(gridDim.x) * blockDim.x) {
     const int64_t e = a.own_begin + k;
-    const double x0 = a.coords[e], y0 = a.coords[n + e];
-    const double j00 = a.coords[2 * n + e] - x0, j10 = a.coords[3 * n + e] - y0;   // vertex 1 - vertex 0
-    const double j01 = a.coords[4 * n + e] - x0, j11 = a.coords[5 * n + e] - y0;   // vertex 2 - vertex 0
+    double x0, y0, x1, y1, x2, y2;
+    if constexpr (VX) {
+      const double2 p0 = reinterpret_cast<const double2*>(a.vxy)[a.ev[e]];
+      const double2 p1 = reinterpret_cast<const double2*>(a.vxy)[a.ev[n + e]];
+      const double2 p2 = reinterpret_cast<const double2*>(a.vxy)[a.ev[2 * n + e]];
+      x0 = p0.x; y0 = p0.y; x1 = p1.x; y1 = p1.y; x2 = p2.x; y2 = p2.y;
+    } else {
+      x0 = a.coords[e]; y0 = a.coords[n + e];
+      x1 = a.coords[2 * n + e]; y1 = a.coords[3 * n + e];
+      x2 = a.coords[4 * n + e]; y2 = a.coords[5 * n + e];
+    }
+    const double j00 = x1 - x0, j10 = y1 - y0;   // vertex 1 - vertex 0
+    const double j01 = x2 - x0, j11 = y2 - y0;   // vertex 2 - vertex 0
     const double det = j00 * j11 - j01 * j10, adet = fabs(det);
     double acc[NB];
 #pragma unroll
@@ -590,10 +604,14 @@ hipError_t launch_rhs(const RhsArgs& a, hipStream_t s)
   const int64_t n_own = a.own_end - a.own_begin;
   if (a.elem_type != HDD_HEX && n_own > 0) {
     const int64_t blocks = std::min<int64_t>((n_own + 255) / 256, int64_t(a.n_cu) * 8);
-    if (a.elem_type == HDD_SIMPLEX)
-      hipLaunchKernelGGL(rhs2d_kernel<true>, dim3(unsigned(blocks)), dim3(256), 0, s, a);
-    else
-      hipLaunchKernelGGL(rhs2d_kernel<false>, dim3(unsigned(blocks)), dim3(256), 0, s, a);
+    const bool tri = a.elem_type == HDD_SIMPLEX;
+    if (a.ev) {
+      if (tri) hipLaunchKernelGGL((rhs2d_kernel<true, true>), dim3(unsigned(blocks)), dim3(256), 0, s, a);
+      else hipLaunchKernelGGL((rhs2d_kernel<false, true>), dim3(unsigned(blocks)), dim3(256), 0, s, a);
+    } else {
+      if (tri) hipLaunchKernelGGL((rhs2d_kernel<true, false>), dim3(unsigned(blocks)), dim3(256), 0, s, a);
+      else hipLaunchKernelGGL((rhs2d_kernel<false, false>), dim3(unsigned(blocks)), dim3(256), 0, s, a);
+    }
     return hipGetLastError();
   }
   const int64_t total = n_own * a.nb;

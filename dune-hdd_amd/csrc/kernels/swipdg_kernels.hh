@@ -105,6 +105,8 @@ struct RhsArgs {
   double qd[16][3];    // Dirichlet face rule: face parameters (2) + weight
   double qn[16][3];    // Neumann face rule
   double* out;         // [nb * n_own]
+  const int32_t* ev;   // optional vertex-indexed geometry (2d): element -> vertex ids [nvpe][n_local]
+  const double* vxy;   //   and vertex coordinates [n_vertices][2]
 };
 hipError_t launch_rhs(const RhsArgs& a, hipStream_t s);
 

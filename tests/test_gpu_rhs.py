@@ -105,3 +105,32 @@ def test_alu_p1_table_from_gpu_system(ctx):
         l2, h1 = O.error_norms_esv2007(og, u)
         l2s.append(sig3(l2)); h1s.append(sig3(h1))
     assert l2s == ALU_L2 and h1s == ALU_H1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["kuhn", "quad", "nvb"])
+def test_rhs_vertex_indexed_equals_element_major(case):
+    """The right-hand side on the vertex-indexed geometry (the default of DeviceMesh) equals the element-major
+    path bit for bit: force + Dirichlet (kappa, tensor) + Neumann data on a mixed-boundary mesh, ragged last
+    256-element chunk."""
+    import torch
+    ctx = H.Context(0)
+    if case == "nvb":
+        from mesh_tools import nvb_mesh
+        et, coords, ev = nvb_mesh(4, 3)
+        grid = H.Grid.from_connectivity(et, coords, ev)
+    else:
+        grid = H.Grid.structured(H.SIMPLEX if case == "kuhn" else H.CUBE, 61, 23, (0, 0), (2, 1))
+    loc = grid.local()
+    bnd = loc.neighbors[0] == H.NBR_DIRICHLET
+    loc.neighbors[0][bnd] = H.NBR_NEUMANN          # some Neumann faces
+    rng = np.random.default_rng(8)
+    ten = H.tensor_fn(H.TENSOR_ISO_PER_ELEM, per_elem=torch.from_numpy(rng.uniform(0.5, 2.0, loc.n_local)).cuda())
+    out = []
+    for vx in (True, False):
+        dm = H.DeviceMesh(loc, vertex_indexed=vx)
+        out.append(H.rhs(ctx, dm, force=H.esv2007_force(), kappa=H.scalar_fn(H.FN_CONST, 1.3), tensor=ten,
+                         dirichlet=H.scalar_fn(H.FN_SINUSOID, 0.5, 1.0, 2.0, 1.0, order=3),
+                         neumann=H.scalar_fn(H.FN_CONST, 0.7)))
+    torch.cuda.synchronize()
+    assert torch.equal(out[0], out[1])
