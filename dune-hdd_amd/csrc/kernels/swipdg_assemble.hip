@@ -1635,41 +1635,58 @@ swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
   }
   if (t >= t_end) return;
   double* scratch = P::PAD ? lds + IMG - RB : lds + IMG + 2;
-  // optional tile list (interior / halo-boundary split of a sharded assembly): position -> tile
-  auto tile_at = [&](int64_t pos) -> int64_t {
-    if constexpr (TL) return int64_t(__builtin_amdgcn_readfirstlane(a.tile_list[pos]));
+  // Loads whose values must be wave-uniform (tile ids of a tile list, the tiles' CSR bounds elem_ptr[]) are
+  // vector loads (the compiler cannot prove elem_ptr unaliased by the value stores, so no s_load); a
+  // readfirstlane right after such a load waits for it -- and, vmcnt being in order, for the previous tile's
+  // stores issued before it.  So they are issued one tile ahead as raw values and made uniform only in the
+  // next iteration, where the wait is a counted one behind the stores.
+  // Tile list (interior / halo-boundary split of a sharded assembly): position -> tile.
+  auto tile_raw = [&](int64_t pos) -> int64_t {
+    if constexpr (TL) return int64_t(a.tile_list[pos]);
     return pos;
   };
-  auto elem_of = [&](int64_t pos) {
-    const int64_t t0 = a.own_begin + tile_at(pos) * 64;
+  auto uni64 = [](int64_t v) -> int64_t { return __builtin_amdgcn_readfirstlane(v); };
+  auto elem_of_tile = [&](int64_t tile) {
+    const int64_t t0 = a.own_begin + tile * 64;
     const int64_t e0 = t0 + lane;
     return e0 < a.own_end ? e0 : t0;
   };
-  auto bounds = [&](int64_t pos, int64_t& base, int64_t& tile_end) {   // scalar loads (lgkmcnt)
-    const int64_t t0 = __builtin_amdgcn_readfirstlane(a.own_begin + tile_at(pos) * 64);
+  auto bounds_raw = [&](int64_t tile, int64_t& base_r, int64_t& end_r) {
+    const int64_t t0 = a.own_begin + tile * 64;
     const int64_t tend = t0 + 64 < a.own_end ? t0 + 64 : a.own_end;
-    base = __builtin_amdgcn_readfirstlane(a.elem_ptr[t0 - a.own_begin]);
-    tile_end = __builtin_amdgcn_readfirstlane(a.elem_ptr[tend - a.own_begin]);
+    base_r = a.elem_ptr[t0 - a.own_begin];
+    end_r = a.elem_ptr[tend - a.own_begin];
   };
-  int64_t e = elem_of(t);
+  int64_t tile = uni64(tile_raw(t));
+  int64_t e = elem_of_tile(tile);
   typename P::Own own;
   typename P::Gat gat;
   P::load_own(a, e, own);
   P::load_gat(a, e, own, gat);
   P::load_gat2(a, gat);
-  int64_t base, tile_end;
-  bounds(t, base, tile_end);
+  int64_t base_r, tile_end_r;
+  bounds_raw(tile, base_r, tile_end_r);
+  int64_t tile_n_r = tile_raw(t + t_step < t_end ? t + t_step : t);
+  // Drain the prologue's loads before entering the loop.  The compiler's wait counts at the loop head are
+  // the minimum over the entry paths: entered straight from the prologue, the first tile's vertex rows
+  // are followed by only ~7 memory operations, so the first compute of EVERY iteration waited with
+  // vmcnt(7) -- i.e. for all but the last two of the previous tile's 20 stores.  With nothing outstanding
+  // on entry only the back edge counts, and that wait skips the stores (in-order vmcnt).
+  __builtin_amdgcn_s_waitcnt(0);
   double* out = a.vals[0];
   for (;;) {
     const bool has_next = t + t_step < t_end;
     const int64_t tn = has_next ? t + t_step : t;
-    const int64_t en = elem_of(tn);
+    const int64_t tile_n = uni64(tile_n_r);   // loaded one iteration ago
+    const int64_t en = elem_of_tile(tile_n);
     typename P::Own own_n;
     P::load_own(a, en, own_n);
-    int64_t base_n, tile_end_n;
-    bounds(tn, base_n, tile_end_n);
+    int64_t base_n_r, tile_end_n_r;
+    bounds_raw(tile_n, base_n_r, tile_end_n_r);
+    const int64_t tile_nn_r = tile_raw(tn + t_step < t_end ? tn + t_step : tn);
+    const int64_t base = uni64(base_r), tile_end = uni64(tile_end_r);   // loaded one iteration ago
 
-    const int64_t t0 = a.own_begin + tile_at(t) * 64;
+    const int64_t t0 = a.own_begin + tile * 64;
     const bool active = t0 + lane < a.own_end;
     const int64_t base_al = base & ~int64_t(1);
     const int off = tile_offset<P::NB>(P::n_interior(own), active) + int(base - base_al);
@@ -1742,11 +1759,13 @@ swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
     if (!HDD_ABL(a, 4)) P::load_gat2(a, gat_n);   // (ablation 4: no stage-1 ids to follow)
     if (!has_next) break;
     t = tn;
+    tile = tile_n;
+    tile_n_r = tile_nn_r;
     e = en;
     own = own_n;
     gat = gat_n;
-    base = base_n;
-    tile_end = tile_end_n;
+    base_r = base_n_r;
+    tile_end_r = tile_end_n_r;
   }
 }
 
