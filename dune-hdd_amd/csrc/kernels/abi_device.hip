@@ -343,15 +343,17 @@ extern "C" int hdd_swipdg_assemble_tiles(hdd_ctx* ctx, const hdd_mesh* m, const 
 }
 
 // ------------------------------------------------------------------------------------------------
-// theta-lincomb: out[s][k] = sum_q theta[s][q] v_q[k]; up to LC_S samples per launch (the components are
-// read once per LC_S samples), 2 values per lane written as one 16-byte non-temporal store per sample
+// theta-lincomb: out[s][k] = sum_q theta[s][q] v_q[k]; up to LC_T / n_comp samples per launch (128 for the
+// affine + 1 component case: the components are read once for all of them), 2 values per lane written as one
+// 16-byte non-temporal store per sample.  All samples in one launch: 12.5-12.7 ms for 128 C3 samples against
+// 15.2 ms in launches of 32 (scripts/microbench/lincomb_mb.hip, profiles/r02/s3/lincomb_mb.log).
 // ------------------------------------------------------------------------------------------------
 namespace {
-constexpr int LC_S = 32;
+constexpr int LC_T = 256;   // theta values per launch (samples x components): 2 KB of kernel arguments
 typedef double lc_dvec2 __attribute__((ext_vector_type(2)));
 struct LincombArgs {
   const double* v[HDD_MAX_COMP];
-  double theta[LC_S][HDD_MAX_COMP];
+  double theta[LC_T];         // [n_s][n_comp]
   double* out;
   int64_t nnz, stride;
   int32_t n_comp, n_s;
@@ -359,6 +361,9 @@ struct LincombArgs {
 
 __global__ void __launch_bounds__(256) lincomb_kernel(const LincombArgs a)
 {
+  __shared__ double th[LC_T];
+  for (int i = threadIdx.x; i < a.n_s * a.n_comp; i += 256) th[i] = a.theta[i];
+  __syncthreads();
   const int64_t n2 = a.nnz >> 1;
   for (int64_t k = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; k < n2; k += int64_t(gridDim.x) * blockDim.x) {
     double2 v[HDD_MAX_COMP];
@@ -367,11 +372,12 @@ __global__ void __launch_bounds__(256) lincomb_kernel(const LincombArgs a)
       v[c] = c < a.n_comp ? reinterpret_cast<const double2*>(a.v[c])[k] : make_double2(0.0, 0.0);
     for (int s = 0; s < a.n_s; ++s) {
       lc_dvec2 r = {0.0, 0.0};
+      const double* ts = th + s * a.n_comp;
 #pragma unroll
       for (int c = 0; c < HDD_MAX_COMP; ++c) {
         if (c < a.n_comp) {
-          r.x += a.theta[s][c] * v[c].x;
-          r.y += a.theta[s][c] * v[c].y;
+          r.x += ts[c] * v[c].x;
+          r.y += ts[c] * v[c].y;
         }
       }
       __builtin_nontemporal_store(r, reinterpret_cast<lc_dvec2*>(a.out + s * a.stride) + k);
@@ -381,7 +387,7 @@ __global__ void __launch_bounds__(256) lincomb_kernel(const LincombArgs a)
     const int64_t k = a.nnz - 1;
     for (int s = 0; s < a.n_s; ++s) {
       double r = 0.0;
-      for (int c = 0; c < a.n_comp; ++c) r += a.theta[s][c] * a.v[c][k];
+      for (int c = 0; c < a.n_comp; ++c) r += th[s * a.n_comp + c] * a.v[c][k];
       a.out[s * a.stride + k] = r;
     }
   }
@@ -402,14 +408,15 @@ extern "C" int hdd_affine_lincomb(hdd_ctx* ctx, int64_t nnz, const double* const
   hipError_t e = hipSetDevice(ctx->device);
   if (e != hipSuccess) return hip_fail(e, "hdd_affine_lincomb: hipSetDevice");
   const int64_t n2 = (nnz + 1) / 2;
-  const unsigned grid = unsigned(std::min<int64_t>(std::max<int64_t>((n2 + 255) / 256, 1), 256 * 16));
-  for (int s0 = 0; s0 < n_samples; s0 += LC_S) {
+  const unsigned grid = unsigned(std::min<int64_t>(std::max<int64_t>((n2 + 255) / 256, 1), 256 * 32));
+  const int per_launch = LC_T / n_comp;
+  for (int s0 = 0; s0 < n_samples; s0 += per_launch) {
     LincombArgs a{};
     for (int c = 0; c < n_comp; ++c) a.v[c] = d_vals[c];
     a.n_comp = n_comp;
-    a.n_s = std::min(LC_S, n_samples - s0);
+    a.n_s = std::min(per_launch, n_samples - s0);
     for (int s = 0; s < a.n_s; ++s)
-      for (int c = 0; c < n_comp; ++c) a.theta[s][c] = theta[(s0 + s) * n_comp + c];
+      for (int c = 0; c < n_comp; ++c) a.theta[s * n_comp + c] = theta[(s0 + s) * n_comp + c];
     a.out = d_out + int64_t(s0) * out_stride;
     a.nnz = nnz;
     a.stride = out_stride;

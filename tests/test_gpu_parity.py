@@ -478,10 +478,12 @@ def test_vertex_indexed_products_equal_element_major(ctx, kind):
     assert torch.equal(vals[0], vals[1])
 
 
-@pytest.mark.parametrize("nnz,n_comp,n_s,stride_pad", [(1001, 3, 40, 6), (75460608 // 64, 2, 33, 0), (7, 1, 1, 2)])
+@pytest.mark.parametrize("nnz,n_comp,n_s,stride_pad", [(1001, 3, 90, 6), (75460608 // 64, 2, 130, 0), (4097, 8, 70, 0),
+                                                        (7, 1, 1, 2)])
 def test_affine_lincomb(ctx, nnz, n_comp, n_s, stride_pad):
-    """theta-lincomb A(mu_s) = sum_q theta_q(mu_s) A_q (freeze_parameter, base.hh:338-361): several passes of
-    32 samples, odd lengths (scalar tail), a padded output stride -- against numpy."""
+    """theta-lincomb A(mu_s) = sum_q theta_q(mu_s) A_q (freeze_parameter, base.hh:338-361): 256 / n_comp samples
+    per launch, so several launches here (90 = 85 + 5 samples of 3 components, 130 = 128 + 2 of 2, 70 = 32 + 32 +
+    6 of 8), odd lengths (scalar tail), a padded output stride -- against numpy."""
     torch = _torch()
     rng = np.random.default_rng(nnz)
     comps = [torch.from_numpy(rng.standard_normal(nnz)).cuda() for _ in range(n_comp)]
