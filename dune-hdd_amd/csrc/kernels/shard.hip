@@ -661,7 +661,9 @@ extern "C" int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm*
     }
   const bool exchange = h.n_peers > 0 && !(flags & HDD_SHARD_NO_HALO) && h.n_arrays > 0;
   if (!exchange) return hdd_swipdg_assemble(ctx, &m, kappa, n_comp, tensor, params, pattern, d_vals, stream);
-  if (!comm) return set_error(HDD_ERR_INVALID, "hdd_block_assemble_sharded: the shard has halo peers but comm is NULL");
+  const bool transfer = !(flags & HDD_SHARD_NO_TRANSFER);
+  if (!comm && transfer)
+    return set_error(HDD_ERR_INVALID, "hdd_block_assemble_sharded: the shard has halo peers but comm is NULL");
   const int32_t R = h.row_first[h.n_arrays];
   if (R > sh->max_rows) return set_error(HDD_ERR_INVALID, "hdd_block_assemble_sharded: too many halo rows");
 
@@ -683,7 +685,16 @@ extern "C" int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm*
     rp[k] = sh->d_rbuf + int64_t(R) * sh->recv_prefix[k];
     rn[k] = int64_t(R) * (sh->recv_prefix[k + 1] - sh->recv_prefix[k]);
   }
-  int rc = hdd_comm_post(comm, h.n_peers, sh->peers.data(), sp.data(), sn.data(), rp.data(), rn.data(), stream);
+  int rc = HDD_OK;
+  if (transfer) {
+    rc = hdd_comm_post(comm, h.n_peers, sh->peers.data(), sp.data(), sn.data(), rp.data(), rn.data(), stream);
+  } else {   // timing studies: the receive buffers get this rank's own messages (stream-ordered device copies)
+    for (int k = 0; k < h.n_peers && rc == HDD_OK; ++k) {
+      const int64_t n = std::min(sn[k], rn[k]);
+      if (n > 0 && hipMemcpyAsync(rp[k], sp[k], size_t(n) * sizeof(double), hipMemcpyDeviceToDevice, s) != hipSuccess)
+        rc = set_error(HDD_ERR_HIP, "hdd_block_assemble_sharded: loopback copy");
+    }
+  }
   if (rc) return rc;
   // 3. interior tiles overlap the transfer (the kernels that take tile lists: P1 / Q1 persistent policies)
   bool overlap = !(flags & HDD_SHARD_NO_OVERLAP) && sh->n_in > 0 && sh->gi.elem_type != HDD_HEX;
@@ -692,12 +703,12 @@ extern "C" int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm*
                                    stream);
     if (rc == HDD_ERR_UNSUPPORTED) overlap = false;   // no tile-list kernel: assemble everything after the halo
     else if (rc) {
-      (void)hdd_comm_wait(comm, stream);
+      if (transfer) (void)hdd_comm_wait(comm, stream);
       return rc;
     }
   }
   // 4. ghost columns after the receives
-  rc = hdd_comm_wait(comm, stream);
+  if (transfer) rc = hdd_comm_wait(comm, stream);
   if (rc) return rc;
   for (int k = 0; k <= h.n_peers; ++k) h.prefix[k] = sh->recv_prefix[k];
   for (int k = 0; k < h.n_peers; ++k) h.col0[k] = sh->recv_col0[k];

@@ -378,7 +378,10 @@ int hdd_shard_pattern_fill(hdd_ctx* ctx, const hdd_shard* sh, int64_t* d_row_ptr
 enum {
   HDD_SHARD_NO_OVERLAP = 1,     /* exchange, then assemble every tile (default: interior tiles overlap the halo) */
   HDD_SHARD_HALO_GEOMETRY = 2,  /* also send the ghost vertex coordinates (default: geometry is rank-local) */
-  HDD_SHARD_NO_HALO = 4         /* ghost columns already valid (static coefficients): no exchange at all */
+  HDD_SHARD_NO_HALO = 4,        /* ghost columns already valid (static coefficients): no exchange at all */
+  HDD_SHARD_NO_TRANSFER = 8     /* timing studies only: pack, split tile launches and unpack as in an exchange,
+                                   but no transfer (comm may be NULL; the ghost columns receive the rank's own
+                                   send buffers, i.e. wrong values) -- the GPU-side cost of the sharded step */
 };
 /* One sharded assembly step -- the LHS of BlockSWIPDG::init() for the owned subdomains: pack the halo
  * records (per-element tensor / kappa rows, [+ coordinates]) of the elements the peers need -> post the
