@@ -208,3 +208,39 @@ def test_cpp_example_rccl_one_rank():
                            timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "rccl rank 0/1" in r.stdout and "NON-FINITE" not in r.stdout
+
+
+@pytest.mark.gpu
+def test_no_transfer_flag_keeps_interior_rows():
+    """HDD_SHARD_NO_TRANSFER (timing studies): rank 0 of 2 runs every launch of the overlapped step without a
+    communicator; the ghost columns then hold the rank's own send buffer (wrong values by design), so exactly
+    the rows of elements without a ghost neighbour must equal the single-GPU assembly, bit for bit.  Without
+    the flag a NULL communicator is an error."""
+    import torch
+    grid = H.Grid.structured(H.SIMPLEX, 96, 20, LOWER, UPPER, px=2, py=1)
+    ctx = H.Context(0)
+    sh = H.Shard(ctx, grid, 2, 0)
+    assert sh.info.n_peers == 1 and sh.info.n_tiles_boundary > 0
+    k = sh.checkerboard(LOWER, UPPER, 100, 20, np.linspace(0.5, 3.0, 2000))
+    tensor = H.tensor_fn(H.TENSOR_ISO_PER_ELEM, per_elem=torch.from_numpy(k).cuda())
+    kap = [H.scalar_fn(H.FN_CONST, 1.0)]
+    rp, col, ep, pat = sh.pattern(ctx)
+    v = [torch.full((sh.info.nnz,), float("nan"), dtype=torch.float64, device="cuda")]
+    with pytest.raises(H.HddError):
+        H.assemble_sharded(ctx, sh, None, kap, tensor, pat, v)
+    H.assemble_sharded(ctx, sh, None, kap, tensor, pat, v, flags=H.SHARD_NO_TRANSFER)
+    loc = grid.local()
+    ref = H.assemble(ctx, H.DeviceMesh(loc, 0), H.DevicePattern(loc, 0), kap,
+                     H.tensor_fn(H.TENSOR_ISO_PER_ELEM, per_elem=torch.from_numpy(
+                         loc.checkerboard(LOWER, UPPER, 100, 20, np.linspace(0.5, 3.0, 2000))).cuda()))[0]
+    torch.cuda.synchronize()
+    got, want = v[0].cpu().numpy(), ref.cpu().numpy()[:sh.info.nnz]
+    colv, epv = col.cpu().numpy(), ep.cpu().numpy()
+    g0, g1 = sh.info.global_first, sh.info.global_first + sh.n_own   # owned global element ids
+    touches = np.zeros(sh.n_own, bool)
+    for e in range(sh.n_own):   # an owned element's row block references a ghost (non-owned) column block
+        g = colv[epv[e]:epv[e + 1]] // sh.nb
+        touches[e] = bool(((g < g0) | (g >= g1)).any())
+    assert touches.any() and not touches.all()
+    for e in np.flatnonzero(~touches)[:: 7]:
+        assert np.array_equal(got[epv[e]:epv[e + 1]], want[epv[e]:epv[e + 1]]), e
