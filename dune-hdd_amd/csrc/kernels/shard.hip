@@ -399,12 +399,15 @@ struct hdd_shard {
   int32_t* d_tiles_bd = nullptr;
   int64_t n_tiles = 0, n_in = 0, n_bd = 0;
   int64_t halo_faces = 0;
+  // host copies of the plan (hdd_shard_halo_lists / hdd_shard_tile_lists)
+  std::vector<int32_t> send_idx, tiles_in, tiles_bd;
+  bool host_only = false;          // created without a context: no device arrays
 };
 
 extern "C" void hdd_shard_destroy(hdd_shard* sh)
 {
   if (!sh) return;
-  (void)hipSetDevice(sh->device);
+  if (!sh->host_only) (void)hipSetDevice(sh->device);
   for (void* p : {static_cast<void*>(sh->d_coords), static_cast<void*>(sh->d_nbrs), static_cast<void*>(sh->d_finfo),
                   static_cast<void*>(sh->d_gid), static_cast<void*>(sh->d_send_idx), static_cast<void*>(sh->d_sbuf),
                   static_cast<void*>(sh->d_rbuf), static_cast<void*>(sh->d_tiles_in),
@@ -417,7 +420,7 @@ extern "C" void hdd_shard_destroy(hdd_shard* sh)
 extern "C" int hdd_shard_create(hdd_ctx* ctx, const hdd_grid* g, int32_t nranks, int32_t rank, const int32_t* owner,
                                 hdd_shard** out)
 {
-  if (!ctx || !g || !out || nranks < 1 || rank < 0 || rank >= nranks)
+  if (!g || !out || nranks < 1 || rank < 0 || rank >= nranks)
     return set_error(HDD_ERR_INVALID, "hdd_shard_create: invalid argument");
   hdd_grid_info gi{};
   int rc = hdd_grid_get_info(g, &gi);
@@ -448,6 +451,7 @@ extern "C" int hdd_shard_create(hdd_ctx* ctx, const hdd_grid* g, int32_t nranks,
     return code;
   };
   sh->device = hdd::ctx_device(ctx);
+  sh->host_only = !ctx;
   sh->gi = gi;
   sh->rank = rank;
   sh->nranks = nranks;
@@ -522,6 +526,16 @@ extern "C" int hdd_shard_create(hdd_ctx* ctx, const hdd_grid* g, int32_t nranks,
   }
   sh->n_in = int64_t(tin.size());
   sh->n_bd = int64_t(tbd.size());
+  sh->send_idx = send_idx;
+  sh->tiles_in = tin;
+  sh->tiles_bd = tbd;
+  // message rows: coordinates + symmetric tensor + one row per diffusion-factor component
+  sh->max_rows = gi.dim * gi.nvpe + (gi.dim == 3 ? 6 : 3) + HDD_MAX_COMP;
+  if (!ctx) {   // host-only shard: plan and local mesh, nothing on a device (CPU tests of the halo protocol)
+    sh->host_only = true;
+    *out = sh;
+    return HDD_OK;
+  }
 
   hipError_t e = hipSetDevice(sh->device);
   if (e == hipSuccess) e = upload(&sh->d_coords, coords);
@@ -533,8 +547,6 @@ extern "C" int hdd_shard_create(hdd_ctx* ctx, const hdd_grid* g, int32_t nranks,
   if (e == hipSuccess) e = upload(&sh->d_send_idx, send_idx);
   if (e == hipSuccess) e = upload(&sh->d_tiles_in, tin);
   if (e == hipSuccess) e = upload(&sh->d_tiles_bd, tbd);
-  // message rows: coordinates + symmetric tensor + one row per diffusion-factor component
-  sh->max_rows = gi.dim * gi.nvpe + (gi.dim == 3 ? 6 : 3) + HDD_MAX_COMP;
   if (e == hipSuccess && sh->send_prefix[np])
     e = hipMalloc(&sh->d_sbuf, size_t(sh->max_rows) * sh->send_prefix[np] * sizeof(double));
   if (e == hipSuccess && sh->recv_prefix[np])
@@ -567,6 +579,27 @@ extern "C" int hdd_shard_get_info(const hdd_shard* sh, hdd_shard_info* o)
   o->halo_send = sh->send_prefix.back();
   o->halo_recv = sh->recv_prefix.back();
   o->halo_faces = sh->halo_faces;
+  return HDD_OK;
+}
+
+extern "C" int hdd_shard_halo_lists(const hdd_shard* sh, int32_t* peers, int64_t* send_prefix, int32_t* send_idx,
+                                    int64_t* recv_prefix, int64_t* recv_col0)
+{
+  if (!sh) return set_error(HDD_ERR_INVALID, "hdd_shard_halo_lists: null shard");
+  const size_t np = sh->peers.size();
+  if (peers) std::copy(sh->peers.begin(), sh->peers.end(), peers);
+  if (send_prefix) std::copy(sh->send_prefix.begin(), sh->send_prefix.end(), send_prefix);
+  if (send_idx) std::copy(sh->send_idx.begin(), sh->send_idx.end(), send_idx);
+  if (recv_prefix) std::copy(sh->recv_prefix.begin(), sh->recv_prefix.end(), recv_prefix);
+  if (recv_col0) std::copy(sh->recv_col0.begin(), sh->recv_col0.begin() + np, recv_col0);
+  return HDD_OK;
+}
+
+extern "C" int hdd_shard_tile_lists(const hdd_shard* sh, int32_t* interior, int32_t* boundary)
+{
+  if (!sh) return set_error(HDD_ERR_INVALID, "hdd_shard_tile_lists: null shard");
+  if (interior) std::copy(sh->tiles_in.begin(), sh->tiles_in.end(), interior);
+  if (boundary) std::copy(sh->tiles_bd.begin(), sh->tiles_bd.end(), boundary);
   return HDD_OK;
 }
 

@@ -173,6 +173,8 @@ def lib():
         "hdd_comm_post": (_I32, [_VP, _I32, _VP, _VP, _VP, _VP, _VP, _VP]),
         "hdd_comm_wait": (_I32, [_VP, _VP]),
         "hdd_shard_create": (_I32, [_VP, _VP, _I32, _I32, _VP, _VP]),
+        "hdd_shard_halo_lists": (_I32, [_VP, _VP, _VP, _VP, _VP, _VP]),
+        "hdd_shard_tile_lists": (_I32, [_VP, _VP, _VP]),
         "hdd_shard_destroy": (None, [_VP]),
         "hdd_shard_get_info": (_I32, [_VP, C.POINTER(ShardInfo)]),
         "hdd_shard_mesh": (_I32, [_VP, C.POINTER(MeshT)]),
@@ -704,9 +706,11 @@ class Shard:
     plan and tile lists.  owner: subdomain -> rank (None: contiguous near-equal ranges)."""
 
     def __init__(self, ctx, grid, nranks, rank, owner=None):
+        """ctx None: a host-only shard (local mesh, halo plan, tile lists; no device arrays)."""
         own = None if owner is None else np.ascontiguousarray(owner, np.int32)
         h = C.c_void_p()
-        _check(lib().hdd_shard_create(ctx.h, grid.h, nranks, rank, _p(own), C.byref(h)), "hdd_shard_create")
+        _check(lib().hdd_shard_create(None if ctx is None else ctx.h, grid.h, nranks, rank, _p(own), C.byref(h)),
+               "hdd_shard_create")
         self.h = h
         self.grid = grid                      # the shard references the grid: keep it alive
         self.info = ShardInfo()
@@ -725,6 +729,22 @@ class Shard:
             except Exception:   # interpreter shutdown
                 pass
             self.h = None
+
+    def halo_lists(self):
+        """-> (peers, send_prefix, send_idx (local element indices), recv_prefix, recv_col0)"""
+        i = self.info
+        peers = np.empty(i.n_peers, np.int32)
+        sp, rp = np.empty(i.n_peers + 1, np.int64), np.empty(i.n_peers + 1, np.int64)
+        idx, col0 = np.empty(i.halo_send, np.int32), np.empty(i.n_peers, np.int64)
+        _check(lib().hdd_shard_halo_lists(self.h, _p(peers), _p(sp), _p(idx), _p(rp), _p(col0)), "hdd_shard_halo_lists")
+        return peers, sp, idx, rp, col0
+
+    def tile_lists(self):
+        """-> (interior, boundary) 64-element tiles relative to own_begin"""
+        tin = np.empty(self.info.n_tiles_interior, np.int32)
+        tbd = np.empty(self.info.n_tiles_boundary, np.int32)
+        _check(lib().hdd_shard_tile_lists(self.h, _p(tin), _p(tbd)), "hdd_shard_tile_lists")
+        return tin, tbd
 
     def global_ids(self):
         g = np.empty(self.n_local, np.int64)

@@ -363,8 +363,19 @@ typedef struct {
  * the interior / halo-boundary 64-element tile lists. */
 int hdd_shard_create(hdd_ctx* ctx, const hdd_grid* g, int32_t nranks, int32_t rank, const int32_t* owner,
                      hdd_shard** out);
+/* ctx == NULL: a host-only shard (local mesh, halo plan, tile lists; no device arrays) -- what a rank can
+ * inspect without a GPU, e.g. to check the halo protocol on CPU ranks (tests/test_distributed.py) */
 void hdd_shard_destroy(hdd_shard* sh);
 int hdd_shard_get_info(const hdd_shard* sh, hdd_shard_info* out);
+/* the halo plan (host copies): peers [n_peers] ascending; send lists = local element indices, peer k's
+ * part at [send_prefix[k], send_prefix[k+1]) of send_idx [halo_send] (send_prefix [n_peers+1]); the
+ * message from peer k fills ghost columns recv_col0[k] .. recv_col0[k] + (recv_prefix[k+1] - recv_prefix[k])
+ * (recv_prefix [n_peers+1], recv_col0 [n_peers]).  Any pointer may be NULL. */
+int hdd_shard_halo_lists(const hdd_shard* sh, int32_t* peers, int64_t* send_prefix, int32_t* send_idx,
+                         int64_t* recv_prefix, int64_t* recv_col0);
+/* the 64-element tiles (relative to own_begin) without / with a ghost face neighbour:
+ * interior [n_tiles_interior], boundary [n_tiles_boundary]; either may be NULL */
+int hdd_shard_tile_lists(const hdd_shard* sh, int32_t* interior, int32_t* boundary);
 /* the shard's device mesh (shard-owned arrays; usable with every hdd_* device call) */
 int hdd_shard_mesh(const hdd_shard* sh, hdd_mesh* out);
 /* host arrays [n_local]: global element ids; element barycentres [dim][n_local] (coefficient lookup) */

@@ -87,6 +87,80 @@ def test_gloo_halo_exchange_cpu():
             assert ok and has_ghosts
 
 
+def _shard_worker(rank, world, port, outdir, case):
+    """rank `rank` of a host-only C++ shard (hdd_shard_create with ctx NULL: the plan the sharded step of
+    hdd_block_assemble_sharded moves its halo by) exchanges a per-element field over gloo exactly as the step
+    does -- pack send_idx per peer, one message per peer in peer order, unpack into the ghost columns at
+    recv_col0 -- and checks every ghost column against the owner's value."""
+    _setup_paths()
+    import torch
+    import torch.distributed as dist
+
+    import hdd_amd as H
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    et, nx, ny, px, py = SHARD_CASES[case]
+    g = H.Grid.structured(et, nx, ny, (0.0, 0.0), (5.0, 1.0), px=px, py=py)
+    sh = H.Shard(None, g, world, rank)
+    gid = sh.global_ids()
+    truth = np.sin(0.37 * gid) + 1e-3 * gid          # one distinct value per global element
+    vals = truth.copy()
+    vals[:sh.own_begin] = np.nan
+    vals[sh.own_end:] = np.nan
+    peers, sp, idx, rp, col0 = sh.halo_lists()
+    ops, recvs = [], []
+    for k, p in enumerate(peers):
+        send = torch.from_numpy(np.ascontiguousarray(vals[idx[sp[k]:sp[k + 1]]]))
+        recv = torch.empty(int(rp[k + 1] - rp[k]), dtype=torch.float64)
+        recvs.append(recv)
+        assert not torch.isnan(send).any(), "a send list names a ghost column"
+        ops += [dist.P2POp(dist.isend, send, int(p)), dist.P2POp(dist.irecv, recv, int(p))]
+    for r in (dist.batch_isend_irecv(ops) if ops else []):
+        r.wait()
+    for k in range(len(peers)):
+        vals[col0[k]:col0[k] + len(recvs[k])] = recvs[k].numpy()
+    tin, tbd = sh.tile_lists()
+    plan = [rank, [int(p) for p in peers], [int(sp[k + 1] - sp[k]) for k in range(len(peers))],
+            [int(rp[k + 1] - rp[k]) for k in range(len(peers))]]
+    plans = [None] * world
+    dist.all_gather_object(plans, plan)
+    ok = bool(np.array_equal(vals, truth))
+    tiles_ok = bool(np.array_equal(np.sort(np.concatenate([tin, tbd])), np.arange(sh.info.n_tiles)))
+    np.save(os.path.join(outdir, "shard_%d.npy" % rank),
+            np.array([ok, tiles_ok, sh.info.n_ghost > 0, len(tbd) > 0, len(peers)]))
+    if rank == 0:   # the plans agree pairwise: r sends p what p expects from r
+        cnt = {(r, p): (sn, rn) for r, ps, sns, rns in plans for p, sn, rn in zip(ps, sns, rns)}
+        sym = all((p, r) in cnt and cnt[(r, p)][0] == cnt[(p, r)][1] for (r, p) in cnt)
+        np.save(os.path.join(outdir, "sym.npy"), np.array([sym, len(cnt)]))
+    dist.destroy_process_group()
+
+
+SHARD_CASES = {
+    # name: (element type, nx, ny, px, py) -- subdomain ids sx * py + sy, so contiguous ranges are columns
+    "p1_strips": (0, 90, 12, 6, 1),
+    "q1_blocks_2x2": (1, 48, 20, 4, 4),
+}
+
+
+@pytest.mark.parametrize("case,world", [("p1_strips", 2), ("p1_strips", 3), ("q1_blocks_2x2", 3)])
+def test_gloo_shard_halo_plan_cpu(case, world):
+    """The C++ shard's halo plan on CPU ranks (world_size 2 and 3: a middle rank has two peers; Q1 block
+    subdomains): exchanging a field through it fills every ghost column with the owner's value, the plans
+    agree pairwise (what r sends p is what p receives from r), and the tile lists partition the owned tiles."""
+    import torch.multiprocessing as mp
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_shard_worker, args=(world, _free_port(), d, case), nprocs=world, join=True)
+        res = [np.load(os.path.join(d, "shard_%d.npy" % r)) for r in range(world)]
+        sym, n_links = np.load(os.path.join(d, "sym.npy"))
+    for r, (ok, tiles_ok, has_ghosts, has_bd, n_peers) in enumerate(res):
+        assert ok and tiles_ok and has_ghosts and has_bd, (r, res[r])
+    assert sym and n_links == 2 * (world - 1)
+    if world == 3:
+        assert res[1][4] == 2   # the middle rank talks to both neighbours
+
+
 def test_halo_tile_split():
     """hdd_amd.halo_tiles: interior and boundary tiles partition the owned tiles; every element with a
     ghost face neighbour sits in a boundary tile, and no interior-tile element has one."""
