@@ -606,6 +606,7 @@ extern "C" int hdd_shard_tile_lists(const hdd_shard* sh, int32_t* interior, int3
 extern "C" int hdd_shard_mesh(const hdd_shard* sh, hdd_mesh* m)
 {
   if (!sh || !m) return set_error(HDD_ERR_INVALID, "hdd_shard_mesh: null argument");
+  if (sh->host_only) return set_error(HDD_ERR_INVALID, "hdd_shard_mesh: host-only shard (no device mesh)");
   *m = hdd_mesh{sh->gi.elem_type, sh->gi.elem_type == HDD_HEX ? sh->degree : 1, sh->li.n_local, sh->li.own_begin,
                 sh->li.own_end, sh->d_coords, sh->d_nbrs, sh->d_finfo, sh->d_ev, sh->d_vxy};
   return HDD_OK;
@@ -629,6 +630,7 @@ extern "C" int hdd_shard_pattern_fill(hdd_ctx* ctx, const hdd_shard* sh, int64_t
 {
   if (!ctx || !sh || !d_row_ptr || !d_col || !d_elem_ptr)
     return set_error(HDD_ERR_INVALID, "hdd_shard_pattern_fill: null argument");
+  if (sh->host_only) return set_error(HDD_ERR_INVALID, "hdd_shard_pattern_fill: host-only shard (created without a context)");
   hdd_mesh m;
   hdd_shard_mesh(sh, &m);
   int64_t nnz = 0;
@@ -658,6 +660,8 @@ extern "C" int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm*
 {
   if (!ctx || !sh || !kappa || !tensor || !params || !pattern || !d_vals)
     return set_error(HDD_ERR_INVALID, "hdd_block_assemble_sharded: null argument");
+  if (sh->host_only)
+    return set_error(HDD_ERR_INVALID, "hdd_block_assemble_sharded: host-only shard (created without a context)");
   if (n_comp < 1 || n_comp > HDD_MAX_COMP)
     return set_error(HDD_ERR_INVALID, "hdd_block_assemble_sharded: need 1 <= n_comp <= HDD_MAX_COMP");
   if (pattern->nnz != sh->nnz || pattern->n_rows != int64_t(sh->gi.nb) * (sh->li.own_end - sh->li.own_begin))

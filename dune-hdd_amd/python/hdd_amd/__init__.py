@@ -716,7 +716,8 @@ class Shard:
         self.info = ShardInfo()
         _check(lib().hdd_shard_get_info(self.h, C.byref(self.info)), "hdd_shard_get_info")
         self.mesh = MeshT()
-        _check(lib().hdd_shard_mesh(self.h, C.byref(self.mesh)), "hdd_shard_mesh")
+        if ctx is not None:   # host-only shards have no device mesh
+            _check(lib().hdd_shard_mesh(self.h, C.byref(self.mesh)), "hdd_shard_mesh")
         i = self.info
         self.n_local, self.own_begin, self.own_end = i.n_local, i.own_begin, i.own_end
         self.n_own = i.own_end - i.own_begin

@@ -161,6 +161,19 @@ def test_gloo_shard_halo_plan_cpu(case, world):
         assert res[1][4] == 2   # the middle rank talks to both neighbours
 
 
+def test_host_only_shard_has_no_device_side():
+    """A shard created without a context answers the plan queries but refuses the device entry points
+    (hdd_shard_mesh / hdd_shard_pattern_fill / hdd_block_assemble_sharded) instead of handing out NULL arrays."""
+    _setup_paths()
+    import ctypes as C
+    import hdd_amd as H
+    g = H.Grid.structured(H.SIMPLEX, 40, 6, (0.0, 0.0), (5.0, 1.0), px=2, py=1)
+    sh = H.Shard(None, g, 2, 1)
+    peers, sp, idx, rp, col0 = sh.halo_lists()
+    assert list(peers) == [0] and sp[-1] == len(idx) > 0 and rp[-1] == sh.info.n_ghost
+    assert H.lib().hdd_shard_mesh(sh.h, C.byref(H.MeshT())) == 1    # HDD_ERR_INVALID
+
+
 def test_halo_tile_split():
     """hdd_amd.halo_tiles: interior and boundary tiles partition the owned tiles; every element with a
     ghost face neighbour sits in a boundary tile, and no interior-tile element has one."""
