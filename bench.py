@@ -55,6 +55,8 @@ def parse():
     ap.add_argument("--no-overlap", action="store_true",
                     help="N>1: exchange the halo before the whole assembly instead of overlapping it "
                          "with the interior tiles")
+    ap.add_argument("--probe-last", action="store_true",
+                    help="run the attainable-bandwidth probe after the timed steps (default: before the warmup)")
     ap.add_argument("--halo", default="step", choices=["step", "once"],
                     help="N>1: exchange the face halo in every step (default) or once at setup -- the mesh and "
                          "the coefficients are static, so a re-assembly needs no exchange (SURVEY.md 8(e))")
@@ -122,10 +124,11 @@ def cpu_baseline(nx_full, ny, target_s, cube=False):
                 cpu_model=_cpu_model(), host_cpus=os.cpu_count())
 
 
-def attainable_hbm(torch, nbytes=1 << 30, reps=10):
+def attainable_hbm(torch, nbytes=1 << 30, reps=None):
     """Attainable HBM bandwidth on this box, measured in the same run ('also report attainable
     BW from a device copy kernel'): a device-to-device copy (reads + writes) and a fill (writes only) of a
     1 GiB buffer, HIP events around `reps` back-to-back launches after one warm-up; GB/s of bytes moved."""
+    reps = reps or int(os.environ.get("HDD_BENCH_PROBE_REPS", "25"))
     a = torch.empty(nbytes // 8, dtype=torch.float64, device="cuda").fill_(1.0)
     b = torch.empty_like(a)
     out = {}
@@ -221,6 +224,11 @@ def main():
     def step(f=flags):
         H.assemble_sharded(ctx, shard, comm, kappa, tensor, pat_t, vals, flags=f)
 
+    # The attainable-bandwidth probe (1 GiB torch copy / fill, ~6 ms of HBM streaming) runs before the
+    # warmup on every rank: sustained HBM streaming on MI355X goes through a power-management transient
+    # (C2 launches 11-30 of a back-to-back run take 225-260 us, before and after 200-215 us:
+    # profiles/r02/s3/long/), and with the probe first the timed steps sit nearer the steady state.
+    att = None if args.probe_last else attainable_hbm(torch)
     # the first step fills the ghost columns (NaN until then); --halo once keeps them for the timed steps
     step()
     if args.halo == "once":
@@ -281,7 +289,8 @@ def main():
         elif world > 1:
             halo_desc = ", %s face halo%s" % ("RCCL" if args.backend == "nccl" else "gloo host-staged (rehearsal)",
                                               " overlapped with interior tiles" if not args.no_overlap else "")
-        att = attainable_hbm(torch)
+        if att is None:
+            att = attainable_hbm(torch)
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(nx // world, ny, args.cpu_seconds, cube=c4)
