@@ -248,7 +248,7 @@ int main(int argc, char** argv)
   }
 
   // 8. parametric right-hand side with kappa_p x g_D,q cross terms (swipdg.hh:257-330): OS2014 kappa, g_D(mu) =
-  //    sin(..) + mu cos(..) cos(..), g_N = 0, f = 1 on 8x8 Kuhn with AllDirichlet
+  //    sin(..) + mu cos(..) cos(..), g_N = 0, f = ESV2007 force on 8x8 Kuhn with AllDirichlet
   {
     S::Grid::Providers::Cube provider(HDD_SIMPLEX, {-1.0, -1.0}, {1.0, 1.0}, {8, 8});
     auto p = Problems::OS2014();

@@ -399,8 +399,9 @@ inline Problem ESV2007()
   return p;
 }
 
-// OS2014 (problems/OS2014.hh:63-76): kappa(mu) = 1 + 3/4 sin(4 pi (x + y/2)) - mu 3/4 sin(4 pi (x + y/2)), A = I,
-// f = 1 (integration order 3 of the Expression functions, 88-96)
+// OS2014::ParametricESV2007 (problems/OS2014.hh:63-76, 106-113): kappa(mu) = 1 + 3/4 sin(4 pi (x + y/2))
+// - mu 3/4 sin(4 pi (x + y/2)), A = I, f = ESV2007 Testcase1Force 1/2 pi^2 cos(pi x/2) cos(pi y/2)
+// (OS2014.hh:48, 110), g_D = g_N = 0; integration order 3 (OS2014.hh:86-96)
 inline Problem OS2014()
 {
   Problem p;
@@ -408,7 +409,7 @@ inline Problem OS2014()
   p.diffusion_factor.affine_part = ScalarFunction::sinusoid(1.0, 0.75, kx, ky, 3);
   p.diffusion_factor.register_component(ScalarFunction::sinusoid(0.0, -0.75, kx, ky, 3),
                                         Pymor::ParameterFunctional("mu", "mu", 1.0));
-  p.force = ScalarFunction::constant(1.0);
+  p.force = ScalarFunction::cos_product(0.5 * M_PI * M_PI, 0.5 * M_PI, 0.5 * M_PI, 0.0, 3);
   return p;
 }
 

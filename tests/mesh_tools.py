@@ -33,3 +33,25 @@ def nvb_mesh(n0, refines, lower=(-1.0, -1.0), upper=(1.0, 1.0)):
             new.append((c, b, m))
         tris = new
     return O.SIMPLEX, np.array(coords, dtype=np.float64), np.array(tris, dtype=np.int32)
+
+
+def affine_quad_mesh(nx, ny, M, c):
+    """Structured quads pushed through x -> M x + c: every element a general parallelogram (non-diagonal
+    Jacobian), Dune vertex order kept."""
+    et, coords, ev = O.cube_grid(nx, ny, (0, 0), (1, 1))
+    return et, coords @ np.asarray(M, float).T + np.asarray(c, float), ev
+
+
+def scrambled_quad_mesh(nx, ny, seed):
+    """Structured quads whose elements are renumbered by random symmetries of the reference square (Dune
+    cube vertex order kept valid: rotations and reflections), so neighbouring elements see each other's
+    faces under every twin-face id and orientation; then a shear."""
+    et, coords, ev = O.cube_grid(nx, ny, (0, 0), (1, 1))
+    rng = np.random.default_rng(seed)
+    # the 8 symmetries of the square as permutations of the lexicographic vertices (00, 10, 01, 11)
+    syms = [(0, 1, 2, 3), (1, 3, 0, 2), (3, 2, 1, 0), (2, 0, 3, 1),     # rotations
+            (1, 0, 3, 2), (2, 3, 0, 1), (0, 2, 1, 3), (3, 1, 2, 0)]     # reflections
+    pick = rng.integers(0, 8, ev.shape[0])
+    ev = np.stack([ev[k, list(syms[p])] for k, p in enumerate(pick)]).astype(np.int32)
+    coords = coords @ np.array([[1.1, 0.3], [0.0, 0.8]]).T
+    return et, coords, ev

@@ -8,6 +8,7 @@ import pytest
 
 import oracle as O
 from cases import SPE10_LOWER, SPE10_UPPER, compare_rows, os2014_components
+from mesh_tools import affine_quad_mesh as _affine_quad_mesh, scrambled_quad_mesh as _scrambled_quad_mesh
 
 H = pytest.importorskip("hdd_amd")
 pytestmark = pytest.mark.gpu
@@ -330,13 +331,6 @@ def test_edge_meshes(ctx, et, nx, ny):
     assert ok, worst
 
 
-def _affine_quad_mesh(nx, ny, M, c):
-    """Structured quads pushed through x -> M x + c: every element a general parallelogram (non-diagonal
-    Jacobian), Dune vertex order kept."""
-    et, coords, ev = O.cube_grid(nx, ny, (0, 0), (1, 1))
-    return et, coords @ np.asarray(M, float).T + np.asarray(c, float), ev
-
-
 @pytest.mark.parametrize("smooth", [False, True])
 def test_parallelogram_mesh_uniform_tiles(ctx, smooth):
     """Q1 on sheared/rotated parallelograms, large enough for tiles of 64 interior elements (the padded
@@ -368,21 +362,6 @@ def test_parallelogram_mesh_uniform_tiles(ctx, smooth):
     assert np.array_equal(col, ocol)
     worst, ok = compare_rows(rp, val, oval, RTOL)
     assert ok, worst
-
-
-def _scrambled_quad_mesh(nx, ny, seed):
-    """Structured quads whose elements are renumbered by random symmetries of the reference square (Dune
-    cube vertex order kept valid: rotations and reflections), so neighbouring elements see each other's
-    faces under every twin-face id and orientation; then a shear."""
-    et, coords, ev = O.cube_grid(nx, ny, (0, 0), (1, 1))
-    rng = np.random.default_rng(seed)
-    # the 8 symmetries of the square as permutations of the lexicographic vertices (00, 10, 01, 11)
-    syms = [(0, 1, 2, 3), (1, 3, 0, 2), (3, 2, 1, 0), (2, 0, 3, 1),     # rotations
-            (1, 0, 3, 2), (2, 3, 0, 1), (0, 2, 1, 3), (3, 1, 2, 0)]     # reflections
-    pick = rng.integers(0, 8, ev.shape[0])
-    ev = np.stack([ev[k, list(syms[p])] for k, p in enumerate(pick)]).astype(np.int32)
-    coords = coords @ np.array([[1.1, 0.3], [0.0, 0.8]]).T
-    return et, coords, ev
 
 
 @pytest.mark.parametrize("smooth", [False, True])

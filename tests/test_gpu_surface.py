@@ -209,7 +209,7 @@ def test_cpp_parametric_rhs_cross_terms(surface_run):
     k_1 = O.scalar(O.FN_SINUSOID, 0.0, -0.75, kx, ky, order=3)
     g_aff = O.scalar(O.FN_SINUSOID, 0.25, 0.5, 1.0, 2.0, order=3)
     g_1 = O.scalar(O.FN_COS_PRODUCT, 0.7, 0.0, 1.5, 0.5, order=3)
-    ref = [O.rhs_swipdg(og, force=O.scalar(O.FN_CONST, 1.0), kappa=k_aff, dirichlet=g_aff),
+    ref = [O.rhs_swipdg(og, force=O.esv2007_force(), kappa=k_aff, dirichlet=g_aff),
            O.rhs_swipdg(og, kappa=k_aff, dirichlet=g_1), O.rhs_swipdg(og, kappa=k_1, dirichlet=g_aff),
            O.rhs_swipdg(og, kappa=k_1, dirichlet=g_1)]
     got = [_ld(d, "prhs_affine")] + [_ld(d, "prhs_comp%d" % q) for q in range(3)]
