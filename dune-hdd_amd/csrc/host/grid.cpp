@@ -768,6 +768,22 @@ extern "C" int hdd_indicator(int64_t n, const double* centers, int32_t n_boxes, 
   return HDD_OK;
 }
 
+extern "C" int hdd_indicator_sum(int64_t n, const double* centers, int32_t n_boxes, const double* boxes, double* out)
+{
+  if (!centers || !out || n_boxes < 0 || (n_boxes && !boxes))
+    return set_error(HDD_ERR_INVALID, "hdd_indicator_sum: invalid argument");
+  for (int64_t e = 0; e < n; ++e) {
+    const double x = centers[e], y = centers[n + e];
+    double v = 0.0;
+    for (int32_t k = 0; k < n_boxes; ++k) {
+      const double* b = boxes + 5 * k;
+      if (b[0] <= x && x <= b[2] && b[1] <= y && y <= b[3]) v += b[4];
+    }
+    out[e] = v;
+  }
+  return HDD_OK;
+}
+
 // ------------------------------------------------------------------------------------------------
 // pattern
 // ------------------------------------------------------------------------------------------------

@@ -89,7 +89,7 @@ extern "C" void hdd_ctx_destroy(hdd_ctx* ctx)
 
 static int fn_order(const hdd_scalar_fn& f)
 {
-  return (f.kind == HDD_FN_SINUSOID || f.kind == HDD_FN_COS_PRODUCT) ? f.order : 0;
+  return (f.kind == HDD_FN_SINUSOID || f.kind == HDD_FN_COS_PRODUCT || f.kind == HDD_FN_FLATTOP) ? f.order : 0;
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -300,14 +300,16 @@ static int assemble_impl(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_fn* k
   const int ko = fn_order(kappa[0]);
   for (int c = 0; c < n_comp; ++c) {
     const hdd_scalar_fn& k = kappa[c];
-    if (k.kind != HDD_FN_CONST && k.kind != HDD_FN_PER_ELEM && k.kind != HDD_FN_SINUSOID)
+    if (k.kind != HDD_FN_CONST && k.kind != HDD_FN_PER_ELEM && k.kind != HDD_FN_SINUSOID && k.kind != HDD_FN_FLATTOP)
       return set_error(HDD_ERR_UNSUPPORTED, "hdd_swipdg_assemble: unknown diffusion factor kind");
     if (k.kind == HDD_FN_PER_ELEM && !k.per_elem)
       return set_error(HDD_ERR_INVALID, "hdd_swipdg_assemble: diffusion factor per_elem missing");
     if (fn_order(k) != ko)
       return set_error(HDD_ERR_UNSUPPORTED, "hdd_swipdg_assemble: components of different integration order");
     if (!d_vals[c]) return set_error(HDD_ERR_INVALID, "hdd_swipdg_assemble: null value array");
-    a.kappa[c] = KappaArg{k.kind, k.order, k.c, k.b, k.kx, k.ky, k.per_elem};
+    if (k.kind == HDD_FN_FLATTOP && (k.n_table < 0 || (k.n_table > 0 && !k.table)))
+      return set_error(HDD_ERR_INVALID, "hdd_swipdg_assemble: FLATTOP box table missing");
+    a.kappa[c] = KappaArg{k.kind, k.order, k.c, k.b, k.kx, k.ky, k.per_elem, k.table, k.n_table, 0};
     a.vals[c] = d_vals[c];
   }
   const int vol_order = p->vol_order >= 0 ? p->vol_order : ko;
@@ -684,8 +686,8 @@ int face_rule(int fdim, int order, double (*q)[3], int cap)
 
 hdd::dev::KappaArg kap_arg(const hdd_scalar_fn* f)
 {
-  if (!f) return hdd::dev::KappaArg{HDD_FN_CONST, 0, 0.0, 0.0, 0.0, 0.0, nullptr};
-  return hdd::dev::KappaArg{f->kind, f->order, f->c, f->b, f->kx, f->ky, f->per_elem};
+  if (!f) return hdd::dev::KappaArg{HDD_FN_CONST, 0, 0.0, 0.0, 0.0, 0.0, nullptr, nullptr, 0, 0};
+  return hdd::dev::KappaArg{f->kind, f->order, f->c, f->b, f->kx, f->ky, f->per_elem, f->table, f->n_table, 0};
 }
 }  // namespace
 
@@ -702,9 +704,13 @@ extern "C" int hdd_swipdg_rhs(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_
     return set_error(HDD_ERR_RANGE, "hdd_swipdg_rhs: 0 <= own_begin <= own_end <= n_local violated");
   if (dirichlet && (!kappa || !tensor))
     return set_error(HDD_ERR_INVALID, "hdd_swipdg_rhs: the Dirichlet functional needs kappa and the tensor");
-  for (const hdd_scalar_fn* f : {force, kappa, dirichlet, neumann})
+  for (const hdd_scalar_fn* f : {force, kappa, dirichlet, neumann}) {
     if (f && f->kind == HDD_FN_PER_ELEM && !f->per_elem)
       return set_error(HDD_ERR_INVALID, "hdd_swipdg_rhs: per_elem function without values");
+    if (f && f->kind == HDD_FN_FLATTOP && (m->elem_type == HDD_HEX || f->n_table < 0 || (f->n_table > 0 && !f->table)))
+      return set_error(f->n_table < 0 || !f->table ? HDD_ERR_INVALID : HDD_ERR_UNSUPPORTED,
+                       "hdd_swipdg_rhs: FLATTOP needs a box table and a 2d mesh");
+  }
   if (tensor && tensor->kind != HDD_TENSOR_CONST && !tensor->per_elem)
     return set_error(HDD_ERR_INVALID, "hdd_swipdg_rhs: tensor per_elem missing");
   const int deg = m->elem_type == HDD_HEX ? std::max(1, int(m->degree)) : 1;
@@ -779,6 +785,9 @@ extern "C" int hdd_product_assemble(hdd_ctx* ctx, const hdd_mesh* m, int32_t pro
     return set_error(HDD_ERR_INVALID, "hdd_product_assemble: elliptic / penalty products need kappa and the tensor");
   if (needs_coeff && kappa->kind == HDD_FN_PER_ELEM && !kappa->per_elem)
     return set_error(HDD_ERR_INVALID, "hdd_product_assemble: kappa per_elem missing");
+  if (needs_coeff && kappa->kind == HDD_FN_FLATTOP &&
+      (m->elem_type == HDD_HEX || kappa->n_table < 0 || (kappa->n_table > 0 && !kappa->table)))
+    return set_error(HDD_ERR_UNSUPPORTED, "hdd_product_assemble: FLATTOP needs a box table and a 2d mesh");
   if (needs_coeff && tensor->kind != HDD_TENSOR_CONST && !tensor->per_elem)
     return set_error(HDD_ERR_INVALID, "hdd_product_assemble: tensor per_elem missing");
   const int deg = m->elem_type == HDD_HEX ? std::max(1, int(m->degree)) : 1;
@@ -871,4 +880,144 @@ extern "C" int hdd_product_assemble(hdd_ctx* ctx, const hdd_mesh* m, int32_t pro
   }
   e = launch_product(a, static_cast<hipStream_t>(stream));
   return e == hipSuccess ? HDD_OK : hip_fail(e, "hdd_product_assemble: launch");
+}
+
+// ------------------------------------------------------------------------------------------------
+// block operators on the device (BlockSWIPDG::get_local_operator / get_coupling_operator,
+// block-swipdg.hh:625-676, 1328-1379): rows [r0, r1) of a sorted CSR pattern restricted to the columns
+// [c0, c1).  In the subdomain-major numbering the columns of one subdomain are ONE contiguous sub-range of
+// every sorted row, found by two binary searches: count -> scan -> fill, thread per row (rows hold <= 5 (2d)
+// or 7 (3d) blocks).  The values need no index map: a second pass copies each row's sub-range.
+// ------------------------------------------------------------------------------------------------
+namespace {
+__device__ __forceinline__ int64_t lower_bound_col(const int32_t* col, int64_t lo, int64_t hi, int64_t v)
+{
+  while (lo < hi) {
+    const int64_t m = (lo + hi) >> 1;
+    if (int64_t(col[m]) < v) lo = m + 1;
+    else hi = m;
+  }
+  return lo;
+}
+
+__global__ void __launch_bounds__(256) subcsr_count_kernel(const int64_t* __restrict__ rp, const int32_t* __restrict__ col,
+                                                           int64_t r0, int64_t n, int64_t c0, int64_t c1,
+                                                           int64_t* __restrict__ out_rp)
+{
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t a = rp[r0 + i], b = rp[r0 + i + 1];
+    const int64_t lo = lower_bound_col(col, a, b, c0);
+    out_rp[i + 1] = lower_bound_col(col, lo, b, c1) - lo;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) out_rp[0] = 0;
+}
+
+__global__ void __launch_bounds__(256) subcsr_fill_kernel(const int64_t* __restrict__ rp, const int32_t* __restrict__ col,
+                                                          int64_t r0, int64_t n, int64_t c0,
+                                                          const int64_t* __restrict__ out_rp, int32_t* __restrict__ out_col,
+                                                          int64_t* __restrict__ out_src)
+{
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t lo = lower_bound_col(col, rp[r0 + i], rp[r0 + i + 1], c0);
+    const int64_t k0 = out_rp[i], len = out_rp[i + 1] - k0;
+    for (int64_t j = 0; j < len; ++j) {
+      out_col[k0 + j] = int32_t(int64_t(col[lo + j]) - c0);
+      if (out_src) out_src[k0 + j] = lo + j;
+    }
+  }
+}
+
+struct ValPtrs {
+  const double* in[HDD_MAX_COMP];
+  double* out[HDD_MAX_COMP];
+};
+
+__global__ void __launch_bounds__(256) subcsr_values_kernel(const int64_t* __restrict__ rp, const int32_t* __restrict__ col,
+                                                            int64_t r0, int64_t n, int64_t c0,
+                                                            const int64_t* __restrict__ out_rp, ValPtrs v, int nc)
+{
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t lo = lower_bound_col(col, rp[r0 + i], rp[r0 + i + 1], c0);
+    const int64_t k0 = out_rp[i], len = out_rp[i + 1] - k0;
+    for (int c = 0; c < nc; ++c)
+      for (int64_t j = 0; j < len; ++j) v.out[c][k0 + j] = v.in[c][lo + j];
+  }
+}
+
+int subcsr_check(const hdd_csr* p, int64_t r0, int64_t r1, int64_t c0, int64_t c1, const char* who)
+{
+  if (!p || !p->row_ptr || !p->col) return set_error(HDD_ERR_INVALID, std::string(who) + ": pattern arrays missing");
+  if (r0 < 0 || r1 < r0 || r1 > p->n_rows || c0 < 0 || c1 < c0)
+    return set_error(HDD_ERR_RANGE, std::string(who) + ": 0 <= row_begin <= row_end <= n_rows, col_begin <= col_end violated");
+  if (c1 - c0 > int64_t(INT32_MAX)) return set_error(HDD_ERR_RANGE, std::string(who) + ": column range exceeds int32");
+  return HDD_OK;
+}
+
+unsigned rows_grid(int64_t n, int n_cu) { return unsigned(std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, int64_t(n_cu) * 16))); }
+}  // namespace
+
+extern "C" int hdd_block_operator_map_device(hdd_ctx* ctx, const hdd_csr* pattern, int64_t row_begin, int64_t row_end,
+                                             int64_t col_begin, int64_t col_end, int64_t* d_out_row_ptr,
+                                             int32_t* d_out_col, int64_t* d_out_src, int64_t* nnz, void* stream)
+{
+  if (!ctx || !d_out_row_ptr) return set_error(HDD_ERR_INVALID, "hdd_block_operator_map_device: null argument");
+  if (int rc = subcsr_check(pattern, row_begin, row_end, col_begin, col_end, "hdd_block_operator_map_device")) return rc;
+  hipError_t e = hipSetDevice(ctx->device);
+  if (e != hipSuccess) return hip_fail(e, "hdd_block_operator_map_device: hipSetDevice");
+  const hipStream_t s = static_cast<hipStream_t>(stream);
+  const int64_t n = row_end - row_begin;
+  const unsigned grid = rows_grid(n, ctx->n_cu);
+  hipLaunchKernelGGL(subcsr_count_kernel, dim3(grid), dim3(256), 0, s, pattern->row_ptr, pattern->col, row_begin, n,
+                     col_begin, col_end, d_out_row_ptr);
+  if ((e = hipGetLastError()) != hipSuccess) return hip_fail(e, "hdd_block_operator_map_device: count");
+  if (n > 0) {
+    size_t tmp = 0;
+    e = hipcub::DeviceScan::InclusiveSum(nullptr, tmp, d_out_row_ptr + 1, d_out_row_ptr + 1, n, s);
+    if (e != hipSuccess) return hip_fail(e, "hdd_block_operator_map_device: scan size");
+    if (tmp > ctx->scan_ws_bytes) {   // grows once per context (one stream at a time per context)
+      (void)hipStreamSynchronize(s);
+      if (ctx->scan_ws) (void)hipFree(ctx->scan_ws);
+      ctx->scan_ws = nullptr;
+      ctx->scan_ws_bytes = 0;
+      if ((e = hipMalloc(&ctx->scan_ws, tmp)) != hipSuccess) return hip_fail(e, "hdd_block_operator_map_device: scratch");
+      ctx->scan_ws_bytes = tmp;
+    }
+    e = hipcub::DeviceScan::InclusiveSum(ctx->scan_ws, tmp, d_out_row_ptr + 1, d_out_row_ptr + 1, n, s);
+    if (e != hipSuccess) return hip_fail(e, "hdd_block_operator_map_device: scan");
+  }
+  if (d_out_col) {
+    hipLaunchKernelGGL(subcsr_fill_kernel, dim3(grid), dim3(256), 0, s, pattern->row_ptr, pattern->col, row_begin, n,
+                       col_begin, d_out_row_ptr, d_out_col, d_out_src);
+    if ((e = hipGetLastError()) != hipSuccess) return hip_fail(e, "hdd_block_operator_map_device: fill");
+  }
+  if (nnz) {
+    e = hipMemcpyAsync(nnz, d_out_row_ptr + n, sizeof(int64_t), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return hip_fail(e, "hdd_block_operator_map_device: read nnz");
+  }
+  return HDD_OK;
+}
+
+extern "C" int hdd_block_operator_values_device(hdd_ctx* ctx, const hdd_csr* pattern, int64_t row_begin, int64_t row_end,
+                                                int64_t col_begin, int64_t col_end, const int64_t* d_out_row_ptr,
+                                                const double* const* d_vals, int32_t n_comp, double* const* d_out,
+                                                void* stream)
+{
+  if (!ctx || !d_out_row_ptr || !d_vals || !d_out || n_comp < 0 || n_comp > HDD_MAX_COMP)
+    return set_error(HDD_ERR_INVALID, "hdd_block_operator_values_device: invalid argument");
+  if (int rc = subcsr_check(pattern, row_begin, row_end, col_begin, col_end, "hdd_block_operator_values_device")) return rc;
+  ValPtrs v{};
+  for (int c = 0; c < n_comp; ++c) {
+    if (!d_vals[c] || !d_out[c]) return set_error(HDD_ERR_INVALID, "hdd_block_operator_values_device: null value array");
+    v.in[c] = d_vals[c];
+    v.out[c] = d_out[c];
+  }
+  hipError_t e = hipSetDevice(ctx->device);
+  if (e != hipSuccess) return hip_fail(e, "hdd_block_operator_values_device: hipSetDevice");
+  const int64_t n = row_end - row_begin;
+  if (n == 0 || n_comp == 0) return HDD_OK;
+  hipLaunchKernelGGL(subcsr_values_kernel, dim3(rows_grid(n, ctx->n_cu)), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     pattern->row_ptr, pattern->col, row_begin, n, col_begin, d_out_row_ptr, v, int(n_comp));
+  e = hipGetLastError();
+  return e == hipSuccess ? HDD_OK : hip_fail(e, "hdd_block_operator_values_device: launch");
 }

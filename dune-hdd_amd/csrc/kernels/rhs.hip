@@ -14,6 +14,7 @@
 #include <cstdint>
 
 #include "swipdg_kernels.hh"
+#include "flattop.hh"
 #include "trig_phase.hh"
 
 namespace hdd {
@@ -24,6 +25,7 @@ __device__ __forceinline__ double rhs_fn(const KappaArg& f, int64_t e, const dou
   switch (f.kind) {
     case HDD_FN_PER_ELEM: return f.per_elem[e];
     case HDD_FN_SINUSOID: return f.c + f.b * sin_phase(f.kx * x[0] + f.ky * x[1]);
+    case HDD_FN_FLATTOP: return flattop_sum(f.table, f.n_table, f.c, f.b, x[0], x[1]);
     case HDD_FN_COS_PRODUCT:
       return f.c * cos_phase(f.kx * x[0]) * cos_phase(f.ky * x[1]) * ((dim == 3 && f.b != 0.0) ? cos_phase(f.b * x[2]) : 1.0);
     default: return f.c;

@@ -1,1887 +1,9 @@
-// dune-hdd_amd/csrc/kernels/swipdg_assemble.hip
-//
-// CDNA4 (gfx950) kernels of the SWIPDG stiffness assembly -- the MI355X replacement of dune-gdt's
-// SystemAssembler::walk() over Operators::EllipticSWIPDG (reference call sites:
-// dune/hdd/linearelliptic/discretizations/swipdg.hh:218-249, 485; block-swipdg.hh:1136-1179, 1270-1326).
-//
-// Design:
-//   * owner-computes: the rows of an element are written by the lanes that own the element; every face
-//     term is evaluated by the row owner on its side (entity/entity + entity/neighbour blocks), so each
-//     CSR value is written exactly once, with no atomics and no zero-fill, in one pass over the mesh;
-//   * a workgroup = one tile of 64 consecutive owned elements; WPE waves per tile, wave w owns the local
-//     test functions (rows) [w*RPT, (w+1)*RPT) of the 64 elements, lane = element (coalesced SoA loads);
-//   * the row block of an element is contiguous in the CSR value array (sorted blocks, element-blocked
-//     DoFs), so each wave stages one row of its 64 elements in LDS and streams it out with consecutive
-//     lanes on consecutive values (6-12 cache lines per store instruction instead of 64);
-//   * reference-element basis/quadrature tables are compile-time constants (immediates), not LDS: at
-//     p = 1 they are a handful of numbers per rule;
-//   * the neighbour geometry is rebuilt from the shared face vertices plus the neighbour's non-face
-//     vertices (twin face / orientation from face_info), so a face gathers 2 (triangle) or 4 (quad)
-//     coordinates, the neighbour's tensor and coefficient;
-//   * XCD-aware tile order: consecutive tiles run on one XCD so the neighbour rows above/below a tile
-//     hit that XCD's L2.
-#include <hip/hip_runtime.h>
-
-#include <cstdint>
-#include <algorithm>
-#include <cstdlib>
-#include <type_traits>
-
-#include "hdd.h"
-#include "swipdg_kernels.hh"
-#include "trig_phase.hh"
-
-#ifndef HDD_MIN_WAVES_PER_EU
-#define HDD_MIN_WAVES_PER_EU 4
-#endif
-// profiling ablations (HDD_DEBUG_FLAGS at run time) exist only in a library built with -DHDD_ABLATION
-// (scripts/ablate.py): 1 = skip compute, 2 = drop the value stores, 4 = skip the neighbour gathers
-#ifdef HDD_ABLATION
-#define HDD_ABL(a, bit) (((a).debug_flags & (bit)) != 0)
-#else
-#define HDD_ABL(a, bit) false
-#endif
+// dune-hdd_amd/csrc/kernels/swipdg_assemble.hip -- dispatch of the SWIPDG stiffness / product kernels
+// (swipdg_device.hh) and the wave-per-row fallback kernels for the remaining quadrature rules.
+#include "swipdg_device.hh"
 
 namespace hdd {
 namespace dev {
-
-// ------------------------------------------------------------------------------------------------
-// reference elements (Dune numbering) and shape functions
-// ------------------------------------------------------------------------------------------------
-struct Simplex {
-  static constexpr int NV = 3, NF = 3, NB = 3;
-  // vertex k of the reference simplex: (0,0), (1,0), (0,1)
-  __host__ __device__ static constexpr double rv(int k, int d) { return (k == 1 + d) ? 1.0 : 0.0; }
-  // faces 0:(0,1) 1:(0,2) 2:(1,2)
-  __host__ __device__ static constexpr int fv(int f, int k) { return f == 0 ? k : (f == 1 ? 2 * k : 1 + k); }
-  // orientation of (t_y, -t_x) w.r.t. the outer normal on the reference element
-  __host__ __device__ static constexpr double face_sign(int f) { return f == 1 ? -1.0 : 1.0; }
-  __device__ static inline void shape(double x, double y, double* phi, double* gx, double* gy)
-  {
-    phi[0] = 1.0 - x - y; phi[1] = x; phi[2] = y;
-    gx[0] = -1.0; gy[0] = -1.0;
-    gx[1] = 1.0;  gy[1] = 0.0;
-    gx[2] = 0.0;  gy[2] = 1.0;
-  }
-};
-
-struct Cube {
-  static constexpr int NV = 4, NF = 4, NB = 4;
-  // vertex k: (k & 1, k >> 1)
-  __host__ __device__ static constexpr double rv(int k, int d) { return double((k >> d) & 1); }
-  // faces 0:(0,2) 1:(1,3) 2:(0,1) 3:(2,3)
-  __host__ __device__ static constexpr int fv(int f, int k)
-  {
-    return f == 0 ? 2 * k : (f == 1 ? 1 + 2 * k : (f == 2 ? k : 2 + k));
-  }
-  __host__ __device__ static constexpr double face_sign(int f) { return (f == 0 || f == 3) ? -1.0 : 1.0; }
-  __device__ static inline void shape(double x, double y, double* phi, double* gx, double* gy)
-  {
-    phi[0] = (1 - x) * (1 - y); phi[1] = x * (1 - y); phi[2] = (1 - x) * y; phi[3] = x * y;
-    gx[0] = -(1 - y); gy[0] = -(1 - x);
-    gx[1] = (1 - y);  gy[1] = -x;
-    gx[2] = -y;       gy[2] = (1 - x);
-    gx[3] = y;        gy[3] = x;
-  }
-};
-
-// ------------------------------------------------------------------------------------------------
-// quadrature (compile-time): Gauss-Legendre on [0,1]; simplex centroid / 3-point / Dunavant-6
-// ------------------------------------------------------------------------------------------------
-template <int N>
-struct Gauss01;
-template <>
-struct Gauss01<1> {
-  __device__ static constexpr double s(int) { return 0.5; }
-  __device__ static constexpr double w(int) { return 1.0; }
-};
-template <>
-struct Gauss01<2> {
-  __device__ static constexpr double s(int q) { return q == 0 ? 0.21132486540518711775 : 0.78867513459481288225; }
-  __device__ static constexpr double w(int) { return 0.5; }
-};
-template <>
-struct Gauss01<3> {
-  __device__ static constexpr double s(int q)
-  {
-    return q == 0 ? 0.11270166537925831148 : (q == 1 ? 0.5 : 0.88729833462074168852);
-  }
-  __device__ static constexpr double w(int q) { return q == 1 ? 8.0 / 18.0 : 5.0 / 18.0; }
-};
-
-template <class E, int NQ>
-struct VolRule;
-template <>
-struct VolRule<Simplex, 1> {
-  __device__ static constexpr double x(int) { return 1.0 / 3.0; }
-  __device__ static constexpr double y(int) { return 1.0 / 3.0; }
-  __device__ static constexpr double w(int) { return 0.5; }
-};
-template <>
-struct VolRule<Simplex, 3> {
-  __device__ static constexpr double x(int q) { return q == 1 ? 2.0 / 3.0 : 1.0 / 6.0; }
-  __device__ static constexpr double y(int q) { return q == 2 ? 2.0 / 3.0 : 1.0 / 6.0; }
-  __device__ static constexpr double w(int) { return 1.0 / 6.0; }
-};
-template <>
-struct VolRule<Simplex, 6> {  // Dunavant degree 4 (used for integrand orders 3 and 4)
-  static constexpr double A = 0.44594849091596488632, WA = 0.22338158967801146570;
-  static constexpr double B = 0.091576213509770743460, WB = 0.10995174365532186764;
-  __device__ static constexpr double pa(int k, int d) { return k == 0 ? A : ((k == 1) == (d == 0) ? 1 - 2 * A : A); }
-  __device__ static constexpr double pb(int k, int d) { return k == 0 ? B : ((k == 1) == (d == 0) ? 1 - 2 * B : B); }
-  __device__ static constexpr double x(int q) { return q < 3 ? pa(q, 0) : pb(q - 3, 0); }
-  __device__ static constexpr double y(int q) { return q < 3 ? pa(q, 1) : pb(q - 3, 1); }
-  __device__ static constexpr double w(int q) { return q < 3 ? 0.5 * WA : 0.5 * WB; }
-};
-template <int NQ>
-struct VolRule<Cube, NQ> {   // tensor Gauss, NQ = n*n, point q = j*n + i
-  static constexpr int N = NQ == 1 ? 1 : (NQ == 4 ? 2 : 3);
-  __device__ static constexpr double x(int q) { return Gauss01<N>::s(q % N); }
-  __device__ static constexpr double y(int q) { return Gauss01<N>::s(q / N); }
-  __device__ static constexpr double w(int q) { return Gauss01<N>::w(q % N) * Gauss01<N>::w(q / N); }
-};
-
-// ------------------------------------------------------------------------------------------------
-// coefficients
-// ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ double kappa_elem(const KappaArg& k, int64_t e)
-{
-  return k.kind == HDD_FN_PER_ELEM ? k.per_elem[e] : k.c;
-}
-// |F|^-beta for beta != 1 (the 2d default is beta = 1/(d-1) = 1, taken inline as 1/|F|): out of line, so
-// libm's pow and its registers stay out of the closed-form kernels' main path (P1 226 -> 191 VGPRs, Q1
-// 62 -> 26 AGPR spill slots)
-__device__ __attribute__((noinline)) double inv_pow(double len, double beta) { return 1.0 / pow(len, beta); }
-__device__ __forceinline__ double kappa_at(const KappaArg& k, double pe, double x, double y)
-{
-  return k.kind == HDD_FN_SINUSOID ? k.c + k.b * sin_phase(k.kx * x + k.ky * y) : pe;
-}
-
-typedef double dvec2 __attribute__((ext_vector_type(2)));
-
-struct Tensor {
-  double a00, a01, a11;
-};
-__device__ __forceinline__ Tensor tensor_of(const AssembleArgs& a, int64_t e)
-{
-  Tensor t;
-  if (a.tkind == HDD_TENSOR_ISO_PER_ELEM) {
-    const double v = a.tper[e];
-    t.a00 = v; t.a01 = 0.0; t.a11 = v;
-  } else if (a.tkind == HDD_TENSOR_SYM_PER_ELEM) {
-    t.a00 = a.tper[e]; t.a01 = a.tper[a.n_local + e]; t.a11 = a.tper[2 * a.n_local + e];
-  } else {
-    t.a00 = a.tc0; t.a01 = a.tc1; t.a11 = a.tc2;
-  }
-  return t;
-}
-// (A g) . n
-__device__ __forceinline__ double agn(const Tensor& A, double gx, double gy, double nx, double ny)
-{
-  return (A.a00 * gx + A.a01 * gy) * nx + (A.a01 * gx + A.a11 * gy) * ny;
-}
-
-// affine geometry x = v0 + J xh;  J^{-T} for the gradients
-struct Geom {
-  double x0, y0, j00, j01, j10, j11, det, i00, i01, i10, i11;   // i = J^{-1}
-  __device__ __forceinline__ void init(double ax, double ay, double bx, double by, double cx, double cy)
-  {
-    x0 = ax; y0 = ay;
-    j00 = bx - ax; j01 = cx - ax; j10 = by - ay; j11 = cy - ay;
-    det = j00 * j11 - j01 * j10;
-    const double id = 1.0 / det;
-    i00 = j11 * id; i01 = -j01 * id; i10 = -j10 * id; i11 = j00 * id;
-  }
-  __device__ __forceinline__ void grad(double ghx, double ghy, double& gx, double& gy) const
-  {
-    gx = i00 * ghx + i10 * ghy;
-    gy = i01 * ghx + i11 * ghy;
-  }
-  __device__ __forceinline__ void global(double xh, double yh, double& x, double& y) const
-  {
-    x = x0 + j00 * xh + j01 * yh;
-    y = y0 + j10 * xh + j11 * yh;
-  }
-};
-
-// ------------------------------------------------------------------------------------------------
-// per-thread element context (loaded once, shared by all components)
-// ------------------------------------------------------------------------------------------------
-template <class E>
-struct ElemCtx {
-  double X[E::NV], Y[E::NV];
-  int32_t nbr[E::NF];
-  uint32_t finfo;
-  Tensor A;
-  Geom G;
-  double adet, osgn;
-  int64_t e;
-  int pos_self, pos[E::NF], rowlen;
-  double* img;   // LDS image of this element's row block
-};
-
-// geometry of the neighbour across face f: shared face vertices + the neighbour's non-face vertices
-template <class E>
-struct NbrFace {
-  Geom H;
-  Tensor A;
-  int ta, tb, to;   // neighbour local vertices on the face (matching my fv(f,0) / fv(f,1) unless rev)
-  bool rev;
-};
-
-template <class E, int F>
-__device__ __forceinline__ void load_neighbor(const AssembleArgs& a, const ElemCtx<E>& c, int32_t n, NbrFace<E>& nf)
-{
-  const int64_t ne = a.n_local;
-  constexpr int fa = E::fv(F, 0), fb = E::fv(F, 1);
-  const uint32_t inf = (c.finfo >> (4 * F)) & 15u;
-  const int tw = int(inf & 7u);
-  nf.rev = (inf & 8u) != 0u;
-  nf.ta = E::fv(tw, 0);
-  nf.tb = E::fv(tw, 1);
-  const double PAx = nf.rev ? c.X[fb] : c.X[fa], PAy = nf.rev ? c.Y[fb] : c.Y[fa];
-  const double PBx = nf.rev ? c.X[fa] : c.X[fb], PBy = nf.rev ? c.Y[fa] : c.Y[fb];
-  double NX[E::NV], NY[E::NV];
-  if constexpr (E::NV == 3) {
-    nf.to = 3 - nf.ta - nf.tb;
-    const double Ox = a.coords[(2 * nf.to) * ne + n], Oy = a.coords[(2 * nf.to + 1) * ne + n];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      NX[k] = k == nf.ta ? PAx : (k == nf.tb ? PBx : Ox);
-      NY[k] = k == nf.ta ? PAy : (k == nf.tb ? PBy : Oy);
-    }
-  } else {
-    nf.to = -1;
-    const int tc = E::fv(tw ^ 1, 0), td = E::fv(tw ^ 1, 1);
-    const double Cx = a.coords[(2 * tc) * ne + n], Cy = a.coords[(2 * tc + 1) * ne + n];
-    const double Dx = a.coords[(2 * td) * ne + n], Dy = a.coords[(2 * td + 1) * ne + n];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      NX[k] = k == nf.ta ? PAx : (k == nf.tb ? PBx : (k == tc ? Cx : Dx));
-      NY[k] = k == nf.ta ? PAy : (k == nf.tb ? PBy : (k == tc ? Cy : Dy));
-    }
-  }
-  nf.H.init(NX[0], NY[0], NX[1], NY[1], NX[2], NY[2]);
-  nf.A = tensor_of(a, n);
-}
-
-struct FaceGeo {
-  double len, nx, ny, hpow, tx, ty, xa, ya;
-};
-
-template <class E, int F>
-__device__ __forceinline__ FaceGeo face_geo(const AssembleArgs& a, const ElemCtx<E>& c)
-{
-  constexpr int fa = E::fv(F, 0), fb = E::fv(F, 1);
-  FaceGeo g;
-  g.xa = c.X[fa];
-  g.ya = c.Y[fa];
-  g.tx = c.X[fb] - c.X[fa];
-  g.ty = c.Y[fb] - c.Y[fa];
-  g.len = sqrt(g.tx * g.tx + g.ty * g.ty);
-  const double nsc = E::face_sign(F) * c.osgn / g.len;
-  g.nx = g.ty * nsc;
-  g.ny = -g.tx * nsc;
-  g.hpow = a.beta == 1.0 ? g.len : pow(g.len, a.beta);
-  return g;
-}
-
-// ------------------------------------------------------------------------------------------------
-// row I of one component, P1 simplex with piecewise-constant coefficients: closed-form face integrals
-// (exactly what the reference's order-2 Gauss rule integrates: int phi = |F|/2, int phi phi = |F|/6 (1+d_ij))
-// ------------------------------------------------------------------------------------------------
-template <int I>
-__device__ __forceinline__ void row_simplex_pwc(const AssembleArgs& a, const ElemCtx<Simplex>& c, const KappaArg& K)
-{
-  using E = Simplex;
-  const double ke = kappa_elem(K, c.e);
-  double g[3][2];
-  {
-    double phi[3], ghx[3], ghy[3];
-    E::shape(1.0 / 3.0, 1.0 / 3.0, phi, ghx, ghy);
-#pragma unroll
-    for (int k = 0; k < 3; ++k) c.G.grad(ghx[k], ghy[k], g[k][0], g[k][1]);
-  }
-  double self[3];
-  {
-    const double fac = 0.5 * c.adet;   // 1-point rule: weight 1/2 * |det J|
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      const double Agx = c.A.a00 * g[j][0] + c.A.a01 * g[j][1];
-      const double Agy = c.A.a01 * g[j][0] + c.A.a11 * g[j][1];
-      self[j] = fac * ke * (Agx * g[I][0] + Agy * g[I][1]);
-    }
-  }
-#pragma unroll
-  for (int f = 0; f < 3; ++f) {
-    const int32_t n = c.nbr[f];
-    if (n <= HDD_NBR_NEUMANN) continue;
-    FaceGeo fg;
-    double Ae[3];
-    // face f as a compile-time constant for the helpers
-    if (f == 0) fg = face_geo<E, 0>(a, c);
-    else if (f == 1) fg = face_geo<E, 1>(a, c);
-    else fg = face_geo<E, 2>(a, c);
-#pragma unroll
-    for (int k = 0; k < 3; ++k) Ae[k] = agn(c.A, g[k][0], g[k][1], fg.nx, fg.ny);
-    const int fa = E::fv(f, 0), fb = E::fv(f, 1), fc = 3 - fa - fb;
-    const double half = 0.5 * fg.len, third = fg.len / 3.0, sixth = fg.len / 6.0;
-    const double M1I = I == fc ? 0.0 : half;
-    const double dm = agn(c.A, fg.nx, fg.ny, fg.nx, fg.ny);
-    if (n >= 0) {
-      NbrFace<E> nf;
-      if (f == 0) load_neighbor<E, 0>(a, c, n, nf);
-      else if (f == 1) load_neighbor<E, 1>(a, c, n, nf);
-      else load_neighbor<E, 2>(a, c, n, nf);
-      const double kn = kappa_elem(K, n);
-      const double dp = agn(nf.A, fg.nx, fg.ny, fg.nx, fg.ny);
-      const double gamma = (dp * dm) / (dp + dm);
-      const double w_plus = dm / (dp + dm);
-      const double w_minus = dp / (dp + dm);
-      const double pen = (ke * kn * a.sigma_inner * gamma) / fg.hpow;
-      double An[3];
-      {
-        double phi[3], ghx[3], ghy[3];
-        E::shape(1.0 / 3.0, 1.0 / 3.0, phi, ghx, ghy);
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-          double hx, hy;
-          nf.H.grad(ghx[k], ghy[k], hx, hy);
-          An[k] = agn(nf.A, hx, hy, fg.nx, fg.ny);
-        }
-      }
-      // neighbour vertex matching my vertex I (only meaningful if I is on the face)
-      const int mI = (I == fa) ? (nf.rev ? nf.tb : nf.ta) : (nf.rev ? nf.ta : nf.tb);
-      double* out = c.img + c.pos[f] * 3;
-#pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        const double M1j = j == nf.to ? 0.0 : half;
-        const double Mx = I == fc ? 0.0 : (j == mI ? third : (j == nf.to ? 0.0 : sixth));
-        out[j] = -w_plus * kn * An[j] * M1I + w_minus * ke * Ae[I] * M1j - pen * Mx;
-      }
-#pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        const double M1j = j == fc ? 0.0 : half;
-        const double Mm = (I == fc || j == fc) ? 0.0 : (I == j ? third : sixth);
-        self[j] += -w_minus * ke * (Ae[j] * M1I + Ae[I] * M1j) + pen * Mm;
-      }
-    } else {   // Dirichlet: SWIPDG::BoundaryLHS
-      const double pen = (a.sigma_boundary * ke * dm) / fg.hpow;
-#pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        const double M1j = j == fc ? 0.0 : half;
-        const double Mm = (I == fc || j == fc) ? 0.0 : (I == j ? third : sixth);
-        self[j] += -ke * (Ae[j] * M1I + Ae[I] * M1j) + pen * Mm;
-      }
-    }
-  }
-  double* out = c.img + c.pos_self * 3;
-#pragma unroll
-  for (int j = 0; j < 3; ++j) out[j] = self[j];
-}
-
-// ------------------------------------------------------------------------------------------------
-// row I of one component, generic quadrature (Q1 quads; smooth coefficients on either element)
-// ------------------------------------------------------------------------------------------------
-template <class E, int NQV, int NQF, int I>
-__device__ __forceinline__ void row_quadrature(const AssembleArgs& a, const ElemCtx<E>& c, const KappaArg& K)
-{
-  constexpr int NB = E::NB, NF = E::NF;
-  const double ke = kappa_elem(K, c.e);
-  double self[NB];
-#pragma unroll
-  for (int j = 0; j < NB; ++j) self[j] = 0.0;
-  // ---- LocalEvaluation::Elliptic ----
-#pragma unroll
-  for (int q = 0; q < NQV; ++q) {
-    double phi[NB], ghx[NB], ghy[NB], gx[NB], gy[NB];
-    E::shape(VolRule<E, NQV>::x(q), VolRule<E, NQV>::y(q), phi, ghx, ghy);
-#pragma unroll
-    for (int k = 0; k < NB; ++k) c.G.grad(ghx[k], ghy[k], gx[k], gy[k]);
-    double px = 0.0, py = 0.0;
-    if (K.kind == HDD_FN_SINUSOID) c.G.global(VolRule<E, NQV>::x(q), VolRule<E, NQV>::y(q), px, py);
-    const double kap = kappa_at(K, ke, px, py);
-    const double fac = VolRule<E, NQV>::w(q) * c.adet;
-#pragma unroll
-    for (int j = 0; j < NB; ++j) {
-      const double Agx = c.A.a00 * gx[j] + c.A.a01 * gy[j];
-      const double Agy = c.A.a01 * gx[j] + c.A.a11 * gy[j];
-      self[j] += fac * kap * (Agx * gx[I] + Agy * gy[I]);
-    }
-  }
-  // ---- faces ----
-#pragma unroll
-  for (int f = 0; f < NF; ++f) {
-    const int32_t n = c.nbr[f];
-    if (n <= HDD_NBR_NEUMANN) continue;
-    FaceGeo fg;
-    if (f == 0) fg = face_geo<E, 0>(a, c);
-    else if (f == 1) fg = face_geo<E, 1>(a, c);
-    else if (f == 2) fg = face_geo<E, 2 % NF>(a, c);
-    else fg = face_geo<E, 3 % NF>(a, c);
-    const int fa = E::fv(f, 0), fb = E::fv(f, 1);
-    const double rax = E::rv(fa, 0), ray = E::rv(fa, 1), rbx = E::rv(fb, 0), rby = E::rv(fb, 1);
-    const double dm = agn(c.A, fg.nx, fg.ny, fg.nx, fg.ny);
-    if (n >= 0) {
-      NbrFace<E> nf;
-      if (f == 0) load_neighbor<E, 0>(a, c, n, nf);
-      else if (f == 1) load_neighbor<E, 1>(a, c, n, nf);
-      else if (f == 2) load_neighbor<E, 2 % NF>(a, c, n, nf);
-      else load_neighbor<E, 3 % NF>(a, c, n, nf);
-      const double kn = kappa_elem(K, n);
-      const double dp = agn(nf.A, fg.nx, fg.ny, fg.nx, fg.ny);
-      const double gamma = (dp * dm) / (dp + dm);
-      const double w_plus = dm / (dp + dm);
-      const double w_minus = dp / (dp + dm);
-      const double sax = E::rv(nf.ta, 0), say = E::rv(nf.ta, 1), sbx = E::rv(nf.tb, 0), sby = E::rv(nf.tb, 1);
-      double nbv[NB];
-#pragma unroll
-      for (int j = 0; j < NB; ++j) nbv[j] = 0.0;
-#pragma unroll
-      for (int q = 0; q < NQF; ++q) {
-        const double s = Gauss01<NQF>::s(q);
-        double pe[NB], ghx[NB], ghy[NB], gex[NB], gey[NB];
-        E::shape(rax + s * (rbx - rax), ray + s * (rby - ray), pe, ghx, ghy);
-#pragma unroll
-        for (int k = 0; k < NB; ++k) c.G.grad(ghx[k], ghy[k], gex[k], gey[k]);
-        const double sn = nf.rev ? 1.0 - s : s;
-        double pn[NB], hhx[NB], hhy[NB], gnx[NB], gny[NB];
-        E::shape(sax + sn * (sbx - sax), say + sn * (sby - say), pn, hhx, hhy);
-#pragma unroll
-        for (int k = 0; k < NB; ++k) nf.H.grad(hhx[k], hhy[k], gnx[k], gny[k]);
-        double kme = ke, knb = kn;
-        if (K.kind == HDD_FN_SINUSOID) {
-          kme = kappa_at(K, ke, fg.xa + s * fg.tx, fg.ya + s * fg.ty);
-          knb = kme;
-        }
-        const double pen = (kme * knb * a.sigma_inner * gamma) / fg.hpow;
-        const double fac = Gauss01<NQF>::w(q) * fg.len;
-        double Ae[NB], An[NB];
-#pragma unroll
-        for (int k = 0; k < NB; ++k) {
-          Ae[k] = agn(c.A, gex[k], gey[k], fg.nx, fg.ny);
-          An[k] = agn(nf.A, gnx[k], gny[k], fg.nx, fg.ny);
-        }
-#pragma unroll
-        for (int j = 0; j < NB; ++j) {
-          self[j] += fac * (-w_minus * kme * Ae[j] * pe[I] - w_minus * kme * pe[j] * Ae[I] + pen * pe[j] * pe[I]);
-          nbv[j] += fac * (-w_plus * knb * An[j] * pe[I] + w_minus * kme * pn[j] * Ae[I] - pen * pn[j] * pe[I]);
-        }
-      }
-      double* out = c.img + c.pos[f] * NB;
-#pragma unroll
-      for (int j = 0; j < NB; ++j) out[j] = nbv[j];
-    } else {   // Dirichlet
-#pragma unroll
-      for (int q = 0; q < NQF; ++q) {
-        const double s = Gauss01<NQF>::s(q);
-        double pe[NB], ghx[NB], ghy[NB], gex[NB], gey[NB];
-        E::shape(rax + s * (rbx - rax), ray + s * (rby - ray), pe, ghx, ghy);
-#pragma unroll
-        for (int k = 0; k < NB; ++k) c.G.grad(ghx[k], ghy[k], gex[k], gey[k]);
-        double kme = ke;
-        if (K.kind == HDD_FN_SINUSOID) kme = kappa_at(K, ke, fg.xa + s * fg.tx, fg.ya + s * fg.ty);
-        const double pen = (a.sigma_boundary * kme * dm) / fg.hpow;
-        const double fac = Gauss01<NQF>::w(q) * fg.len;
-        double Ae[NB];
-#pragma unroll
-        for (int k = 0; k < NB; ++k) Ae[k] = agn(c.A, gex[k], gey[k], fg.nx, fg.ny);
-#pragma unroll
-        for (int j = 0; j < NB; ++j) self[j] += fac * (-kme * Ae[j] * pe[I] - kme * pe[j] * Ae[I] + pen * pe[j] * pe[I]);
-      }
-    }
-  }
-  double* out = c.img + c.pos_self * NB;
-#pragma unroll
-  for (int j = 0; j < NB; ++j) out[j] = self[j];
-}
-
-template <class E, int NQV, int NQF, bool PWC, int I>
-__device__ __forceinline__ void row(const AssembleArgs& a, const ElemCtx<E>& c, const KappaArg& K)
-{
-  if constexpr (PWC && std::is_same<E, Simplex>::value && NQV == 1 && NQF == 2)
-    row_simplex_pwc<I>(a, c, K);
-  else
-    row_quadrature<E, NQV, NQF, I>(a, c, K);
-}
-
-// ------------------------------------------------------------------------------------------------
-// the kernel: one workgroup = 64 consecutive owned elements x NB waves (wave w = local row w)
-// ------------------------------------------------------------------------------------------------
-template <class E, int NQV, int NQF, bool PWC>
-__global__ void __launch_bounds__(64 * E::NB, HDD_MIN_WAVES_PER_EU)
-swipdg_assemble_kernel(const AssembleArgs a)
-{
-  constexpr int NB = E::NB, NF = E::NF, NV = E::NV;
-  extern __shared__ __attribute__((aligned(16))) double lds[];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-
-  // XCD-aware tile order (bijective): hardware block b runs on XCD b % 8; each XCD gets a contiguous
-  // range of tiles so the element rows above / below a tile sit in the same L2.
-  const int64_t nwg = gridDim.x;
-  const int64_t b = blockIdx.x;
-  const int64_t q8 = nwg >> 3, r8 = nwg & 7, xcd = b & 7;
-  const int64_t tile = xcd * q8 + (xcd < r8 ? xcd : r8) + (b >> 3);
-
-  const int64_t t0 = a.own_begin + tile * 64;
-  const int64_t tend = t0 + 64 < a.own_end ? t0 + 64 : a.own_end;
-  const int64_t e = t0 + lane;
-  const bool active = e < tend;
-  const int64_t ne = a.n_local;
-  const int64_t* eptr = a.elem_ptr - a.own_begin;
-  const int64_t base = eptr[t0];
-  const int64_t base_al = base & ~int64_t(1);          // 16-byte aligned image origin
-  const int64_t tile_end = eptr[tend];
-
-  ElemCtx<E> c;
-  c.e = active ? e : t0;   // inactive tail lanes shadow a valid element; their LDS writes are skipped
-#pragma unroll
-  for (int k = 0; k < NV; ++k) {
-    c.X[k] = a.coords[(2 * k) * ne + c.e];
-    c.Y[k] = a.coords[(2 * k + 1) * ne + c.e];
-  }
-#pragma unroll
-  for (int f = 0; f < NF; ++f) c.nbr[f] = a.nbrs[f * ne + c.e];
-  c.finfo = a.finfo[c.e];
-  c.A = tensor_of(a, c.e);
-  const int64_t my_off = eptr[c.e];
-  c.G.init(c.X[0], c.Y[0], c.X[1], c.Y[1], c.X[2], c.Y[2]);
-  c.adet = fabs(c.G.det);
-  c.osgn = c.G.det > 0.0 ? 1.0 : -1.0;
-  int nblk = 1;
-  c.pos_self = 0;
-#pragma unroll
-  for (int f = 0; f < NF; ++f) {
-    nblk += c.nbr[f] >= 0;
-    c.pos_self += (c.nbr[f] >= 0 && c.nbr[f] < c.e);
-  }
-#pragma unroll
-  for (int f = 0; f < NF; ++f) {
-    int p = (c.e < c.nbr[f]) ? 1 : 0;
-#pragma unroll
-    for (int g = 0; g < NF; ++g) p += (c.nbr[g] >= 0 && c.nbr[g] < c.nbr[f]);
-    c.pos[f] = p;
-  }
-  c.rowlen = nblk * NB;
-  // lanes past the tile end write to a scratch row after the image
-  c.img = active ? lds + (my_off - base_al) + int64_t(wave) * c.rowlen
-                 : lds + 64 * NB * (NF + 1) * NB + 2;
-
-  // one component per launch (the host loops over the affine components): a component loop in here
-  // would let the compiler hoist every component-invariant face quantity of all faces above the loop
-  {
-    const KappaArg K = a.kappa[0];
-    double* out = a.vals[0];
-    switch (wave) {
-      case 0: row<E, NQV, NQF, PWC, 0>(a, c, K); break;
-      case 1: row<E, NQV, NQF, PWC, 1>(a, c, K); break;
-      case 2: row<E, NQV, NQF, PWC, 2>(a, c, K); break;
-      default: if constexpr (NB > 3) row<E, NQV, NQF, PWC, NB - 1>(a, c, K); break;
-    }
-    __syncthreads();
-    // stream the tile's contiguous row blocks [base, tile_end) out of LDS, 16 bytes per lane
-    const int64_t lo = base_al, hi = tile_end;
-    const int64_t n2 = (hi - lo) >> 1;
-    for (int64_t k = threadIdx.x; k < n2; k += blockDim.x) {
-      const int64_t gi = lo + 2 * k;
-      const dvec2 v = *reinterpret_cast<const dvec2*>(lds + 2 * k);
-      if (gi >= base) {
-        __builtin_nontemporal_store(v, reinterpret_cast<dvec2*>(out + gi));
-      } else {   // first pair straddles the tile start: only the upper value is ours
-        out[gi + 1] = v.y;
-      }
-    }
-    if (((hi - lo) & 1) && threadIdx.x == 0) out[hi - 1] = lds[hi - 1 - lo];
-  }
-}
-
-// ------------------------------------------------------------------------------------------------
-// P1 simplex, piecewise-constant coefficients: one thread per element computes all 3 rows.
-//
-// Face terms in "role" form: for face f with my vertices a = fv(f,0), b = fv(f,1), the neighbour's
-// vertices are named by their physical position (role A = position of my a, B = position of my b,
-// O = the neighbour's opposite vertex).  Then every coefficient of the entity/entity and
-// entity/neighbour blocks is orientation-free, and the twin face / reversal only decides the three LDS
-// column slots j(A), j(B), j(O) the entity/neighbour values are stored to.  The neighbour gradients come
-// from the triangle (A, B, O) (barycentric gradients), so a face gathers only O (2 doubles), the
-// neighbour tensor and, if per element, its diffusion factor.
-//
-// fp64 reciprocals / rsqrt use the hardware estimate + two Newton steps (< 1 ulp off the IEEE result);
-// the oracle comparison tolerance is 1e-12 of the row maximum.
-// ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ double rcp_nr(double x)
-{
-  double r = __builtin_amdgcn_rcp(x);
-  double e = fma(-x, r, 1.0);
-  r = fma(r, e, r);
-  e = fma(-x, r, 1.0);
-  return fma(r, e, r);
-}
-__device__ __forceinline__ double rsq_nr(double x)
-{
-  double y = __builtin_amdgcn_rsq(x);
-  double h = 0.5 * x;
-  y = y * fma(-h * y, y, 1.5);
-  y = y * fma(-h * y, y, 1.5);
-  return y;
-}
-
-// ------------------------------------------------------------------------------------------------
-// Persistent, software-pipelined variant of the P1 kernel.
-//
-// gfx950's vmcnt is in order and counts stores: a wave that waits for a load issued after its stores
-// also waits for those stores.  So each wave walks a sequence of tiles and orders its memory operations
-//   [prefetch own data of tile t+1] [compute tile t -> LDS] [gathers of tile t+1] [stores of tile t]
-// The loads of tile t+1 are in flight while tile t computes, the neighbour gathers are issued before the
-// store burst, and the stores are branch-free buffer stores (fixed count, out-of-range ones dropped by
-// the descriptor's range check), so the next wait can stay counted instead of draining the stores.
-// ------------------------------------------------------------------------------------------------
-struct P1Own {
-  double X[3], Y[3];
-  int32_t nbr[3];
-  uint32_t finfo;
-  Tensor A;
-  double ke;
-  int32_t vid[3];   // vertex-indexed geometry (VX): local vertex ids; X / Y then arrive with the gathers
-};
-struct P1Gat {
-  double Ox[3], Oy[3];
-  Tensor Ap[3];
-  double kn[3];
-  int32_t ov[3];    // VX: the neighbour's off-face vertex id; Ox / Oy arrive in the second gather stage
-};
-
-// vertex (x, y) of the vertex-indexed geometry: one 16-byte load
-__device__ __forceinline__ void vertex_xy(const AssembleArgs& a, int32_t v, double& x, double& y)
-{
-  const dvec2 p = *reinterpret_cast<const dvec2*>(a.vxy + 2 * int64_t(v));
-  x = p.x;
-  y = p.y;
-}
-
-template <int TK>
-__device__ __forceinline__ Tensor tensor_k(const AssembleArgs& a, int64_t e)
-{
-  Tensor t;
-  if constexpr (TK == HDD_TENSOR_ISO_PER_ELEM) {
-    const double v = a.tper[e];
-    t.a00 = v; t.a01 = 0.0; t.a11 = v;
-  } else if constexpr (TK == HDD_TENSOR_SYM_PER_ELEM) {
-    t.a00 = a.tper[e]; t.a01 = a.tper[a.n_local + e]; t.a11 = a.tper[2 * a.n_local + e];
-  } else {
-    t.a00 = a.tc0; t.a01 = a.tc1; t.a11 = a.tc2;
-  }
-  return t;
-}
-template <int KK>
-__device__ __forceinline__ double kappa_k(const AssembleArgs& a, int64_t e)
-{
-  if constexpr (KK == HDD_FN_PER_ELEM) return a.kappa[0].per_elem[e];
-  else return a.kappa[0].c;
-}
-
-// Own-data loads of a tile (coalesced SoA).  VX: vertex ids instead of coordinates -- the vertex
-// coordinates are then gathered with the neighbour data (p1_load_gat), the neighbour's off-face vertex in a
-// second stage (p1_load_gat2) that the persistent driver issues after the tile's stores.
-template <int TK, int KK, bool VX = false>
-__device__ __forceinline__ void p1_load_own(const AssembleArgs& a, int64_t e, P1Own& o)
-{
-  const int64_t ne = a.n_local;
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    if constexpr (VX) {
-      o.vid[k] = a.ev[k * ne + e];
-    } else {
-      o.X[k] = a.coords[(2 * k) * ne + e];
-      o.Y[k] = a.coords[(2 * k + 1) * ne + e];
-    }
-  }
-#pragma unroll
-  for (int f = 0; f < 3; ++f) o.nbr[f] = a.nbrs[f * ne + e];
-  o.finfo = a.finfo[e];
-  o.A = tensor_k<TK>(a, e);
-  o.ke = kappa_k<KK>(a, e);
-}
-
-template <int TK, int KK, bool VX = false>
-__device__ __forceinline__ void p1_load_gat(const AssembleArgs& a, int64_t e, P1Own& o, P1Gat& g)
-{
-  const int64_t ne = a.n_local;
-  if constexpr (VX) {
-#pragma unroll
-    for (int k = 0; k < 3; ++k) vertex_xy(a, o.vid[k], o.X[k], o.Y[k]);
-  }
-#pragma unroll
-  for (int f = 0; f < 3; ++f) {
-    const int64_t n = o.nbr[f] >= 0 ? int64_t(o.nbr[f]) : e;   // boundary faces: harmless own reload
-    const uint32_t inf = (o.finfo >> (4 * f)) & 15u;
-    const int tw = int(inf & 7u);
-    const int to = 3 - Simplex::fv(tw, 0) - Simplex::fv(tw, 1);
-    if constexpr (VX) {
-      g.ov[f] = a.ev[to * ne + n];
-    } else {
-      g.Ox[f] = a.coords[(2 * to) * ne + n];
-      g.Oy[f] = a.coords[(2 * to + 1) * ne + n];
-    }
-    g.Ap[f] = tensor_k<TK>(a, n);
-    g.kn[f] = kappa_k<KK>(a, n);
-  }
-}
-template <bool VX>
-__device__ __forceinline__ void p1_load_gat2(const AssembleArgs& a, P1Gat& g)
-{
-  if constexpr (VX) {
-#pragma unroll
-    for (int f = 0; f < 3; ++f) vertex_xy(a, g.ov[f], g.Ox[f], g.Oy[f]);
-  }
-}
-
-// P1 closed-form per-element math on preloaded data (role form, see above); writes the row block into `img`.
-// PEN: only the interior-penalty terms (the SWIPDG penalty product, swipdg.hh:462-508), no volume and no
-// consistency / symmetry terms.
-template <bool PEN = false>
-__device__ __forceinline__ void p1_compute(const AssembleArgs& a, int64_t e, const P1Own& o, const P1Gat& gt,
-                                           double* img)
-{
-  using E = Simplex;
-  const double j00 = o.X[1] - o.X[0], j01 = o.X[2] - o.X[0], j10 = o.Y[1] - o.Y[0], j11 = o.Y[2] - o.Y[0];
-  const double det = j00 * j11 - j01 * j10;
-  const double id = rcp_nr(det);
-  const double i00 = j11 * id, i01 = -j01 * id, i10 = -j10 * id, i11 = j00 * id;
-  double g[3][2];
-  g[1][0] = i00; g[1][1] = i01;
-  g[2][0] = i10; g[2][1] = i11;
-  g[0][0] = -i00 - i10; g[0][1] = -i01 - i11;
-  double Ag[3][2];
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    Ag[k][0] = o.A.a00 * g[k][0] + o.A.a01 * g[k][1];
-    Ag[k][1] = o.A.a01 * g[k][0] + o.A.a11 * g[k][1];
-  }
-  const double adet = fabs(det);
-  const double osgn = det > 0.0 ? 1.0 : -1.0;
-  int nblk = 1, pos_self = 0, pos[3];
-#pragma unroll
-  for (int f = 0; f < 3; ++f) {
-    nblk += o.nbr[f] >= 0;
-    pos_self += (o.nbr[f] >= 0 && o.nbr[f] < e);
-  }
-#pragma unroll
-  for (int f = 0; f < 3; ++f) {
-    int p = (e < o.nbr[f]) ? 1 : 0;
-#pragma unroll
-    for (int q = 0; q < 3; ++q) p += (o.nbr[q] >= 0 && o.nbr[q] < o.nbr[f]);
-    pos[f] = p;
-  }
-  const int rowlen = nblk * 3;
-  const double ke = o.ke;
-  double S[3][3];
-  {
-    const double fac = PEN ? 0.0 : 0.5 * adet * ke;
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-#pragma unroll
-      for (int j = 0; j < 3; ++j) S[i][j] = fac * (Ag[j][0] * g[i][0] + Ag[j][1] * g[i][1]);
-  }
-  constexpr double CS = PEN ? 0.0 : 1.0;   // consistency / symmetry terms on (stiffness) or off (penalty)
-#pragma unroll
-  for (int f = 0; f < 3; ++f) {
-    const int32_t n = o.nbr[f];
-    if (n <= HDD_NBR_NEUMANN) continue;
-    const int fa = E::fv(f, 0), fb = E::fv(f, 1), fc = 3 - fa - fb;
-    const double tx = o.X[fb] - o.X[fa], ty = o.Y[fb] - o.Y[fa];
-    const double il = rsq_nr(tx * tx + ty * ty);
-    const double len = (tx * tx + ty * ty) * il;
-    const double nsc = E::face_sign(f) * osgn * il;
-    const double nx = ty * nsc, ny = -tx * nsc;
-    double Ae[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) Ae[k] = Ag[k][0] * nx + Ag[k][1] * ny;
-    const double dm = agn(o.A, nx, ny, nx, ny);
-    const double ihp = a.beta == 1.0 ? il : inv_pow(len, a.beta);
-    const double half = 0.5 * len, third = len * (1.0 / 3.0), sixth = len * (1.0 / 6.0);
-    if (n >= 0) {
-      const uint32_t inf = (o.finfo >> (4 * f)) & 15u;
-      const int tw = int(inf & 7u);
-      const bool rev = (inf & 8u) != 0u;
-      const int ta = E::fv(tw, 0), tb = E::fv(tw, 1), to = 3 - ta - tb;
-      const double Ox = gt.Ox[f], Oy = gt.Oy[f];
-      const Tensor Ap = gt.Ap[f];
-      const double kn = gt.kn[f];
-      const double dp = agn(Ap, nx, ny, nx, ny);
-      const double rs = rcp_nr(dp + dm);
-      const double gamma = (dp * dm) * rs;
-      const double w_plus = dm * rs, w_minus = dp * rs;
-      const double pen = (ke * kn * a.sigma_inner * gamma) * ihp;
-      const double Ax = o.X[fa], Ay = o.Y[fa], Bx = o.X[fb], By = o.Y[fb];
-      const double iD = rcp_nr((Bx - Ax) * (Oy - Ay) - (By - Ay) * (Ox - Ax));
-      const double mx = Ap.a00 * nx + Ap.a01 * ny, my = Ap.a01 * nx + Ap.a11 * ny;
-      const double AnA = ((By - Oy) * mx + (Ox - Bx) * my) * iD;
-      const double AnB = ((Oy - Ay) * mx + (Ax - Ox) * my) * iD;
-      const double AnO = ((Ay - By) * mx + (Bx - Ax) * my) * iD;
-      const int jA = rev ? tb : ta, jB = rev ? ta : tb;
-      const double cpl = -w_plus * kn * CS;
-      const double sym = w_minus * ke * CS;
-#pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        double* row = img + i * rowlen + pos[f] * 3;
-        const double m1i = i == fc ? 0.0 : half;
-        row[jA] = cpl * AnA * m1i + sym * Ae[i] * half - pen * (i == fc ? 0.0 : (i == fa ? third : sixth));
-        row[jB] = cpl * AnB * m1i + sym * Ae[i] * half - pen * (i == fc ? 0.0 : (i == fb ? third : sixth));
-        row[to] = cpl * AnO * m1i;
-      }
-#pragma unroll
-      for (int i = 0; i < 3; ++i)
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          const double m1i = i == fc ? 0.0 : half, m1j = j == fc ? 0.0 : half;
-          const double mm = (i == fc || j == fc) ? 0.0 : (i == j ? third : sixth);
-          S[i][j] += -w_minus * ke * CS * (Ae[j] * m1i + Ae[i] * m1j) + pen * mm;
-        }
-    } else {
-      const double pen = (a.sigma_boundary * ke * dm) * ihp;
-#pragma unroll
-      for (int i = 0; i < 3; ++i)
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          const double m1i = i == fc ? 0.0 : half, m1j = j == fc ? 0.0 : half;
-          const double mm = (i == fc || j == fc) ? 0.0 : (i == j ? third : sixth);
-          S[i][j] += -ke * CS * (Ae[j] * m1i + Ae[i] * m1j) + pen * mm;
-        }
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < 3; ++i)
-#pragma unroll
-    for (int j = 0; j < 3; ++j) img[i * rowlen + pos_self * 3 + j] = S[i][j];
-}
-
-typedef int ivec4 __attribute__((ext_vector_type(4)));
-
-// ------------------------------------------------------------------------------------------------
-// Generic thread-per-element policy (Q1 parallelograms, smooth coefficients): quadrature at compile-time
-// points on my side, "role" coordinates on the neighbour side.  Roles are named by physical position
-// (A = my fv(f,0), B = my fv(f,1), third role = the neighbour vertex next to A off the face, fourth
-// (cubes) = next to B) and numbered like the reference element, so the neighbour's basis in role
-// coordinates is E::shape at the compile-time point (s, 0) and only the LDS column slots depend on the
-// twin face / reversal.  Gathers per face: one neighbour vertex (2 doubles), its tensor, its kappa.
-// ------------------------------------------------------------------------------------------------
-template <class E>
-struct GOwn {
-  double X[E::NV], Y[E::NV];
-  int32_t nbr[E::NF];
-  uint32_t finfo;
-  Tensor A;
-  double ke;
-  int32_t vid[E::NV];   // VX: local vertex ids (as P1Own)
-};
-template <class E>
-struct GGat {
-  double Cx[E::NF], Cy[E::NF];
-  Tensor Ap[E::NF];
-  double kn[E::NF];
-  int32_t ov[E::NF];    // VX: the neighbour's third-role vertex id
-};
-
-template <class E>
-__device__ __forceinline__ int role_slot(uint32_t finfo, int f, int r)
-{
-  const uint32_t inf = (finfo >> (4 * f)) & 15u;
-  const int tw = int(inf & 7u);
-  const bool rev = (inf & 8u) != 0u;
-  const int ka = rev ? 1 : 0;
-  if (r == 0) return E::fv(tw, ka);
-  if (r == 1) return E::fv(tw, 1 - ka);
-  if constexpr (E::NV == 3) return 3 - E::fv(tw, 0) - E::fv(tw, 1);
-  else return r == 2 ? E::fv(tw ^ 1, ka) : E::fv(tw ^ 1, 1 - ka);
-}
-
-// One lane's row block in the LDS tile image, written at index i -> (i + rot) mod RB (rot = 0: plain).
-// Uniform Q1 tiles use rot = 2 ((lane >> 1) & 15): see the persistent kernel's image comment.
-template <int RB>
-struct RotImg {
-  double* p;
-  int rot;
-  __device__ __forceinline__ double& operator[](int i) const
-  {
-    const unsigned q = unsigned(i + rot);
-    return p[q < unsigned(RB) ? q : q - unsigned(RB)];
-  }
-};
-
-template <class E, int NQV, int NQF, int TK, int KK, bool VX = false>
-struct GenericPolicy {
-  static constexpr int NB = E::NB, NF = E::NF, NV = E::NV;
-  static constexpr int RB = (NF + 1) * NB * NB;
-  // workgroups (single-wave tiles) per CU and the register cap: simplices (18 KB tiles) run 8 per CU at
-  // <= 256 registers (2 waves / SIMD hide the sinusoid's VALU latency: C3 0.278 -> 0.241 ms per component,
-  // profiles/r01/s2/ab1.log); quads are LDS-bound at 4 per CU (40 KB rotated image) and keep the full
-  // register file (capping them at 256 spills: 0.84 -> 1.30 ms)
-  static constexpr int WGCU = NB == 4 ? 4 : 8;
-  static constexpr int MINW = NB == 4 ? 1 : 2;
-  static constexpr bool PAD = NB == 4;   // rotated LDS image for uniform tiles (see the persistent kernel)
-  using Own = GOwn<E>;
-  using Gat = GGat<E>;
-
-  __device__ static void load_own(const AssembleArgs& a, int64_t e, Own& o)
-  {
-    const int64_t ne = a.n_local;
-#pragma unroll
-    for (int k = 0; k < NV; ++k) {
-      if constexpr (VX) {
-        o.vid[k] = a.ev[k * ne + e];
-      } else {
-        o.X[k] = a.coords[(2 * k) * ne + e];
-        o.Y[k] = a.coords[(2 * k + 1) * ne + e];
-      }
-    }
-#pragma unroll
-    for (int f = 0; f < NF; ++f) o.nbr[f] = a.nbrs[f * ne + e];
-    o.finfo = a.finfo[e];
-    o.A = tensor_k<TK>(a, e);
-    o.ke = KK == HDD_FN_SINUSOID ? 0.0 : kappa_k<KK == HDD_FN_PER_ELEM ? HDD_FN_PER_ELEM : HDD_FN_CONST>(a, e);
-  }
-
-  __device__ static void load_gat(const AssembleArgs& a, int64_t e, Own& o, Gat& g)
-  {
-    const int64_t ne = a.n_local;
-    if constexpr (VX) {
-#pragma unroll
-      for (int k = 0; k < NV; ++k) vertex_xy(a, o.vid[k], o.X[k], o.Y[k]);
-    }
-#pragma unroll
-    for (int f = 0; f < NF; ++f) {
-      const int64_t n = o.nbr[f] >= 0 ? int64_t(o.nbr[f]) : e;
-      const int c = role_slot<E>(o.finfo, f, 2);
-      if constexpr (VX) {
-        g.ov[f] = a.ev[c * ne + n];
-      } else {
-        g.Cx[f] = a.coords[(2 * c) * ne + n];
-        g.Cy[f] = a.coords[(2 * c + 1) * ne + n];
-      }
-      g.Ap[f] = tensor_k<TK>(a, n);
-      g.kn[f] = KK == HDD_FN_SINUSOID ? 0.0 : kappa_k<KK == HDD_FN_PER_ELEM ? HDD_FN_PER_ELEM : HDD_FN_CONST>(a, n);
-    }
-  }
-
-  __device__ static void load_gat2(const AssembleArgs& a, Gat& g)
-  {
-    if constexpr (VX) {
-#pragma unroll
-      for (int f = 0; f < NF; ++f) vertex_xy(a, g.ov[f], g.Cx[f], g.Cy[f]);
-    }
-  }
-
-  __device__ static double kap(const AssembleArgs& a, double x, double y)
-  {
-    const KappaArg& K = a.kappa[0];
-    return K.c + K.b * sin_phase(K.kx * x + K.ky * y);
-  }
-
-  __device__ static int n_interior(const Own& o)
-  {
-    int c = 0;
-#pragma unroll
-    for (int f = 0; f < NF; ++f) c += o.nbr[f] >= 0;
-    return c;
-  }
-
-  template <class IMG>
-  __device__ static void compute(const AssembleArgs& a, int64_t e, const Own& o, const Gat& gt, IMG img)
-  {
-    Geom G;
-    G.init(o.X[0], o.Y[0], o.X[1], o.Y[1], o.X[2], o.Y[2]);
-    const double adet = fabs(G.det);
-    const double osgn = G.det > 0.0 ? 1.0 : -1.0;
-    int pos_self = 0, pos[NF];
-#pragma unroll
-    for (int f = 0; f < NF; ++f) pos_self += (o.nbr[f] >= 0 && o.nbr[f] < e);
-#pragma unroll
-    for (int f = 0; f < NF; ++f) {
-      int p = (e < o.nbr[f]) ? 1 : 0;
-#pragma unroll
-      for (int q = 0; q < NF; ++q) p += (o.nbr[q] >= 0 && o.nbr[q] < o.nbr[f]);
-      pos[f] = p;
-    }
-    const int rowlen = (n_interior(o) + 1) * NB;
-    double S[NB][NB];
-#pragma unroll
-    for (int i = 0; i < NB; ++i)
-#pragma unroll
-      for (int j = 0; j < NB; ++j) S[i][j] = 0.0;
-    // ---- LocalEvaluation::Elliptic ----
-#pragma unroll
-    for (int q = 0; q < NQV; ++q) {
-      double phi[NB], ghx[NB], ghy[NB], gx[NB], gy[NB];
-      E::shape(VolRule<E, NQV>::x(q), VolRule<E, NQV>::y(q), phi, ghx, ghy);
-#pragma unroll
-      for (int k = 0; k < NB; ++k) G.grad(ghx[k], ghy[k], gx[k], gy[k]);
-      double kq = o.ke;
-      if constexpr (KK == HDD_FN_SINUSOID) {
-        double px, py;
-        G.global(VolRule<E, NQV>::x(q), VolRule<E, NQV>::y(q), px, py);
-        kq = kap(a, px, py);
-      }
-      const double fac = VolRule<E, NQV>::w(q) * adet * kq;
-#pragma unroll
-      for (int j = 0; j < NB; ++j) {
-        const double Agx = o.A.a00 * gx[j] + o.A.a01 * gy[j];
-        const double Agy = o.A.a01 * gx[j] + o.A.a11 * gy[j];
-#pragma unroll
-        for (int i = 0; i < NB; ++i) S[i][j] += fac * (Agx * gx[i] + Agy * gy[i]);
-      }
-    }
-    // ---- faces ----
-#pragma unroll
-    for (int f = 0; f < NF; ++f) {
-      const int32_t n = o.nbr[f];
-      if (n <= HDD_NBR_NEUMANN) continue;
-      const int fa = E::fv(f, 0), fb = E::fv(f, 1);
-      const double Ax = o.X[fa], Ay = o.Y[fa], Bx = o.X[fb], By = o.Y[fb];
-      const double tx = Bx - Ax, ty = By - Ay;
-      const double il = rsq_nr(tx * tx + ty * ty);
-      const double len = (tx * tx + ty * ty) * il;
-      const double nsc = E::face_sign(f) * osgn * il;
-      const double nx = ty * nsc, ny = -tx * nsc;
-      const double dm = agn(o.A, nx, ny, nx, ny);
-      const double ihp = a.beta == 1.0 ? il : inv_pow(len, a.beta);
-      const double rax = E::rv(fa, 0), ray = E::rv(fa, 1), rbx = E::rv(fb, 0), rby = E::rv(fb, 1);
-      if (n >= 0) {
-        Geom Hn;   // neighbour in role coordinates: A = (0,0), B = (1,0), third role = (0,1)
-        Hn.init(Ax, Ay, Bx, By, gt.Cx[f], gt.Cy[f]);
-        const Tensor Ap = gt.Ap[f];
-        const double dp = agn(Ap, nx, ny, nx, ny);
-        const double rs = rcp_nr(dp + dm);
-        const double gamma = (dp * dm) * rs;
-        const double w_plus = dm * rs, w_minus = dp * rs;
-        double EN[NB][NB];
-#pragma unroll
-        for (int i = 0; i < NB; ++i)
-#pragma unroll
-          for (int j = 0; j < NB; ++j) EN[i][j] = 0.0;
-#pragma unroll
-        for (int q = 0; q < NQF; ++q) {
-          const double s = Gauss01<NQF>::s(q);
-          double pe[NB], ghx[NB], ghy[NB], gex[NB], gey[NB];
-          E::shape(rax + s * (rbx - rax), ray + s * (rby - ray), pe, ghx, ghy);
-#pragma unroll
-          for (int k = 0; k < NB; ++k) G.grad(ghx[k], ghy[k], gex[k], gey[k]);
-          double pn[NB], hhx[NB], hhy[NB];
-          E::shape(s, 0.0, pn, hhx, hhy);
-          double kme = o.ke, knb = gt.kn[f];
-          if constexpr (KK == HDD_FN_SINUSOID) {
-            kme = kap(a, Ax + s * tx, Ay + s * ty);
-            knb = kme;
-          }
-          const double pen = (kme * knb * a.sigma_inner * gamma) * ihp;
-          const double fac = Gauss01<NQF>::w(q) * len;
-          double Ae[NB], An[NB];
-#pragma unroll
-          for (int k = 0; k < NB; ++k) {
-            double hx, hy;
-            Hn.grad(hhx[k], hhy[k], hx, hy);
-            Ae[k] = agn(o.A, gex[k], gey[k], nx, ny);
-            An[k] = agn(Ap, hx, hy, nx, ny);
-          }
-#pragma unroll
-          for (int i = 0; i < NB; ++i)
-#pragma unroll
-            for (int j = 0; j < NB; ++j) {
-              S[i][j] += fac * (-w_minus * kme * Ae[j] * pe[i] - w_minus * kme * pe[j] * Ae[i] + pen * pe[j] * pe[i]);
-              EN[i][j] += fac * (-w_plus * knb * An[j] * pe[i] + w_minus * kme * pn[j] * Ae[i] - pen * pn[j] * pe[i]);
-            }
-        }
-        int slot[NB];
-#pragma unroll
-        for (int r = 0; r < NB; ++r) slot[r] = role_slot<E>(o.finfo, f, r);
-#pragma unroll
-        for (int i = 0; i < NB; ++i)
-#pragma unroll
-          for (int r = 0; r < NB; ++r) img[i * rowlen + pos[f] * NB + slot[r]] = EN[i][r];
-      } else {   // Dirichlet: SWIPDG::BoundaryLHS
-#pragma unroll
-        for (int q = 0; q < NQF; ++q) {
-          const double s = Gauss01<NQF>::s(q);
-          double pe[NB], ghx[NB], ghy[NB], gex[NB], gey[NB];
-          E::shape(rax + s * (rbx - rax), ray + s * (rby - ray), pe, ghx, ghy);
-#pragma unroll
-          for (int k = 0; k < NB; ++k) G.grad(ghx[k], ghy[k], gex[k], gey[k]);
-          double kme = o.ke;
-          if constexpr (KK == HDD_FN_SINUSOID) kme = kap(a, Ax + s * tx, Ay + s * ty);
-          const double pen = (a.sigma_boundary * kme * dm) * ihp;
-          const double fac = Gauss01<NQF>::w(q) * len;
-          double Ae[NB];
-#pragma unroll
-          for (int k = 0; k < NB; ++k) Ae[k] = agn(o.A, gex[k], gey[k], nx, ny);
-#pragma unroll
-          for (int i = 0; i < NB; ++i)
-#pragma unroll
-            for (int j = 0; j < NB; ++j)
-              S[i][j] += fac * (-kme * Ae[j] * pe[i] - kme * pe[j] * Ae[i] + pen * pe[j] * pe[i]);
-        }
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < NB; ++i)
-#pragma unroll
-      for (int j = 0; j < NB; ++j) img[i * rowlen + pos_self * NB + j] = S[i][j];
-  }
-};
-
-// ------------------------------------------------------------------------------------------------
-// Q1 on parallelograms, piecewise-constant coefficients: closed-form face integrals.
-//
-// On an affine quadrilateral the trace of a Q1 function on a face is linear in the face parameter s and
-// so is (A grad phi) . n, so every face integrand of SWIPDG::Inner / BoundaryLHS is a quadratic in s: the
-// reference's 2-point Gauss rule integrates it exactly, and so does the closed form used here,
-//   int (A grad phi_j . n) phi_i = |F| (p_i alpha_j + q_i beta_j),  int phi_i phi_j = |F| M_ij,
-// with alpha_j / beta_j the values at the face's first / second vertex, (p, q) = (1/3, 1/6) for the first
-// face vertex and (1/6, 1/3) for the second, M = [[1/3, 1/6], [1/6, 1/3]] on the face vertices.  The
-// vertex values are ghat_j(v) . m with m = J^{-1} A n (one 2-vector per face and side) and the reference
-// gradients ghat_j(v) compile-time constants in {0, +-1}.  The volume term keeps the reference's 1-point
-// rule (integrand order 0 for piecewise-constant data): S_ij = |det J| kappa ghat_i(c)^T J^{-1} A J^{-T}
-// ghat_j(c).  Results equal the quadrature form up to rounding (GPU parity tolerance 1e-12 of the row
-// maximum).  Neighbour quantities are in role coordinates (A = my face vertex a, B = b, C = the
-// neighbour vertex next to A), as in GenericPolicy.
-// ------------------------------------------------------------------------------------------------
-template <int TK, int KK, bool PEN = false, bool VX = false>   // PEN: penalty terms only (the SWIPDG penalty product)
-struct Q1PwcPolicy : GenericPolicy<Cube, 1, 2, TK, KK, VX> {
-  using Base = GenericPolicy<Cube, 1, 2, TK, KK, VX>;
-  using E = Cube;
-  static constexpr int NB = 4, NF = 4;
-  using Own = typename Base::Own;
-  using Gat = typename Base::Gat;
-
-  // reference Q1 gradient of basis k at the reference point (x, y): component d
-  __host__ __device__ static constexpr double gh(int k, int d, double x, double y)
-  {
-    return d == 0 ? ((k & 1) ? 1.0 : -1.0) * ((k & 2) ? y : 1.0 - y)
-                  : ((k & 2) ? 1.0 : -1.0) * ((k & 1) ? x : 1.0 - x);
-  }
-
-  template <class IMG>
-  __device__ static void compute(const AssembleArgs& a, int64_t e, const Own& o, const Gat& gt, IMG img)
-  {
-    const double j00 = o.X[1] - o.X[0], j01 = o.X[2] - o.X[0], j10 = o.Y[1] - o.Y[0], j11 = o.Y[2] - o.Y[0];
-    const double det = j00 * j11 - j01 * j10;
-    const double id = rcp_nr(det);
-    const double i00 = j11 * id, i01 = -j01 * id, i10 = -j10 * id, i11 = j00 * id;   // J^{-1}
-    const double adet = fabs(det);
-    const double osgn = det > 0.0 ? 1.0 : -1.0;
-    int pos_self = 0, pos[NF];
-#pragma unroll
-    for (int f = 0; f < NF; ++f) pos_self += (o.nbr[f] >= 0 && o.nbr[f] < e);
-#pragma unroll
-    for (int f = 0; f < NF; ++f) {
-      int p = (e < o.nbr[f]) ? 1 : 0;
-#pragma unroll
-      for (int q = 0; q < NF; ++q) p += (o.nbr[q] >= 0 && o.nbr[q] < o.nbr[f]);
-      pos[f] = p;
-    }
-    const int rowlen = (Base::n_interior(o) + 1) * NB;
-    const Tensor A = o.A;
-    const double ke = o.ke;
-    double S[NB][NB];
-    {   // LocalEvaluation::Elliptic, 1-point rule: K = J^{-1} A J^{-T}
-      const double p00 = i00 * A.a00 + i01 * A.a01, p01 = i00 * A.a01 + i01 * A.a11;
-      const double p10 = i10 * A.a00 + i11 * A.a01, p11 = i10 * A.a01 + i11 * A.a11;
-      const double k00 = p00 * i00 + p01 * i01, k01 = p00 * i10 + p01 * i11, k11 = p10 * i10 + p11 * i11;
-      const double fac = PEN ? 0.0 : adet * ke;
-#pragma unroll
-      for (int i = 0; i < NB; ++i)
-#pragma unroll
-        for (int j = 0; j < NB; ++j) {
-          const double gix = gh(i, 0, 0.5, 0.5), giy = gh(i, 1, 0.5, 0.5);
-          const double gjx = gh(j, 0, 0.5, 0.5), gjy = gh(j, 1, 0.5, 0.5);
-          S[i][j] = fac * (gix * (k00 * gjx + k01 * gjy) + giy * (k01 * gjx + k11 * gjy));
-        }
-    }
-#pragma unroll
-    for (int f = 0; f < NF; ++f) {
-      const int32_t n = o.nbr[f];
-      if (n <= HDD_NBR_NEUMANN) continue;
-      const int fa = E::fv(f, 0), fb = E::fv(f, 1);
-      const double ax = E::rv(fa, 0), ay = E::rv(fa, 1), bx = E::rv(fb, 0), by = E::rv(fb, 1);
-      const double Ax = o.X[fa], Ay = o.Y[fa], Bx = o.X[fb], By = o.Y[fb];
-      const double tx = Bx - Ax, ty = By - Ay;
-      const double il = rsq_nr(tx * tx + ty * ty);
-      const double len = (tx * tx + ty * ty) * il;
-      const double nsc = E::face_sign(f) * osgn * il;
-      const double nx = ty * nsc, ny = -tx * nsc;
-      const double anx = A.a00 * nx + A.a01 * ny, any = A.a01 * nx + A.a11 * ny;
-      const double dm = anx * nx + any * ny;
-      const double ihp = a.beta == 1.0 ? il : inv_pow(len, a.beta);
-      const double mx = i00 * anx + i01 * any, my = i10 * anx + i11 * any;   // J^{-1} A n
-      double al[NB], be[NB];   // (A grad phi_k . n) at my face vertices a, b
-#pragma unroll
-      for (int k = 0; k < NB; ++k) {
-        al[k] = gh(k, 0, ax, ay) * mx + gh(k, 1, ax, ay) * my;
-        be[k] = gh(k, 0, bx, by) * mx + gh(k, 1, bx, by) * my;
-      }
-      const double L3 = len * (1.0 / 3.0), L6 = len * (1.0 / 6.0);
-      // int (A grad phi_j . n) phi_i  and  int phi_i phi_j
-      auto I1 = [&](int j, int i) { return i == fa ? L3 * al[j] + L6 * be[j] : (i == fb ? L6 * al[j] + L3 * be[j] : 0.0); };
-      auto MM = [&](int i, int j) {
-        return (i == fa || i == fb) && (j == fa || j == fb) ? (i == j ? L3 : L6) : 0.0;
-      };
-      if (n >= 0) {
-        const double Cx = gt.Cx[f], Cy = gt.Cy[f];
-        const Tensor Ap = gt.Ap[f];
-        const double kn = gt.kn[f];
-        // neighbour in role coordinates: A = (0,0), B = (1,0), C = (0,1)
-        const double h00 = Bx - Ax, h01 = Cx - Ax, h10 = By - Ay, h11 = Cy - Ay;
-        const double hid = rcp_nr(h00 * h11 - h01 * h10);
-        const double anpx = Ap.a00 * nx + Ap.a01 * ny, anpy = Ap.a01 * nx + Ap.a11 * ny;
-        const double dp = anpx * nx + anpy * ny;
-        const double mpx = (h11 * anpx - h01 * anpy) * hid, mpy = (-h10 * anpx + h00 * anpy) * hid;
-        double alp[NB], bep[NB];   // (A+ grad phi+_r . n) at A (0,0) and B (1,0)
-#pragma unroll
-        for (int r = 0; r < NB; ++r) {
-          alp[r] = gh(r, 0, 0.0, 0.0) * mpx + gh(r, 1, 0.0, 0.0) * mpy;
-          bep[r] = gh(r, 0, 1.0, 0.0) * mpx + gh(r, 1, 1.0, 0.0) * mpy;
-        }
-        const double rs = rcp_nr(dp + dm);
-        const double gamma = (dp * dm) * rs;
-        const double w_plus = dm * rs, w_minus = dp * rs;
-        const double pen = (ke * kn * a.sigma_inner * gamma) * ihp;
-        constexpr double CS = PEN ? 0.0 : 1.0;
-        const double cs = -w_minus * ke * CS, cp = -w_plus * kn * CS, cm = w_minus * ke * CS;
-#pragma unroll
-        for (int i = 0; i < NB; ++i)
-#pragma unroll
-          for (int j = 0; j < NB; ++j) S[i][j] += cs * (I1(j, i) + I1(i, j)) + pen * MM(i, j);
-        int slot[NB];
-#pragma unroll
-        for (int r = 0; r < NB; ++r) slot[r] = role_slot<E>(o.finfo, f, r);
-#pragma unroll
-        for (int i = 0; i < NB; ++i) {
-          // int phi+_r phi_i: phi+_A = 1 - s, phi+_B = s (roles 0, 1); int phi+_r (A grad phi_i . n) likewise
-          const double pi = i == fa ? L3 : (i == fb ? L6 : 0.0), qi = i == fa ? L6 : (i == fb ? L3 : 0.0);
-#pragma unroll
-          for (int r = 0; r < NB; ++r) {
-            const double anr = pi * alp[r] + qi * bep[r];
-            const double ai = r == 0 ? L3 * al[i] + L6 * be[i] : (r == 1 ? L6 * al[i] + L3 * be[i] : 0.0);
-            const double mr = r == 0 ? pi : (r == 1 ? qi : 0.0);
-            img[i * rowlen + pos[f] * NB + slot[r]] = cp * anr + cm * ai - pen * mr;
-          }
-        }
-      } else {   // Dirichlet: SWIPDG::BoundaryLHS
-        const double pen = (a.sigma_boundary * ke * dm) * ihp;
-#pragma unroll
-        for (int i = 0; i < NB; ++i)
-#pragma unroll
-          for (int j = 0; j < NB; ++j) S[i][j] += -ke * (PEN ? 0.0 : 1.0) * (I1(j, i) + I1(i, j)) + pen * MM(i, j);
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < NB; ++i)
-#pragma unroll
-      for (int j = 0; j < NB; ++j) img[i * rowlen + pos_self * NB + j] = S[i][j];
-  }
-};
-
-// P1 simplex, piecewise-constant coefficients: the closed-form policy (p1_compute above)
-template <int TK, int KK, bool PEN = false, bool VX = false>
-struct P1PwcPolicy {
-  static constexpr int NB = 3, NF = 3;
-  static constexpr int RB = 36;
-  // store-bound.  Element-major geometry: 8 tiles per CU since the out-of-line pow (191 VGPRs, 2 waves per
-  // SIMD): C2 0.310 / 0.305 vs 0.312 / 0.314 ms at 4 (profiles/r01/s3/sweep_wgcu_s3.log).  Vertex-indexed
-  // geometry: 4 (one wave per SIMD): C2 0.230-0.237 ms vs 0.246-0.247 at 8, 0.242 at 6, 0.256 at 3
-  // (same box, profiles/r02/s2/ab_wgcu_vx*)
-  static constexpr int WGCU = VX ? 4 : 8, MINW = 1;
-  static constexpr bool PAD = false;          // store-bound: its 4-way write conflicts stay hidden
-  using Own = P1Own;
-  using Gat = P1Gat;
-  __device__ static void load_own(const AssembleArgs& a, int64_t e, Own& o) { p1_load_own<TK, KK, VX>(a, e, o); }
-  __device__ static void load_gat(const AssembleArgs& a, int64_t e, Own& o, Gat& g) { p1_load_gat<TK, KK, VX>(a, e, o, g); }
-  __device__ static void load_gat2(const AssembleArgs& a, Gat& g) { p1_load_gat2<VX>(a, g); }
-  __device__ static int n_interior(const Own& o) { return int(o.nbr[0] >= 0) + int(o.nbr[1] >= 0) + int(o.nbr[2] >= 0); }
-  __device__ static void compute(const AssembleArgs& a, int64_t e, const Own& o, const Gat& g, double* img)
-  {
-    p1_compute<PEN>(a, e, o, g, img);
-  }
-};
-
-// ------------------------------------------------------------------------------------------------
-// P1 with a smooth diffusion factor (OS2014 sinusoid, C3): kappa moments.
-//
-// P1 gradients, and hence (A grad phi) . n, are constant on an element, so every integrand is kappa (or
-// kappa^2 in the interior penalty, kappa^- kappa^+ with one smooth kappa) times a polynomial of the trace:
-//   volume   int kappa grad phi_j . A grad phi_i  = |det J| (sum_q w_q kappa(x_q)) g_i . A g_j      (Dunavant 6)
-//   face     int kappa phi_i        = |F| sum_q w_q kappa(x_q) phi_i(s_q)                         (Gauss 3)
-//            int kappa^m phi_i phi_j = |F| sum_q w_q kappa(x_q)^m phi_i(s_q) phi_j(s_q)  (m = 2 inner, 1 Dirichlet)
-// The moments use the reference's points and weights (the same rules as GenericPolicy: integrand orders
-// ord kappa + 0 / ord kappa + 2 with ord kappa = 3), so the entries equal the quadrature form up to
-// rounding, at 15 kappa evaluations and the P1 closed-form entry count per element.
-// ------------------------------------------------------------------------------------------------
-template <int TK, bool VX = false>
-struct P1SmoothPolicy {
-  static constexpr int NB = 3, NF = 3;
-  static constexpr int RB = 36;
-  // 8 tiles per CU at <= 256 registers: 0.201 ms per C3 component vs 0.231 at 4 (and 0.230 for the
-  // quadrature policy at 8; profiles/r01/s2/ab_p1s.log)
-  static constexpr int WGCU = 8, MINW = 2;
-  static constexpr bool PAD = false;
-  using Own = P1Own;
-  using Gat = P1Gat;
-  __device__ static void load_own(const AssembleArgs& a, int64_t e, Own& o) { p1_load_own<TK, HDD_FN_CONST, VX>(a, e, o); }
-  __device__ static void load_gat(const AssembleArgs& a, int64_t e, Own& o, Gat& g)
-  {
-    p1_load_gat<TK, HDD_FN_CONST, VX>(a, e, o, g);
-  }
-  __device__ static void load_gat2(const AssembleArgs& a, Gat& g) { p1_load_gat2<VX>(a, g); }
-  __device__ static int n_interior(const Own& o) { return int(o.nbr[0] >= 0) + int(o.nbr[1] >= 0) + int(o.nbr[2] >= 0); }
-
-  __device__ static void compute(const AssembleArgs& a, int64_t e, const Own& o, const Gat& gt, double* img)
-  {
-    using E = Simplex;
-    const KappaArg& K = a.kappa[0];
-    auto kap = [&](double x, double y) { return K.c + K.b * sin_phase(K.kx * x + K.ky * y); };
-    const double j00 = o.X[1] - o.X[0], j01 = o.X[2] - o.X[0], j10 = o.Y[1] - o.Y[0], j11 = o.Y[2] - o.Y[0];
-    const double det = j00 * j11 - j01 * j10;
-    const double id = rcp_nr(det);
-    const double i00 = j11 * id, i01 = -j01 * id, i10 = -j10 * id, i11 = j00 * id;
-    double g[3][2];
-    g[1][0] = i00; g[1][1] = i01;
-    g[2][0] = i10; g[2][1] = i11;
-    g[0][0] = -i00 - i10; g[0][1] = -i01 - i11;
-    double Ag[3][2];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      Ag[k][0] = o.A.a00 * g[k][0] + o.A.a01 * g[k][1];
-      Ag[k][1] = o.A.a01 * g[k][0] + o.A.a11 * g[k][1];
-    }
-    const double adet = fabs(det);
-    const double osgn = det > 0.0 ? 1.0 : -1.0;
-    int nblk = 1, pos_self = 0, pos[3];
-#pragma unroll
-    for (int f = 0; f < 3; ++f) {
-      nblk += o.nbr[f] >= 0;
-      pos_self += (o.nbr[f] >= 0 && o.nbr[f] < e);
-    }
-#pragma unroll
-    for (int f = 0; f < 3; ++f) {
-      int p = (e < o.nbr[f]) ? 1 : 0;
-#pragma unroll
-      for (int q = 0; q < 3; ++q) p += (o.nbr[q] >= 0 && o.nbr[q] < o.nbr[f]);
-      pos[f] = p;
-    }
-    const int rowlen = nblk * 3;
-    double kv = 0.0;   // sum_q w_q kappa(x_q), Dunavant 6
-#pragma unroll
-    for (int q = 0; q < 6; ++q) {
-      const double xh = VolRule<Simplex, 6>::x(q), yh = VolRule<Simplex, 6>::y(q);
-      kv += VolRule<Simplex, 6>::w(q) * kap(o.X[0] + j00 * xh + j01 * yh, o.Y[0] + j10 * xh + j11 * yh);
-    }
-    double S[3][3];
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-#pragma unroll
-      for (int j = 0; j < 3; ++j) S[i][j] = adet * kv * (Ag[j][0] * g[i][0] + Ag[j][1] * g[i][1]);
-#pragma unroll
-    for (int f = 0; f < 3; ++f) {
-      const int32_t n = o.nbr[f];
-      if (n <= HDD_NBR_NEUMANN) continue;
-      const int fa = E::fv(f, 0), fb = E::fv(f, 1), fc = 3 - fa - fb;
-      const double Ax = o.X[fa], Ay = o.Y[fa], Bx = o.X[fb], By = o.Y[fb];
-      const double tx = Bx - Ax, ty = By - Ay;
-      const double il = rsq_nr(tx * tx + ty * ty);
-      const double len = (tx * tx + ty * ty) * il;
-      const double nsc = E::face_sign(f) * osgn * il;
-      const double nx = ty * nsc, ny = -tx * nsc;
-      double Ae[3];
-#pragma unroll
-      for (int k = 0; k < 3; ++k) Ae[k] = Ag[k][0] * nx + Ag[k][1] * ny;
-      const double dm = agn(o.A, nx, ny, nx, ny);
-      const double ihp = a.beta == 1.0 ? il : inv_pow(len, a.beta);
-      const bool inner = n >= 0;
-      // moments over the face's Gauss 3 points (s from vertex a to vertex b)
-      double k1a = 0.0, k1b = 0.0, qaa = 0.0, qab = 0.0, qbb = 0.0;
-#pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        const double sq = Gauss01<3>::s(q), wq = Gauss01<3>::w(q) * len;
-        const double k = kap(Ax + sq * tx, Ay + sq * ty);
-        const double kk = inner ? k * k : k;
-        k1a += wq * k * (1.0 - sq);
-        k1b += wq * k * sq;
-        qaa += wq * kk * (1.0 - sq) * (1.0 - sq);
-        qab += wq * kk * sq * (1.0 - sq);
-        qbb += wq * kk * sq * sq;
-      }
-      auto M1 = [&](int i) { return i == fa ? k1a : (i == fb ? k1b : 0.0); };
-      auto MM = [&](int i, int j) {
-        return (i == fc || j == fc) ? 0.0 : (i != j ? qab : (i == fa ? qaa : qbb));
-      };
-      if (inner) {
-        const uint32_t inf = (o.finfo >> (4 * f)) & 15u;
-        const int tw = int(inf & 7u);
-        const bool rev = (inf & 8u) != 0u;
-        const int ta = E::fv(tw, 0), tb = E::fv(tw, 1), to = 3 - ta - tb;
-        const double Ox = gt.Ox[f], Oy = gt.Oy[f];
-        const Tensor Ap = gt.Ap[f];
-        const double dp = agn(Ap, nx, ny, nx, ny);
-        const double rs = rcp_nr(dp + dm);
-        const double gamma = (dp * dm) * rs;
-        const double w_plus = dm * rs, w_minus = dp * rs;
-        const double pc = (a.sigma_inner * gamma) * ihp;
-        const double iD = rcp_nr((Bx - Ax) * (Oy - Ay) - (By - Ay) * (Ox - Ax));
-        const double mx = Ap.a00 * nx + Ap.a01 * ny, my = Ap.a01 * nx + Ap.a11 * ny;
-        const double AnA = ((By - Oy) * mx + (Ox - Bx) * my) * iD;
-        const double AnB = ((Oy - Ay) * mx + (Ax - Ox) * my) * iD;
-        const double AnO = ((Ay - By) * mx + (Bx - Ax) * my) * iD;
-        const int jA = rev ? tb : ta, jB = rev ? ta : tb;
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-          double* row = img + i * rowlen + pos[f] * 3;
-          const double m1i = M1(i);
-          row[jA] = -w_plus * AnA * m1i + w_minus * Ae[i] * k1a - pc * MM(i, fa);
-          row[jB] = -w_plus * AnB * m1i + w_minus * Ae[i] * k1b - pc * MM(i, fb);
-          row[to] = -w_plus * AnO * m1i;
-        }
-#pragma unroll
-        for (int i = 0; i < 3; ++i)
-#pragma unroll
-          for (int j = 0; j < 3; ++j) S[i][j] += -w_minus * (Ae[j] * M1(i) + Ae[i] * M1(j)) + pc * MM(i, j);
-      } else {   // Dirichlet: SWIPDG::BoundaryLHS, penalty sigma_b kappa (n.An) / |F|^beta
-        const double pc = (a.sigma_boundary * dm) * ihp;
-#pragma unroll
-        for (int i = 0; i < 3; ++i)
-#pragma unroll
-          for (int j = 0; j < 3; ++j) S[i][j] += -(Ae[j] * M1(i) + Ae[i] * M1(j)) + pc * MM(i, j);
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-#pragma unroll
-      for (int j = 0; j < 3; ++j) img[i * rowlen + pos_self * 3 + j] = S[i][j];
-  }
-};
-
-// ------------------------------------------------------------------------------------------------
-// Element-local products on the element-diagonal (volume) pattern (swipdg.hh:358-461: L2, H1Semi,
-// Elliptic, BoundaryL2 with over_integrate = 2), P1 triangles / Q1 parallelograms, piecewise-constant
-// data.  The reference's rules (orders 2p + 2, 2(p-1) + 2 [+ ord kappa]) integrate these polynomial
-// integrands exactly, so the closed forms below equal them up to rounding:
-//   P1:  l2 |det| (1 + d_ij) / 24;  h1 / elliptic  (|det| / 2) ghat_i^T K ghat_j
-//   Q1:  l2 |det| M(i0,j0) M(i1,j1);  h1 / elliptic  sum_ab K_ab F^ab(i,j) with the 1D integrals
-//        M = int L_i L_j, D = int L_i' L_j', C = int L_i' L_j (F^00 = D x M, F^01 = C x C^T, F^10 = C^T x C,
-//        F^11 = M x D);  K = |det J| kappa J^-1 A J^-T (A = I for h1)
-//   boundary l2: sum over boundary faces of |F| (1/3, 1/6) on the face vertices.
-// Row block = nb x nb (no neighbour blocks), so tiles are 64 nb^2 doubles and no gathers are needed.
-// ------------------------------------------------------------------------------------------------
-template <class E, int KIND, int TK, int KK, int VX = 0>   // VX: vertex-indexed geometry (P1 / Q1 kernels' VX)
-struct VolProductPolicy {
-  static constexpr int NB = E::NB, NF = E::NF, NV = E::NV;
-  static constexpr int RB = NB * NB;
-  static constexpr int WGCU = 4, MINW = 1;
-  static constexpr bool PAD = false;
-  struct Own {
-    double X[NV], Y[NV];
-    int32_t nbr[NF];
-    Tensor A;
-    double ke;
-    int32_t vid[NV];
-  };
-  struct Gat {};
-  static constexpr int NVL = KIND == HDD_PRODUCT_BOUNDARY_L2 ? NV : 3;   // vertices read (0, 1, 2 span the map)
-  __device__ static void load_own(const AssembleArgs& a, int64_t e, Own& o)
-  {
-    const int64_t ne = a.n_local;
-#pragma unroll
-    for (int k = 0; k < NVL; ++k) {
-      if constexpr (VX != 0) {
-        o.vid[k] = a.ev[k * ne + e];
-      } else {
-        o.X[k] = a.coords[(2 * k) * ne + e];
-        o.Y[k] = a.coords[(2 * k + 1) * ne + e];
-      }
-    }
-    if constexpr (KIND == HDD_PRODUCT_BOUNDARY_L2) {
-#pragma unroll
-      for (int f = 0; f < NF; ++f) o.nbr[f] = a.nbrs[f * ne + e];
-    }
-    if constexpr (KIND == HDD_PRODUCT_ELLIPTIC) {
-      o.A = tensor_k<TK>(a, e);
-      o.ke = kappa_k<KK>(a, e);
-    }
-  }
-  __device__ static void load_gat(const AssembleArgs& a, int64_t, Own& o, Gat&)
-  {
-    if constexpr (VX != 0) {
-#pragma unroll
-      for (int k = 0; k < NVL; ++k) vertex_xy(a, o.vid[k], o.X[k], o.Y[k]);
-    }
-  }
-  __device__ static void load_gat2(const AssembleArgs&, Gat&) {}
-  __device__ static int n_interior(const Own&) { return 0; }
-
-  __host__ __device__ static constexpr double m1(int i, int j) { return i == j ? 1.0 / 3.0 : 1.0 / 6.0; }
-  __host__ __device__ static constexpr double d1(int i, int j) { return i == j ? 1.0 : -1.0; }
-  __host__ __device__ static constexpr double c1(int i, int) { return i ? 0.5 : -0.5; }   // int L_i' L_j
-
-  __device__ static void compute(const AssembleArgs&, int64_t, const Own& o, const Gat&, double* img)
-  {
-    const double j00 = o.X[1] - o.X[0], j01 = o.X[2] - o.X[0], j10 = o.Y[1] - o.Y[0], j11 = o.Y[2] - o.Y[0];
-    const double det = j00 * j11 - j01 * j10;
-    const double adet = fabs(det);
-    double S[NB][NB];
-    if constexpr (KIND == HDD_PRODUCT_L2) {
-#pragma unroll
-      for (int i = 0; i < NB; ++i)
-#pragma unroll
-        for (int j = 0; j < NB; ++j)
-          S[i][j] = std::is_same<E, Simplex>::value ? adet * (i == j ? 1.0 / 12.0 : 1.0 / 24.0)
-                                                     : adet * (m1(i & 1, j & 1) * m1(i >> 1, j >> 1));
-    } else if constexpr (KIND == HDD_PRODUCT_BOUNDARY_L2) {
-#pragma unroll
-      for (int i = 0; i < NB; ++i)
-#pragma unroll
-        for (int j = 0; j < NB; ++j) S[i][j] = 0.0;
-#pragma unroll
-      for (int f = 0; f < NF; ++f) {
-        if (o.nbr[f] >= 0) continue;
-        const int fa = E::fv(f, 0), fb = E::fv(f, 1);
-        const double tx = o.X[fb] - o.X[fa], ty = o.Y[fb] - o.Y[fa];
-        const double len = sqrt(tx * tx + ty * ty);
-        S[fa][fa] += len * (1.0 / 3.0);
-        S[fb][fb] += len * (1.0 / 3.0);
-        S[fa][fb] += len * (1.0 / 6.0);
-        S[fb][fa] += len * (1.0 / 6.0);
-      }
-    } else {   // H1_SEMI / ELLIPTIC: K = |det| kappa J^-1 A J^-T
-      const double id = rcp_nr(det);
-      const double i00 = j11 * id, i01 = -j01 * id, i10 = -j10 * id, i11 = j00 * id;
-      double a00 = 1.0, a01 = 0.0, a11 = 1.0, fac = adet;
-      if constexpr (KIND == HDD_PRODUCT_ELLIPTIC) {
-        a00 = o.A.a00; a01 = o.A.a01; a11 = o.A.a11;
-        fac *= o.ke;
-      }
-      const double p00 = i00 * a00 + i01 * a01, p01 = i00 * a01 + i01 * a11;
-      const double p10 = i10 * a00 + i11 * a01, p11 = i10 * a01 + i11 * a11;
-      const double k00 = fac * (p00 * i00 + p01 * i01), k01 = fac * (p00 * i10 + p01 * i11);
-      const double k11 = fac * (p10 * i10 + p11 * i11);
-#pragma unroll
-      for (int i = 0; i < NB; ++i)
-#pragma unroll
-        for (int j = 0; j < NB; ++j) {
-          if constexpr (std::is_same<E, Simplex>::value) {
-            const double gix = i == 1 ? 1.0 : (i == 0 ? -1.0 : 0.0), giy = i == 2 ? 1.0 : (i == 0 ? -1.0 : 0.0);
-            const double gjx = j == 1 ? 1.0 : (j == 0 ? -1.0 : 0.0), gjy = j == 2 ? 1.0 : (j == 0 ? -1.0 : 0.0);
-            S[i][j] = 0.5 * (gix * (k00 * gjx + k01 * gjy) + giy * (k01 * gjx + k11 * gjy));
-          } else {
-            const int i0 = i & 1, i1 = i >> 1, jj0 = j & 1, jj1 = j >> 1;
-            S[i][j] = k00 * d1(i0, jj0) * m1(i1, jj1) + k01 * c1(i0, jj0) * c1(jj1, i1) +
-                      k01 * c1(jj0, i0) * c1(i1, jj1) + k11 * m1(i0, jj0) * d1(i1, jj1);
-          }
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < NB; ++i)
-#pragma unroll
-      for (int j = 0; j < NB; ++j) img[i * NB + j] = S[i][j];
-  }
-};
-
-// offset of this lane's row block inside the tile: NB^2 * sum over the active lanes below of (1 + interior
-// faces) -- the pattern's elem_ptr rule -- from ballots + mbcnt instead of a per-element elem_ptr load
-template <int NB>
-__device__ __forceinline__ int tile_offset(int c, bool active)
-{
-  auto below = [](uint64_t m) {
-    return int(__builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u)));
-  };
-  int sum = below(__ballot(active));
-  sum += below(__ballot(active && (c & 1)));
-  sum += 2 * below(__ballot(active && (c & 2)));
-  sum += 4 * below(__ballot(active && (c & 4)));
-  return NB * NB * sum;
-}
-
-// ------------------------------------------------------------------------------------------------
-// Persistent, software-pipelined driver (see the P1 comment above): per wave a sequence of 64-element
-// tiles, memory order [prefetch own data t+1][compute t -> LDS][gathers t+1][stores t].
-// ------------------------------------------------------------------------------------------------
-//
-// LDS image.  Contiguous (element i at its CSR offset inside the tile, streamed with aligned 16-byte reads)
-// puts the lanes' row blocks RB doubles apart: for Q1 (RB = 80 = 160 dwords) a ds_write_b64 meets only
-// two bank pairs per 32 lanes, a 16-way conflict (80 such writes per tile).  Policies with P::PAD stage
-// *uniform* tiles (every element with all NF faces interior: tile length = nact * RB, the bulk of a mesh)
-// rotated instead: lane i's value j at lds[i RB + (j + 2 ((i >> 1) & 15)) mod RB] -- 2-way conflicts (the
-// floor for a layout that keeps value pairs 16-byte aligned), no padding, so the image is exactly 64 RB
-// doubles (40 KB for Q1: 4 tiles per CU instead of 3), and the reader fetches each 16-byte chunk of the
-// tile's CSR range with one ds_read_b128.  Other tiles use the contiguous image; for P::PAD policies their
-// tail lanes dump into the image's last row block (free: a non-uniform tile with < 64 elements holds at
-// most 63 RB - NB^2 values).
-template <class P, bool TL>   // TL: tiles come from a.tile_list (interior / halo split), else 0..n_tiles-1
-__global__ void __launch_bounds__(64, P::MINW)
-swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
-{
-  constexpr int RB = P::RB;
-  constexpr int IMG = 64 * RB;
-  constexpr int STORES = (IMG / 2 + 63) / 64;
-  extern __shared__ __attribute__((aligned(16))) double lds[];
-  const int lane = threadIdx.x;
-  const int64_t G = gridDim.x, b = blockIdx.x;
-  int64_t t, t_end, t_step;
-  if (G >= n_tiles) {
-    t = b; t_end = b + 1; t_step = 1;
-  } else {   // XCD-aware: the 8 XCDs sweep contiguous eighths of the tile range
-    const int64_t x = b & 7, w = b >> 3, gx = G >> 3;
-    t = (n_tiles * x) / 8 + w;
-    t_end = (n_tiles * (x + 1)) / 8;
-    t_step = gx;
-  }
-  if (t >= t_end) return;
-  double* scratch = P::PAD ? lds + IMG - RB : lds + IMG + 2;
-  // Loads whose values must be wave-uniform (tile ids of a tile list, the tiles' CSR bounds elem_ptr[]) are
-  // vector loads (the compiler cannot prove elem_ptr unaliased by the value stores, so no s_load); a
-  // readfirstlane right after such a load waits for it -- and, vmcnt being in order, for the previous tile's
-  // stores issued before it.  So they are issued one tile ahead as raw values and made uniform only in the
-  // next iteration, where the wait is a counted one behind the stores.
-  // Tile list (interior / halo-boundary split of a sharded assembly): position -> tile.
-  auto tile_raw = [&](int64_t pos) -> int64_t {
-    if constexpr (TL) return int64_t(a.tile_list[pos]);
-    return pos;
-  };
-  auto uni64 = [](int64_t v) -> int64_t { return __builtin_amdgcn_readfirstlane(v); };
-  auto elem_of_tile = [&](int64_t tile) {
-    const int64_t t0 = a.own_begin + tile * 64;
-    const int64_t e0 = t0 + lane;
-    return e0 < a.own_end ? e0 : t0;
-  };
-  auto bounds_raw = [&](int64_t tile, int64_t& base_r, int64_t& end_r) {
-    const int64_t t0 = a.own_begin + tile * 64;
-    const int64_t tend = t0 + 64 < a.own_end ? t0 + 64 : a.own_end;
-    base_r = a.elem_ptr[t0 - a.own_begin];
-    end_r = a.elem_ptr[tend - a.own_begin];
-  };
-  int64_t tile = uni64(tile_raw(t));
-  int64_t e = elem_of_tile(tile);
-  typename P::Own own;
-  typename P::Gat gat;
-  P::load_own(a, e, own);
-  P::load_gat(a, e, own, gat);
-  P::load_gat2(a, gat);
-  int64_t base_r, tile_end_r;
-  bounds_raw(tile, base_r, tile_end_r);
-  int64_t tile_n_r = tile_raw(t + t_step < t_end ? t + t_step : t);
-  // Drain the prologue's loads before entering the loop.  The compiler's wait counts at the loop head are
-  // the minimum over the entry paths: entered straight from the prologue, the first tile's vertex rows
-  // are followed by only ~7 memory operations, so the first compute of EVERY iteration waited with
-  // vmcnt(7) -- i.e. for all but the last two of the previous tile's 20 stores.  With nothing outstanding
-  // on entry only the back edge counts, and that wait skips the stores (in-order vmcnt).
-  __builtin_amdgcn_s_waitcnt(0);
-  double* out = a.vals[0];
-  for (;;) {
-    const bool has_next = t + t_step < t_end;
-    const int64_t tn = has_next ? t + t_step : t;
-    const int64_t tile_n = uni64(tile_n_r);   // loaded one iteration ago
-    const int64_t en = elem_of_tile(tile_n);
-    typename P::Own own_n;
-    P::load_own(a, en, own_n);
-    int64_t base_n_r, tile_end_n_r;
-    bounds_raw(tile_n, base_n_r, tile_end_n_r);
-    const int64_t tile_nn_r = tile_raw(tn + t_step < t_end ? tn + t_step : tn);
-    const int64_t base = uni64(base_r), tile_end = uni64(tile_end_r);   // loaded one iteration ago
-
-    const int64_t t0 = a.own_begin + tile * 64;
-    const bool active = t0 + lane < a.own_end;
-    const int64_t base_al = base & ~int64_t(1);
-    const int off = tile_offset<P::NB>(P::n_interior(own), active) + int(base - base_al);
-    const int tlen = int(tile_end - base);
-    const bool uni = P::PAD && tlen == RB * int(a.own_end - t0 < 64 ? a.own_end - t0 : 64);   // wave-uniform
-    if constexpr (P::PAD) {
-      const RotImg<RB> img{uni ? lds + lane * RB : (active ? lds + off : scratch), uni ? 2 * ((lane >> 1) & 15) : 0};
-      if (!HDD_ABL(a, 1)) P::compute(a, e, own, gat, img);
-    } else {
-      double* img = active ? lds + off : scratch;
-      if (!HDD_ABL(a, 1)) P::compute(a, e, own, gat, img);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-
-    typename P::Gat gat_n;
-    if (!HDD_ABL(a, 4)) P::load_gat(a, en, own_n, gat_n);
-
-    const int64_t start = (base + 1) & ~int64_t(1);
-    const int64_t stop = tile_end & ~int64_t(1);
-    const int nbytes = stop > start && !HDD_ABL(a, 2) ? int(stop - start) * 8 : 0;
-    __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(out + start, (short)0, nbytes, 0x00020000);
-    if (P::PAD && uni) {
-      auto at = [](int d) {   // rotated slot of the tile's CSR value d
-        const int l = d / RB, j = d - l * RB;
-        const int q = j + 2 * ((l >> 1) & 15);
-        return l * RB + (q < RB ? q : q - RB);
-      };
-      const double head = lds[at(0)];
-      const double tail = lds[at(tlen - 1)];
-      out[base] = head;
-      out[tile_end - 1] = tail;
-      const int d0 = int(start - base), dmax = tlen - 2;
-      if (d0 == 0) {   // element blocks start on even d: every 16-byte chunk is one aligned LDS pair
-#pragma unroll
-        for (int k = 0; k < STORES; ++k) {
-          const int d = 2 * (lane + 64 * k);
-          const dvec2 v = *reinterpret_cast<const dvec2*>(lds + at(d <= dmax ? d : 0));
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ivec4, v), rsrc, d * 8, 0, 2);
-        }
-      } else {
-#pragma unroll
-        for (int k = 0; k < STORES; ++k) {
-          const int m2 = 2 * (lane + 64 * k);
-          const int d = m2 + 1 <= dmax ? m2 + 1 : 0;
-          dvec2 v;
-          v.x = lds[at(d)];
-          v.y = lds[at(d + 1)];
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ivec4, v), rsrc, m2 * 8, 0, 2);
-        }
-      }
-    } else {
-      const double head = lds[base - base_al];
-      const double tail = lds[tile_end - 1 - base_al];
-      out[base] = head;
-      out[tile_end - 1] = tail;
-      const double* src = lds + (start - base_al);
-#pragma unroll
-      for (int k = 0; k < STORES; ++k) {
-        const int idx = 2 * (lane + 64 * k);
-        const int li = idx < IMG ? idx : 0;
-        const dvec2 v = *reinterpret_cast<const dvec2*>(src + li);
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ivec4, v), rsrc, idx * 8, 0, 2);
-      }
-    }
-    // second gather stage of tile t+1 (vertex-indexed geometry: the neighbours' off-face vertices by the
-    // ids the first stage brought): its wait covers the first stage only, which was issued before the
-    // stores of tile t (vmcnt is in order), so it never waits for those stores
-    if (!HDD_ABL(a, 4)) P::load_gat2(a, gat_n);   // (ablation 4: no stage-1 ids to follow)
-    if (!has_next) break;
-    t = tn;
-    tile = tile_n;
-    tile_n_r = tile_nn_r;
-    e = en;
-    own = own_n;
-    gat = gat_n;
-    base_r = base_n_r;
-    tile_end_r = tile_end_n_r;
-  }
-}
-
-// ------------------------------------------------------------------------------------------------
-// host-side launch
-// ------------------------------------------------------------------------------------------------
-template <class E, int NQV, int NQF, bool PWC>
-static hipError_t launch_t(const AssembleArgs& a, hipStream_t s)
-{
-  const int64_t n_own = a.own_end - a.own_begin;
-  if (n_own <= 0) return hipSuccess;
-  const int64_t tiles = (n_own + 63) / 64;
-  // tile image (64 elements x full row blocks) + 1 alignment slot + a scratch row for tail lanes
-  const size_t lds = (size_t(64) * E::NB * (E::NF + 1) * E::NB + 2 + (E::NF + 1) * E::NB) * sizeof(double);
-  for (int c = 0; c < a.n_comp; ++c) {
-    AssembleArgs ac = a;
-    ac.n_comp = 1;
-    ac.kappa[0] = a.kappa[c];
-    ac.vals[0] = a.vals[c];
-    hipLaunchKernelGGL((swipdg_assemble_kernel<E, NQV, NQF, PWC>), dim3(unsigned(tiles)), dim3(64 * E::NB), lds, s, ac);
-    const hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-  }
-  return hipSuccess;
-}
-
-template <class P>
-static hipError_t launch_persistent(const AssembleArgs& a, hipStream_t s)
-{
-  const int64_t n_own = a.own_end - a.own_begin;
-  if (n_own <= 0) return hipSuccess;
-  const int64_t tiles = a.tile_list ? a.n_tile_list : (n_own + 63) / 64;
-  if (tiles <= 0) return hipSuccess;
-  const size_t lds = (P::PAD ? size_t(64) * P::RB : size_t(64) * P::RB + 2 + P::RB) * sizeof(double);
-  const int cus = a.n_cu;
-  // tiles per CU measured per policy (profiles/r01/sweep_wg_per_cu.log, profiles/r01/s2/); a.wgcu > 0 is the
-  // HDD_P1_WGCU sweep override, read once per context
-  int wgcu = a.wgcu > 0 ? a.wgcu : P::WGCU;
-  wgcu = std::max(1, std::min<int>(wgcu, int((160 * 1024) / lds)));   // resident by LDS (Q1 tiles: 3 per CU)
-  const int64_t G = std::min<int64_t>(tiles, int64_t(cus) * wgcu);
-  for (int c = 0; c < a.n_comp; ++c) {
-    AssembleArgs ac = a;
-    ac.n_comp = 1;
-    ac.kappa[0] = a.kappa[c];
-    ac.vals[0] = a.vals[c];
-    if (a.tile_list)
-      hipLaunchKernelGGL((swipdg_persistent_kernel<P, true>), dim3(unsigned(G)), dim3(64), lds, s, ac, tiles);
-    else
-      hipLaunchKernelGGL((swipdg_persistent_kernel<P, false>), dim3(unsigned(G)), dim3(64), lds, s, ac, tiles);
-    const hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-  }
-  return hipSuccess;
-}
-
-// instantiate a policy for the runtime (tensor kind, piecewise-constant kappa kind) pair
-template <template <int, int> class PT>
-static hipError_t dispatch_pwc(const AssembleArgs& a, hipStream_t s)
-{
-  const int tk = a.tkind;
-  const bool pe = a.kappa[0].kind == HDD_FN_PER_ELEM;
-  if (tk == HDD_TENSOR_CONST)
-    return pe ? launch_persistent<PT<HDD_TENSOR_CONST, HDD_FN_PER_ELEM>>(a, s) : launch_persistent<PT<HDD_TENSOR_CONST, HDD_FN_CONST>>(a, s);
-  if (tk == HDD_TENSOR_ISO_PER_ELEM)
-    return pe ? launch_persistent<PT<HDD_TENSOR_ISO_PER_ELEM, HDD_FN_PER_ELEM>>(a, s) : launch_persistent<PT<HDD_TENSOR_ISO_PER_ELEM, HDD_FN_CONST>>(a, s);
-  return pe ? launch_persistent<PT<HDD_TENSOR_SYM_PER_ELEM, HDD_FN_PER_ELEM>>(a, s) : launch_persistent<PT<HDD_TENSOR_SYM_PER_ELEM, HDD_FN_CONST>>(a, s);
-}
-
-// instantiate a policy for the runtime (tensor kind, kappa kind) pair; VX: vertex-indexed geometry
-template <template <int, int, bool> class PT, bool VX>
-static hipError_t dispatch_kinds_vx(const AssembleArgs& a, hipStream_t s, bool smooth)
-{
-  const int tk = a.tkind, kk = a.kappa[0].kind;
-  if (smooth) {
-    if (tk == HDD_TENSOR_CONST) return launch_persistent<PT<HDD_TENSOR_CONST, HDD_FN_SINUSOID, VX>>(a, s);
-    if (tk == HDD_TENSOR_ISO_PER_ELEM) return launch_persistent<PT<HDD_TENSOR_ISO_PER_ELEM, HDD_FN_SINUSOID, VX>>(a, s);
-    return launch_persistent<PT<HDD_TENSOR_SYM_PER_ELEM, HDD_FN_SINUSOID, VX>>(a, s);
-  }
-  const bool pe = kk == HDD_FN_PER_ELEM;
-  if (tk == HDD_TENSOR_CONST)
-    return pe ? launch_persistent<PT<HDD_TENSOR_CONST, HDD_FN_PER_ELEM, VX>>(a, s)
-              : launch_persistent<PT<HDD_TENSOR_CONST, HDD_FN_CONST, VX>>(a, s);
-  if (tk == HDD_TENSOR_ISO_PER_ELEM)
-    return pe ? launch_persistent<PT<HDD_TENSOR_ISO_PER_ELEM, HDD_FN_PER_ELEM, VX>>(a, s)
-              : launch_persistent<PT<HDD_TENSOR_ISO_PER_ELEM, HDD_FN_CONST, VX>>(a, s);
-  return pe ? launch_persistent<PT<HDD_TENSOR_SYM_PER_ELEM, HDD_FN_PER_ELEM, VX>>(a, s)
-            : launch_persistent<PT<HDD_TENSOR_SYM_PER_ELEM, HDD_FN_CONST, VX>>(a, s);
-}
-// Vertex-indexed geometry pays on triangles (C2 0.323 -> 0.245 ms, same box: 2 waves per SIMD hide the
-// second gather stage); the Q1 tiles run one wave per SIMD (40 KB image), where that stage's latency is
-// exposed (C4 0.600 -> 0.690 ms), so quads keep the element-major coords.
-template <template <int, int, bool> class PT>
-static hipError_t dispatch_kinds(const AssembleArgs& a, hipStream_t s, bool smooth)
-{
-  return a.ev && a.elem_type == HDD_SIMPLEX ? dispatch_kinds_vx<PT, true>(a, s, smooth)
-                                            : dispatch_kinds_vx<PT, false>(a, s, smooth);
-}
-
-template <int TK, int KK, bool VX> using P1Pwc = P1PwcPolicy<TK, KK, false, VX>;
-template <int TK, int KK, bool VX> using Q1Pwc = Q1PwcPolicy<TK, KK, false, VX>;
-template <int TK, int KK, bool VX> using Q1Smooth3 = GenericPolicy<Cube, 4, 3, TK, KK, VX>;
-template <int TK, int KK, bool VX> using P1Smooth3 = GenericPolicy<Simplex, 6, 3, TK, KK, VX>;
-
-static hipError_t dispatch_smooth_p1(const AssembleArgs& a, hipStream_t s)
-{
-  if (a.debug_flags & 256) return dispatch_kinds<P1Smooth3>(a, s, true);   // A/B: the quadrature policy
-  const int tk = a.tkind;
-  if (a.ev) {
-    if (tk == HDD_TENSOR_CONST) return launch_persistent<P1SmoothPolicy<HDD_TENSOR_CONST, true>>(a, s);
-    if (tk == HDD_TENSOR_ISO_PER_ELEM) return launch_persistent<P1SmoothPolicy<HDD_TENSOR_ISO_PER_ELEM, true>>(a, s);
-    return launch_persistent<P1SmoothPolicy<HDD_TENSOR_SYM_PER_ELEM, true>>(a, s);
-  }
-  if (tk == HDD_TENSOR_CONST) return launch_persistent<P1SmoothPolicy<HDD_TENSOR_CONST>>(a, s);
-  if (tk == HDD_TENSOR_ISO_PER_ELEM) return launch_persistent<P1SmoothPolicy<HDD_TENSOR_ISO_PER_ELEM>>(a, s);
-  return launch_persistent<P1SmoothPolicy<HDD_TENSOR_SYM_PER_ELEM>>(a, s);
-}
 
 // one launch per component: components of one call may differ in kind (affine part const, component
 // per-element, ...) -- the kinds are compile-time inside the kernels
@@ -1892,12 +14,12 @@ static hipError_t launch_components(const AssembleArgs& a, int nqv, int nqf, hip
     ac.n_comp = 1;
     ac.kappa[0] = a.kappa[c];
     ac.vals[0] = a.vals[c];
-    const bool smooth = ac.kappa[0].kind == HDD_FN_SINUSOID;
+    const bool smooth = smooth_kind(ac.kappa[0].kind);
     hipError_t e = hipSuccess;
-    if (ac.elem_type == HDD_SIMPLEX && nqv == 1 && nqf == 2 && !smooth) e = dispatch_kinds<P1Pwc>(ac, s, false);
-    else if (ac.elem_type == HDD_SIMPLEX && nqv == 6 && nqf == 3 && smooth) e = dispatch_smooth_p1(ac, s);
-    else if (ac.elem_type == HDD_CUBE && nqv == 1 && nqf == 2 && !smooth) e = dispatch_kinds<Q1Pwc>(ac, s, false);
-    else if (ac.elem_type == HDD_CUBE && nqv == 4 && nqf == 3 && smooth) e = dispatch_kinds<Q1Smooth3>(ac, s, true);
+    if (ac.elem_type == HDD_SIMPLEX && nqv == 1 && nqf == 2 && !smooth) e = launch_p1_pwc(ac, s);
+    else if (ac.elem_type == HDD_SIMPLEX && nqv == 6 && nqf == 3 && smooth) e = launch_p1_smooth(ac, s);
+    else if (ac.elem_type == HDD_CUBE && nqv == 1 && nqf == 2 && !smooth) e = launch_q1_pwc(ac, s);
+    else if (ac.elem_type == HDD_CUBE && nqv == 4 && nqf == 3 && smooth) e = launch_q1_smooth(ac, s);
     else {
       *supported = false;
       return hipSuccess;
@@ -1911,36 +33,6 @@ static hipError_t launch_components(const AssembleArgs& a, int nqv, int nqf, hip
 // products (hdd_product_assemble) on the persistent driver: P1 / Q1 with piecewise-constant kappa; the
 // caller falls back to the generic product kernel (rhs.hip) for smooth kappa and hexahedra
 // ------------------------------------------------------------------------------------------------
-template <class E, int KIND, int VX>
-static hipError_t launch_vol_product_vx(const AssembleArgs& a, hipStream_t s)
-{
-  if constexpr (KIND != HDD_PRODUCT_ELLIPTIC) {
-    return launch_persistent<VolProductPolicy<E, KIND, HDD_TENSOR_CONST, HDD_FN_CONST, VX>>(a, s);
-  } else {
-    const bool pe = a.kappa[0].kind == HDD_FN_PER_ELEM;
-    if (a.tkind == HDD_TENSOR_CONST)
-      return pe ? launch_persistent<VolProductPolicy<E, KIND, HDD_TENSOR_CONST, HDD_FN_PER_ELEM, VX>>(a, s)
-                : launch_persistent<VolProductPolicy<E, KIND, HDD_TENSOR_CONST, HDD_FN_CONST, VX>>(a, s);
-    if (a.tkind == HDD_TENSOR_ISO_PER_ELEM)
-      return pe ? launch_persistent<VolProductPolicy<E, KIND, HDD_TENSOR_ISO_PER_ELEM, HDD_FN_PER_ELEM, VX>>(a, s)
-                : launch_persistent<VolProductPolicy<E, KIND, HDD_TENSOR_ISO_PER_ELEM, HDD_FN_CONST, VX>>(a, s);
-    return pe ? launch_persistent<VolProductPolicy<E, KIND, HDD_TENSOR_SYM_PER_ELEM, HDD_FN_PER_ELEM, VX>>(a, s)
-              : launch_persistent<VolProductPolicy<E, KIND, HDD_TENSOR_SYM_PER_ELEM, HDD_FN_CONST, VX>>(a, s);
-  }
-}
-
-template <class E, int KIND>
-static hipError_t launch_vol_product(const AssembleArgs& a, hipStream_t s)
-{
-  if constexpr (std::is_same_v<E, Simplex>)
-    if (a.ev) return launch_vol_product_vx<E, KIND, 1>(a, s);
-  return launch_vol_product_vx<E, KIND, 0>(a, s);
-}
-
-template <int TK, int KK> using P1Pen = P1PwcPolicy<TK, KK, true>;
-template <int TK, int KK> using P1PenVX = P1PwcPolicy<TK, KK, true, 1>;
-template <int TK, int KK> using Q1Pen = Q1PwcPolicy<TK, KK, true>;
-
 hipError_t launch_product_fast(const AssembleArgs& a, int product, hipStream_t s, bool* supported)
 {
   *supported = true;
@@ -1951,23 +43,8 @@ hipError_t launch_product_fast(const AssembleArgs& a, int product, hipStream_t s
     *supported = false;
     return hipSuccess;
   }
-  const bool tri = a.elem_type == HDD_SIMPLEX;
-  switch (product) {
-    case HDD_PRODUCT_L2:
-      return tri ? launch_vol_product<Simplex, HDD_PRODUCT_L2>(a, s) : launch_vol_product<Cube, HDD_PRODUCT_L2>(a, s);
-    case HDD_PRODUCT_H1_SEMI:
-      return tri ? launch_vol_product<Simplex, HDD_PRODUCT_H1_SEMI>(a, s)
-                 : launch_vol_product<Cube, HDD_PRODUCT_H1_SEMI>(a, s);
-    case HDD_PRODUCT_ELLIPTIC:
-      return tri ? launch_vol_product<Simplex, HDD_PRODUCT_ELLIPTIC>(a, s)
-                 : launch_vol_product<Cube, HDD_PRODUCT_ELLIPTIC>(a, s);
-    case HDD_PRODUCT_BOUNDARY_L2:
-      return tri ? launch_vol_product<Simplex, HDD_PRODUCT_BOUNDARY_L2>(a, s)
-                 : launch_vol_product<Cube, HDD_PRODUCT_BOUNDARY_L2>(a, s);
-    default:
-      if (tri && a.ev) return dispatch_pwc<P1PenVX>(a, s);   // vertex-indexed geometry (triangles, as the stiffness)
-      return tri ? dispatch_pwc<P1Pen>(a, s) : dispatch_pwc<Q1Pen>(a, s);
-  }
+  if (product != HDD_PRODUCT_PENALTY) return launch_vol_products(a, product, s);
+  return a.elem_type == HDD_SIMPLEX ? launch_p1_penalty(a, s) : launch_q1_penalty(a, s);
 }
 
 int volume_points(int elem_type, int order)
@@ -1995,7 +72,7 @@ hipError_t launch_assemble(const AssembleArgs& a, int nqv, int nqf, hipStream_t 
     return hipSuccess;
   }
   bool pwc = true;
-  for (int c = 0; c < a.n_comp; ++c) pwc &= a.kappa[c].kind != HDD_FN_SINUSOID;
+  for (int c = 0; c < a.n_comp; ++c) pwc &= !smooth_kind(a.kappa[c].kind);
   if (a.elem_type == HDD_SIMPLEX) {
     if (nqv == 1 && nqf == 2) return pwc ? launch_t<Simplex, 1, 2, true>(a, s) : launch_t<Simplex, 1, 2, false>(a, s);
     if (nqv == 6 && nqf == 3) return launch_t<Simplex, 6, 3, false>(a, s);

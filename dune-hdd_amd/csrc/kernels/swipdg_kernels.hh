@@ -13,7 +13,11 @@ struct KappaArg {
   int32_t kind, order;
   double c, b, kx, ky;
   const double* per_elem;
+  const double* table;   // HDD_FN_FLATTOP boxes [n_table][HDD_FLATTOP_REC] (flattop.hh)
+  int32_t n_table, pad;
 };
+// smooth (evaluated at quadrature points) diffusion-factor kinds
+__host__ __device__ constexpr bool smooth_kind(int k) { return k == HDD_FN_SINUSOID || k == HDD_FN_FLATTOP; }
 
 struct AssembleArgs {
   int32_t elem_type, n_comp;

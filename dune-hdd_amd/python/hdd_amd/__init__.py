@@ -17,7 +17,8 @@ HEADER = os.path.abspath(os.path.join(ROOT, "..", "include", "hdd.h"))
 
 SIMPLEX, CUBE, HEX = 0, 1, 2
 NBR_DIRICHLET, NBR_NEUMANN = -1, -2
-FN_CONST, FN_PER_ELEM, FN_SINUSOID, FN_COS_PRODUCT = 0, 1, 2, 3
+FN_CONST, FN_PER_ELEM, FN_SINUSOID, FN_COS_PRODUCT, FN_FLATTOP = 0, 1, 2, 3, 4
+FLATTOP_REC = 7   # lx, ly, ux, uy, layer_x, layer_y, value
 PRODUCT_L2, PRODUCT_H1_SEMI, PRODUCT_ELLIPTIC, PRODUCT_BOUNDARY_L2, PRODUCT_PENALTY = 0, 1, 2, 3, 4
 TENSOR_CONST, TENSOR_ISO_PER_ELEM, TENSOR_SYM_PER_ELEM = 0, 1, 2
 BOUNDARY_ALL_DIRICHLET, BOUNDARY_ALL_NEUMANN = 0, 1
@@ -74,7 +75,8 @@ class MeshT(C.Structure):
 
 class ScalarFn(C.Structure):
     _fields_ = [("kind", C.c_int32), ("order", C.c_int32), ("c", C.c_double), ("b", C.c_double),
-                ("kx", C.c_double), ("ky", C.c_double), ("per_elem", C.c_void_p)]
+                ("kx", C.c_double), ("ky", C.c_double), ("per_elem", C.c_void_p), ("table", C.c_void_p),
+                ("n_table", C.c_int32), ("pad1", C.c_int32)]
 
 
 class TensorFn(C.Structure):
@@ -147,6 +149,7 @@ def lib():
         "hdd_local_send_list": (_I32, [_VP, _VP, _I32, _I32, _VP]),
         "hdd_checkerboard": (_I32, [_I64, _VP, _VP, _VP, _I32, _I32, _VP, _VP]),
         "hdd_indicator": (_I32, [_I64, _VP, _I32, _VP, _VP]),
+        "hdd_indicator_sum": (_I32, [_I64, _VP, _I32, _VP, _VP]),
         "hdd_pattern_count": (_I32, [_I32, _I64, _I64, _I64, _VP, C.POINTER(_I64)]),
         "hdd_pattern_fill": (_I32, [_I32, _I64, _I64, _I64, _VP, _VP, _VP, _VP, _VP]),
         "hdd_dg_pattern_count": (_I32, [_I32, _I32, _I64, _I64, _I64, _VP, C.POINTER(_I64)]),
@@ -163,6 +166,8 @@ def lib():
         "hdd_swipdg_rhs": (_I32, [_VP, C.POINTER(MeshT), _VP, _VP, _VP, _VP, _VP, C.POINTER(Params), _VP, _VP]),
         "hdd_block_operator_map": (_I32, [_VP, _I32, _I32, _VP, _VP, _VP, _VP, _VP, C.POINTER(_I64)]),
         "hdd_gather_values": (_I32, [_VP, _VP, _VP, _I64, _VP, _VP]),
+        "hdd_block_operator_map_device": (_I32, [_VP, _VP, _I64, _I64, _I64, _I64, _VP, _VP, _VP, _VP, _VP]),
+        "hdd_block_operator_values_device": (_I32, [_VP, _VP, _I64, _I64, _I64, _I64, _VP, _VP, _I32, _VP, _VP]),
         "hdd_soa_gather": (_I32, [_VP, _VP, _VP, _I32, _I64, _VP, _I64, _VP, _VP]),
         "hdd_soa_scatter": (_I32, [_VP, _VP, _VP, _I32, _I64, _I64, _I64, _VP, _VP]),
         "hdd_rccl_get_unique_id": (_I32, [_VP]),
@@ -209,12 +214,14 @@ def declared_symbols(header=HEADER):
     return sorted(set(re.findall(r"\b(hdd_[a-z0-9_]+)\s*\(", txt)))
 
 
-def indicator(centers, boxes):
-    """dune-stuff Indicator at points centers [2][n] (hdd_indicator): boxes [k][5] = lx, ly, ux, uy, value."""
+def indicator(centers, boxes, summed=False):
+    """dune-stuff Indicator at points centers [2][n] (hdd_indicator): boxes [k][5] = lx, ly, ux, uy, value;
+    summed=True: the sum of one-box Indicators (hdd_indicator_sum, the Spe10 channel at layer 0)."""
     c = np.ascontiguousarray(centers, np.float64)
     b = np.ascontiguousarray(boxes, np.float64).reshape(-1, 5)
     out = np.empty(c.shape[1])
-    _check(lib().hdd_indicator(c.shape[1], _p(c), b.shape[0], _p(b), _p(out)), "hdd_indicator")
+    fn = lib().hdd_indicator_sum if summed else lib().hdd_indicator
+    _check(fn(c.shape[1], _p(c), b.shape[0], _p(b), _p(out)), "hdd_indicator")
     return out
 
 
@@ -418,11 +425,25 @@ class Context:
             self.h = None
 
 
-def scalar_fn(kind=FN_CONST, c=1.0, b=0.0, kx=0.0, ky=0.0, per_elem=None, order=0):
-    """A diffusion-factor component; per_elem is a device tensor (kept alive by the returned object)."""
-    f = ScalarFn(kind, order, c, b, kx, ky, None if per_elem is None else per_elem.data_ptr())
-    f._keep = per_elem
+def scalar_fn(kind=FN_CONST, c=1.0, b=0.0, kx=0.0, ky=0.0, per_elem=None, order=0, table=None):
+    """A diffusion-factor component; per_elem (PER_ELEM) and table (FLATTOP: [n][FLATTOP_REC] boxes) are device
+    tensors kept alive by the returned object."""
+    n_table = 0 if table is None else int(table.numel()) // FLATTOP_REC
+    f = ScalarFn(kind, order, c, b, kx, ky, None if per_elem is None else per_elem.data_ptr(),
+                 None if table is None else table.data_ptr(), n_table, 0)
+    f._keep = (per_elem, table)
     return f
+
+
+def flattop_fn(boxes, c=0.0, b=1.0, order=3, device="cuda"):
+    """HDD_FN_FLATTOP: c + b * sum of dune-stuff FlatTop functions (problems/spe10.hh:139-148, 213-222);
+    boxes [k][7] = lx, ly, ux, uy, layer_x, layer_y, value (layers > 0); order = the integration order the
+    function carries (Stuff's order(); assumption 3, the degree of the transitions per coordinate)."""
+    import torch
+    t = torch.as_tensor(np.ascontiguousarray(boxes, np.float64).reshape(-1, FLATTOP_REC)).to(device)
+    if t.shape[0] and not bool((t[:, 4:6] > 0).all()):
+        raise HddError("flattop_fn: boundary layers must be > 0 (layer 0 is the Indicator)")
+    return scalar_fn(FN_FLATTOP, c, b, order=order, table=t)
 
 
 def tensor_fn(kind=TENSOR_CONST, c=(1.0, 0.0, 1.0), per_elem=None, dim=2):
@@ -508,6 +529,53 @@ class DevicePattern:
         n_cols = int(local.grid.ne) * local.nb
         self.t = CsrT(row_ptr.shape[0] - 1, n_cols, self.nnz, self.row_ptr.data_ptr(), self.col.data_ptr(),
                       self.elem_ptr.data_ptr())
+
+
+def block_operator_nnz(local, nb=None):
+    """nnz of every block operator (ss, nn) of a BlockSWIPDG pattern from the mesh alone (no pattern pass):
+    nb^2 x #(element of ss, face neighbour in nn), plus nb^2 |ss| on the diagonal.  dict (ss, nn) -> nnz."""
+    nb = nb or local.nb
+    o0, o1 = local.own_begin, local.own_end
+    sd = local.subdomain
+    own_sd = sd[o0:o1].astype(np.int64)
+    n_sub = int(local.grid.n_sub)
+    cnt = np.bincount(own_sd * n_sub + own_sd, minlength=n_sub * n_sub).astype(np.int64)
+    for f in range(local.nf):
+        nbr = local.neighbors[f, o0:o1]
+        m = nbr >= 0
+        cnt += np.bincount(own_sd[m] * n_sub + sd[nbr[m]].astype(np.int64), minlength=n_sub * n_sub)
+    nz = np.nonzero(cnt)[0]
+    return {(int(k // n_sub), int(k % n_sub)): int(cnt[k]) * nb * nb for k in nz}
+
+
+def block_operator(ctx, grid, dpattern, vals, ss, nn, nnz=None, stream=None):
+    """BlockSWIPDG::get_local_operator(ss) (nn == ss) / get_coupling_operator(ss, nn) on the device
+    (hdd_block_operator_map_device + hdd_block_operator_values_device, block-swipdg.hh:625-676) from the global
+    device pattern: returns (row_ptr, col, [values per component]) device tensors in the operator's local
+    numbering.  nnz (e.g. from block_operator_nnz) keeps the call asynchronous; None synchronises once."""
+    torch = _torch()
+    dev = dpattern.row_ptr.device
+    nb = grid.nb
+    a, b = grid.subdomain_range(ss, ss + 1)
+    c, d = grid.subdomain_range(nn, nn + 1)
+    s = C.c_void_p(stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream)
+    rows = (b - a) * nb
+    orp = torch.empty(rows + 1, dtype=torch.int64, device=dev)
+    if nnz is None:
+        n = C.c_int64()
+        _check(lib().hdd_block_operator_map_device(ctx.h, C.byref(dpattern.t), a * nb, b * nb, c * nb, d * nb,
+                                                   orp.data_ptr(), None, None, C.byref(n), s), "block_operator")
+        nnz = n.value
+    ocol = torch.empty(max(nnz, 1), dtype=torch.int32, device=dev)
+    _check(lib().hdd_block_operator_map_device(ctx.h, C.byref(dpattern.t), a * nb, b * nb, c * nb, d * nb,
+                                               orp.data_ptr(), ocol.data_ptr(), None, None, s), "block_operator")
+    vals = list(vals)
+    outs = [torch.empty(max(nnz, 1), dtype=torch.float64, device=dev) for _ in vals]
+    vin = (C.c_void_p * max(1, len(vals)))(*[v.data_ptr() for v in vals])
+    vout = (C.c_void_p * max(1, len(vals)))(*[o.data_ptr() for o in outs])
+    _check(lib().hdd_block_operator_values_device(ctx.h, C.byref(dpattern.t), a * nb, b * nb, c * nb, d * nb,
+                                                  orp.data_ptr(), vin, len(vals), vout, s), "block_operator")
+    return orp, ocol[:nnz], [o[:nnz] for o in outs]
 
 
 def assemble(ctx, dmesh, dpattern, kappas, tensor, prm=None, vals=None, stream=None):

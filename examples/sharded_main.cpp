@@ -85,7 +85,7 @@ Problems::Problem spe10_parametric()
   std::vector<std::array<double, 5>> forces = {{0.95, 0.30, 1.10, 0.45, 2000.0},
                                                {3.00, 0.75, 3.15, 0.90, -1000.0},
                                                {4.25, 0.25, 4.40, 0.40, -1000.0}};
-  return Problems::Spe10Model1(perm, channel, forces, /*parametric_channel=*/true);
+  return Problems::Spe10Model1(perm, channel, forces, /*parametric_channel=*/true, /*channel_boundary_layer=*/{{0.0, 0.0}});
 }
 
 template <class T>
@@ -107,11 +107,24 @@ std::vector<double> rank_values(const D::ShardedBlockSWIPDG& sh)
   return out;
 }
 
+// diffusion-factor parts of different integration orders (affine part: the per-element Indicator channel,
+// order 0; component: a sinusoid of order 3): ShardedBlockSWIPDG makes one sharded call per order
+Problems::Problem mixed_orders()
+{
+  auto p = spe10_parametric();
+  p.diffusion_factor.components.clear();
+  p.diffusion_factor.coefficients.clear();
+  p.diffusion_factor.register_component(Problems::ScalarFunction::sinusoid(0.0, 0.5, 3.0, 2.0, 3),
+                                        Pymor::ParameterFunctional("mu", "mu", 1.0));
+  return p;
+}
+
 int run_threads(int n, const std::string& outdir)
 {
-  const auto problem = spe10_parametric();
   int fails = 0;
+  for (int pi = 0; pi < 2; ++pi)
   for (int et : {HDD_SIMPLEX, HDD_CUBE}) {
+    const auto problem = pi == 0 ? spe10_parametric() : mixed_orders();
     Dune::grid::Multiscale::Providers::Cube ms(et, {0.0, 0.0}, {5.0, 1.0}, {40 * n, 24}, {2 * n, 2});
     // the reference: single-GPU BlockSWIPDG of the whole multiscale grid
     D::BlockSWIPDG block(ms, Dune::Stuff::Common::Configuration(), problem);
@@ -119,6 +132,8 @@ int run_threads(int n, const std::string& outdir)
     const auto& G = block.system_matrix();
     const auto ga = G.affine_part(), gc = G.component(0);
     const auto& gp = block.pattern();
+    const auto& grp = gp.row_ptr();
+    const auto& gcol = gp.col();
 
     Mailbox mb;
     std::vector<std::vector<double>> vals(static_cast<size_t>(n)), rhs(static_cast<size_t>(n));
@@ -140,10 +155,10 @@ int run_threads(int n, const std::string& outdir)
           const auto c = A.component(0);
           vals[size_t(r)].insert(vals[size_t(r)].end(), c.begin(), c.end());
           rhs[size_t(r)] = sh.rhs().affine_part();
-          cols[size_t(r)] = sh.pattern().col;
+          cols[size_t(r)] = sh.pattern().col();
           first[size_t(r)] = sh.first_owned_dof();
           rows[size_t(r)] = sh.pattern().rows;
-          if (!outdir.empty()) dump(outdir + "/thread_rank" + std::to_string(r) + ".bin", vals[size_t(r)]);
+          if (!outdir.empty() && pi == 0) dump(outdir + "/thread_rank" + std::to_string(r) + ".bin", vals[size_t(r)]);
         } catch (const std::exception& e) {
           err[size_t(r)] = e.what();
         }
@@ -157,19 +172,20 @@ int run_threads(int n, const std::string& outdir)
         ++fails;
         continue;
       }
-      const int64_t r0 = first[size_t(r)], q0 = gp.row_ptr[size_t(r0)], q1 = gp.row_ptr[size_t(r0 + rows[size_t(r)])];
+      const int64_t r0 = first[size_t(r)], q0 = grp[size_t(r0)], q1 = grp[size_t(r0 + rows[size_t(r)])];
       const int64_t nnz = q1 - q0;
       if (int64_t(cols[size_t(r)].size()) != nnz) { ++mismatches; continue; }
       for (int64_t k = 0; k < nnz; ++k) {
-        mismatches += cols[size_t(r)][size_t(k)] != gp.col[size_t(q0 + k)];
+        mismatches += cols[size_t(r)][size_t(k)] != gcol[size_t(q0 + k)];
         mismatches += std::memcmp(&vals[size_t(r)][size_t(k)], &ga[size_t(q0 + k)], sizeof(double)) != 0;
         mismatches += std::memcmp(&vals[size_t(r)][size_t(nnz + k)], &gc[size_t(q0 + k)], sizeof(double)) != 0;
       }
       for (int64_t i = 0; i < rows[size_t(r)]; ++i)
         mismatches += std::memcmp(&rhs[size_t(r)][size_t(i)], &grhs[size_t(r0 + i)], sizeof(double)) != 0;
     }
-    std::printf("%s: %d thread ranks, %lld nnz, mismatches vs single-GPU BlockSWIPDG: %lld\n",
-                et == HDD_SIMPLEX ? "P1 Kuhn" : "Q1 quads", n, (long long)gp.nnz, (long long)mismatches);
+    std::printf("%s, %s: %d thread ranks, %lld nnz, mismatches vs single-GPU BlockSWIPDG: %lld\n",
+                pi == 0 ? "parametric SPE10" : "mixed-order kappa parts", et == HDD_SIMPLEX ? "P1 Kuhn" : "Q1 quads", n,
+                (long long)gp.nnz, (long long)mismatches);
     fails += mismatches != 0;
   }
   if (!fails) std::printf("sharded threads ok\n");

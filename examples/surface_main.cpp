@@ -5,6 +5,8 @@
 // Writes raw arrays to <outdir> for tests/test_gpu_surface.py to compare with the CPU oracle.
 #include <cmath>
 #include <cstdio>
+#include <cstring>
+#include <stdexcept>
 #include <fstream>
 #include <iostream>
 #include <string>
@@ -13,6 +15,9 @@
 #include "hdd_discretizations.hh"
 
 using namespace Dune::HDD::LinearElliptic;
+namespace S = Dune::Stuff;
+template <class T>
+using internal_array_t = Dune::HDD::LinearElliptic::internal::DeviceArray<T>;
 
 template <class T>
 static void dump(const std::string& path, const std::vector<T>& v)
@@ -21,8 +26,68 @@ static void dump(const std::string& path, const std::vector<T>& v)
   f.write(reinterpret_cast<const char*>(v.data()), std::streamsize(v.size() * sizeof(T)));
 }
 
+// position-weighted 64-bit checksum of a device array's bit patterns: sum_k bits[k] * (2k + 1) mod 2^64 (the
+// Python front-end computes the same on its own assembly: tests/test_gpu_surface.py::test_cpp_full_size_*)
+template <class T>
+uint64_t checksum(const internal_array_t<T>& a, int64_t n)
+{
+  uint64_t h = 0;
+  const int64_t chunk = int64_t(1) << 26;
+  std::vector<T> buf;
+  for (int64_t k0 = 0; k0 < n; k0 += chunk) {
+    const int64_t m = std::min(chunk, n - k0);
+    buf.resize(size_t(m));
+    if (hipMemcpy(buf.data(), a.get() + k0, size_t(m) * sizeof(T), hipMemcpyDeviceToHost) != hipSuccess)
+      throw std::runtime_error("checksum: D2H");
+    for (int64_t k = 0; k < m; ++k) {
+      uint64_t bits = 0;
+      std::memcpy(&bits, &buf[size_t(k)], sizeof(T));
+      h += bits * uint64_t(2 * (k0 + k) + 1);
+    }
+  }
+  return h;
+}
+
+// full-size runs of the reference-signature SWIPDG (device pattern, no host copy of it): C2 (SPE10 P1,
+// 3200 x 640 Kuhn) and ESV2007 3d Q3 on n^3 hexahedra
+int run_big(const std::string& which, int n)
+{
+  if (which == "c2") {
+    S::Grid::Providers::Cube provider(HDD_SIMPLEX, {0.0, 0.0}, {5.0, 1.0}, {3200, 640});
+    std::vector<double> perm(2000);
+    for (int i = 0; i < 2000; ++i) perm[size_t(i)] = std::pow(10.0, -3.0 + 6.0 * std::fmod(0.618033988749895 * i, 1.0));
+    Discretizations::SWIPDG sw(provider, S::Grid::BoundaryInfos::AllDirichlet::default_config(),
+                               Problems::Spe10Model1(perm, {}, {}, false), 0, {});
+    sw.init();
+    const auto& A = sw.system_matrix();
+    std::printf("big c2: rows %lld nnz %lld col_hash %llu val_hash %llu\n", (long long)A.pattern->rows,
+                (long long)A.pattern->nnz, (unsigned long long)checksum(A.pattern->d_col, A.pattern->nnz),
+                (unsigned long long)checksum(*A.affine, A.pattern->nnz));
+    return 0;
+  }
+  hdd_structured3_desc d3{n, n, n, 1, 1, 1, HDD_BOUNDARY_ALL_DIRICHLET, 3, {-1.0, -1.0, -1.0}, {1.0, 1.0, 1.0}};
+  hdd_grid* g = nullptr;
+  if (hdd_grid_create_structured_3d(&d3, &g) != HDD_OK) return 1;
+  Problems::Problem esv3;
+  esv3.diffusion_tensor = Problems::TensorFunction::identity3d();
+  esv3.force = Problems::ScalarFunction::cos_product(0.75 * M_PI * M_PI, 0.5 * M_PI, 0.5 * M_PI, 0.5 * M_PI, 3);
+  {
+    Discretizations::SWIPDG sw(g, S::Common::Configuration(), esv3, Discretizations::SWIPDG::Layer::leaf, 0, {}, 0,
+                               /*grid_boundary=*/true);
+    sw.init();
+    const auto& A = sw.system_matrix();
+    std::printf("big hex%d: order %d rows %lld nnz %lld col_hash %llu val_hash %llu\n", n, sw.polynomial_order(),
+                (long long)A.pattern->rows, (long long)A.pattern->nnz,
+                (unsigned long long)checksum(A.pattern->d_col, A.pattern->nnz),
+                (unsigned long long)checksum(*A.affine, A.pattern->nnz));
+  }
+  hdd_grid_destroy(g);
+  return 0;
+}
+
 int main(int argc, char** argv)
 {
+  if (argc > 2 && std::string(argv[1]) == "big") return run_big(argv[2], argc > 3 ? std::atoi(argv[3]) : 32);
   const std::string out = argc > 1 ? argv[1] : ".";
   // 1. ESV2007 on a multiscale cube grid: 16x16 Kuhn triangles of [-1,1]^2, partitions [2 2 1]
   hdd_structured_desc d{HDD_SIMPLEX, 16, 16, 2, 2, HDD_BOUNDARY_ALL_DIRICHLET, 0, {-1.0, -1.0}, {1.0, 1.0}};
@@ -37,7 +102,7 @@ int main(int argc, char** argv)
     std::printf("rhs components %d\n", block.rhs().num_components());
     for (const char* id : {"l2", "penalty"}) {
       const auto P = block.get_product(id);
-      dump(out + "/product_" + std::string(id) + "_row_ptr.bin", P.pattern->row_ptr);
+      dump(out + "/product_" + std::string(id) + "_row_ptr.bin", P.pattern->row_ptr());
       auto pv = P.affine_part();
       pv.resize(size_t(P.pattern->nnz));
       dump(out + "/product_" + std::string(id) + ".bin", pv);
@@ -49,22 +114,22 @@ int main(int argc, char** argv)
       std::printf("product rejected: %s\n", e.what());
     }
     const auto& A = block.system_matrix();
-    dump(out + "/block_row_ptr.bin", A.pattern->row_ptr);
-    dump(out + "/block_col.bin", A.pattern->col);
+    dump(out + "/block_row_ptr.bin", A.pattern->row_ptr());
+    dump(out + "/block_col.bin", A.pattern->col());
     auto v = A.affine_part();
     v.resize(size_t(A.pattern->nnz));
     dump(out + "/block_affine.bin", v);
     const auto nbs = block.neighbouring_subdomains(0);
     dump(out + "/neighbours0.bin", std::vector<int32_t>(nbs.begin(), nbs.end()));
     const auto L = block.get_local_operator(0);
-    dump(out + "/local0_row_ptr.bin", L.pattern->row_ptr);
-    dump(out + "/local0_col.bin", L.pattern->col);
+    dump(out + "/local0_row_ptr.bin", L.pattern->row_ptr());
+    dump(out + "/local0_col.bin", L.pattern->col());
     auto lv = L.affine_part();
     lv.resize(size_t(L.pattern->nnz));
     dump(out + "/local0_affine.bin", lv);
     const auto C = block.get_coupling_operator(0, nbs.at(0));
-    dump(out + "/coupling0_row_ptr.bin", C.pattern->row_ptr);
-    dump(out + "/coupling0_col.bin", C.pattern->col);
+    dump(out + "/coupling0_row_ptr.bin", C.pattern->row_ptr());
+    dump(out + "/coupling0_col.bin", C.pattern->col());
     auto cv = C.affine_part();
     cv.resize(size_t(C.pattern->nnz));
     dump(out + "/coupling0_affine.bin", cv);
@@ -125,15 +190,14 @@ int main(int argc, char** argv)
     const auto& A = sw.system_matrix();
     std::printf("hex order %d dofs %lld\n", sw.polynomial_order(), (long long)sw.num_dofs());
     auto a = A.affine_part(); a.resize(size_t(A.pattern->nnz));
-    dump(out + "/hex_row_ptr.bin", A.pattern->row_ptr);
-    dump(out + "/hex_col.bin", A.pattern->col);
+    dump(out + "/hex_row_ptr.bin", A.pattern->row_ptr());
+    dump(out + "/hex_col.bin", A.pattern->col());
     dump(out + "/hex_affine.bin", a);
     dump(out + "/hex_rhs.bin", sw.rhs().affine_part());
   }
   hdd_grid_destroy(g);
 
   // 5. the reference's constructor / init surface (swipdg.hh:159-163, 206, 216-217, 486; base.hh:272-291)
-  namespace S = Dune::Stuff;
   {
     S::Grid::Providers::Cube provider(HDD_SIMPLEX, {-1.0, -1.0}, {1.0, 1.0}, {8, 8}, 1);   // levels 8^2, 16^2
     Discretizations::SWIPDG sw(provider, S::Grid::BoundaryInfos::AllDirichlet::default_config(), Problems::ESV2007(),
@@ -147,7 +211,7 @@ int main(int argc, char** argv)
     } catch (const S::Exceptions::wrong_input_given& e) {
       std::printf("not requested: %s\n", e.what());
     }
-    dump(out + "/lvl1_row_ptr.bin", sw.pattern().row_ptr);
+    dump(out + "/lvl1_row_ptr.bin", sw.pattern().row_ptr());
     dump(out + "/lvl1_affine.bin", sw.system_matrix().affine_part());
     dump(out + "/lvl1_rhs.bin", sw.rhs().affine_part());
     Discretizations::SWIPDG bare(provider, S::Grid::BoundaryInfos::AllDirichlet::default_config(), Problems::ESV2007());
@@ -180,11 +244,11 @@ int main(int argc, char** argv)
     std::printf("local discretization 0: layer local %d, dofs %lld, purely neumann %d\n",
                 int(L0.layer() == Discretizations::SWIPDG::Layer::local), (long long)L0.num_dofs(),
                 int(L0.purely_neumann()));
-    dump(out + "/ld0_row_ptr.bin", L0.pattern().row_ptr);
-    dump(out + "/ld0_col.bin", L0.pattern().col);
+    dump(out + "/ld0_row_ptr.bin", L0.pattern().row_ptr());
+    dump(out + "/ld0_col.bin", L0.pattern().col());
     dump(out + "/ld0_affine.bin", L0.system_matrix().affine_part());
     const auto& P0 = block.get_local_product(0, "l2");
-    dump(out + "/lp0_row_ptr.bin", P0.pattern->row_ptr);
+    dump(out + "/lp0_row_ptr.bin", P0.pattern->row_ptr());
     dump(out + "/lp0_l2.bin", P0.affine_part());
     const auto F0 = block.get_local_functional(0);
     dump(out + "/lf0.bin", F0.affine_part());
@@ -198,8 +262,8 @@ int main(int argc, char** argv)
     // block-swipdg.hh:783-817: subdomain 0 + one ring of face neighbours, Dirichlet / Neumann boundary
     for (const char* bt : {"dirichlet", "neumann"}) {
       const auto& O = block.get_oversampled_discretization(0, bt);
-      dump(out + "/os0_" + std::string(bt) + "_row_ptr.bin", O.pattern().row_ptr);
-      dump(out + "/os0_" + std::string(bt) + "_col.bin", O.pattern().col);
+      dump(out + "/os0_" + std::string(bt) + "_row_ptr.bin", O.pattern().row_ptr());
+      dump(out + "/os0_" + std::string(bt) + "_col.bin", O.pattern().col());
       dump(out + "/os0_" + std::string(bt) + "_affine.bin", O.system_matrix().affine_part());
       dump(out + "/os0_" + std::string(bt) + "_rhs.bin", O.rhs().affine_part());
     }
@@ -232,7 +296,7 @@ int main(int argc, char** argv)
     dump(out + "/spe10_perm.bin", perm);
     S::Grid::Providers::Cube provider(HDD_SIMPLEX, {0.0, 0.0}, {5.0, 1.0}, {100, 20});
     Discretizations::SWIPDG sw(provider, S::Grid::BoundaryInfos::AllDirichlet::default_config(),
-                               Problems::Spe10Model1(perm, channel, forces, true), 0, {"elliptic"});
+                               Problems::Spe10Model1(perm, channel, forces, true, {{0.0, 0.0}}), 0, {"elliptic"});
     sw.init();
     const auto& A = sw.system_matrix();
     std::printf("spe10 parametric %d components %d coefficient %s rhs components %d coefficient %s\n",
@@ -245,6 +309,20 @@ int main(int argc, char** argv)
     dump(out + "/spe10_rhs_comp0.bin", sw.rhs().component(0));
     const auto& E = sw.get_product("elliptic");
     dump(out + "/spe10_elliptic_comp0.bin", E.component(0));
+    // the reference's default channel_boundary_layer (problems/spe10.hh:86, FlatTop's default): the channel is a
+    // sum of FlatTop functions (213-222), evaluated at quadrature points; non-parametric 1 + 0.9 channel and
+    // the parametric split
+    Discretizations::SWIPDG ft(provider, S::Grid::BoundaryInfos::AllDirichlet::default_config(),
+                               Problems::Spe10Model1(perm, channel, forces, false));
+    ft.init();
+    dump(out + "/spe10ft_affine.bin", ft.system_matrix().affine_part());
+    Discretizations::SWIPDG ftp(provider, S::Grid::BoundaryInfos::AllDirichlet::default_config(),
+                                Problems::Spe10Model1(perm, channel, forces, true));
+    ftp.init();
+    std::printf("spe10 flattop channel: components %d order %d\n", ftp.system_matrix().num_components(),
+                ftp.problem().diffusion_factor.components.at(0).order);
+    dump(out + "/spe10ftp_affine.bin", ftp.system_matrix().affine_part());
+    dump(out + "/spe10ftp_comp0.bin", ftp.system_matrix().component(0));
   }
 
   // 8. parametric right-hand side with kappa_p x g_D,q cross terms (swipdg.hh:257-330): OS2014 kappa, g_D(mu) =

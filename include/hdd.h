@@ -11,8 +11,11 @@
  *   - device work is enqueued on the hipStream_t passed as `stream` (NULL = legacy default stream) and
  *     is NOT synchronised; no synchronisation happens inside hdd_swipdg_assemble / hdd_affine_lincomb /
  *     hdd_soa_gather / hdd_soa_scatter, and no allocation either except that hdd_swipdg_assemble on
- *     HDD_HEX p=3 meshes grows a context-owned workspace (576 B per owned element) the first time a
- *     context sees a larger mesh: warm a context up once, then the calls are hipGraph-capturable;
+ *     HDD_HEX p=3 meshes grows a context-owned workspace the first time a context sees a larger mesh --
+ *     8 * (72 n + 1280 ceil(n / 16) + 2 n) bytes for n owned elements (the 576-byte element records, the
+ *     GEMM coefficient fragments of 80 doubles per element padded to groups of 16, 16 bytes of layout per
+ *     element; ~1.23 KB per element) -- and allocates, on its first p=3 call, the context's 80 x 4096 table
+ *     of reference matrices (2.6 MB): warm a context up once, then the calls are hipGraph-capturable;
  *   - one context per thread at a time (thread-compatible, like the reference's single-threaded init()),
  *     and one stream at a time per context: the HDD_HEX p=3 coefficient records live in a per-context
  *     workspace, so concurrent assemblies on different streams need different contexts.
@@ -33,7 +36,8 @@
 extern "C" {
 #endif
 
-#define HDD_ABI_VERSION 3   /* 3: hdd_mesh vertex-indexed geometry, hdd_local_vertices */
+#define HDD_ABI_VERSION 4   /* 3: hdd_mesh vertex-indexed geometry, hdd_local_vertices;
+                               4: HDD_FN_FLATTOP (hdd_scalar_fn.table / n_table), hdd_indicator_sum */
 #define HDD_MAX_COMP 8
 
 typedef enum {
@@ -48,7 +52,8 @@ typedef enum {
 enum { HDD_SIMPLEX = 0, HDD_CUBE = 1,                       /* P1 triangles / Q1 parallelograms (2d) */
        HDD_HEX = 2 };                                        /* Q_p (p = 1..3) on affine hexahedra (3d) */
 enum { HDD_NBR_DIRICHLET = -1, HDD_NBR_NEUMANN = -2 };       /* neighbour codes of domain-boundary faces */
-enum { HDD_FN_CONST = 0, HDD_FN_PER_ELEM = 1, HDD_FN_SINUSOID = 2, HDD_FN_COS_PRODUCT = 3 };
+enum { HDD_FN_CONST = 0, HDD_FN_PER_ELEM = 1, HDD_FN_SINUSOID = 2, HDD_FN_COS_PRODUCT = 3, HDD_FN_FLATTOP = 4 };
+#define HDD_FLATTOP_REC 7      /* doubles per HDD_FN_FLATTOP box: lx, ly, ux, uy, layer_x, layer_y, value */
 enum { HDD_TENSOR_CONST = 0, HDD_TENSOR_ISO_PER_ELEM = 1, HDD_TENSOR_SYM_PER_ELEM = 2 };
 enum { HDD_BOUNDARY_ALL_DIRICHLET = 0, HDD_BOUNDARY_ALL_NEUMANN = 1 };
 
@@ -158,6 +163,9 @@ int hdd_checkerboard(int64_t n, const double* centers /*[2][n]*/, const double l
  * force): value of the first closed box [lx, ux] x [ly, uy] containing the barycentre, 0 if none;
  * boxes[5k .. 5k+4] = lx, ly, ux, uy, value */
 int hdd_indicator(int64_t n, const double* centers /*[2][n]*/, int32_t n_boxes, const double* boxes, double* out);
+/* the sum of one-box Indicators (make_sum of the channel's per-box functions, problems/spe10.hh:139-148 with
+ * channel_boundary_layer == 0): sum of the values of every closed box containing the barycentre */
+int hdd_indicator_sum(int64_t n, const double* centers /*[2][n]*/, int32_t n_boxes, const double* boxes, double* out);
 
 /* ---------------------------------------------------------------------------------------------- */
 /* sparsity pattern (host) -- replaces EllipticSWIPDG::pattern(test, ansatz) (swipdg.hh:169) and the */
@@ -211,6 +219,15 @@ typedef struct {              /* one diffusion-factor component kappa_q (a Stuff
                                  COS_PRODUCT: a*cos(kx*x)*cos(ky*y) [*cos(b*z) in 3d when b != 0]
                                  (ESV2007 Testcase1Force, problems/ESV2007.hh:78) -- right-hand sides */
   const double* per_elem;     /* PER_ELEM: device [n_local] */
+  /* FLATTOP: c + b * sum_k value_k phi(x; lx_k, ux_k, layer_x_k) phi(y; ly_k, uy_k, layer_y_k) -- the sum of
+   * dune-stuff FlatTop functions the Spe10::Model1 channel is built from when channel_boundary_layer != 0
+   * (problems/spe10.hh:139-148, 213-222): per coordinate 1 on [l + d, u - d], 0 outside [l - d, u + d] and
+   * the C^1 cubic transitions (1 + t)^2 (1 - 2t), t = (x - (l + d)) / 2d in [-1, 0), and (1 - t)^2 (1 + 2t),
+   * t = (x - (u - d)) / 2d in [0, 1) (layers d > 0).  `order` is the integration order the caller
+   * assigns to the function (Stuff's order()).  2d meshes only. */
+  const double* table;        /* FLATTOP: device [n_table][HDD_FLATTOP_REC] */
+  int32_t n_table;            /* FLATTOP: number of boxes */
+  int32_t pad1;
 } hdd_scalar_fn;
 
 typedef struct {              /* the (non-parametric) diffusion tensor A */
@@ -311,6 +328,19 @@ int hdd_block_operator_map(const hdd_grid* g, int32_t ss, int32_t nn, const int6
                            int64_t* out_row_ptr, int32_t* out_col, int64_t* out_src, int64_t* nnz);
 /* d_out[k] = d_vals[d_src[k]] for k < n (device arrays) */
 int hdd_gather_values(hdd_ctx* ctx, const double* d_vals, const int64_t* d_src, int64_t n, double* d_out, void* stream);
+/* The same on the device, from the device pattern: rows [row_begin, row_end) of `pattern` restricted to the
+ * columns [col_begin, col_end) (operator (ss, nn): rows / columns of the element ranges of ss / nn times nb,
+ * hdd_grid_subdomain_range), renumbered col - col_begin.  Writes d_out_row_ptr [rows+1] always; d_out_col /
+ * d_out_src [nnz] when d_out_col != NULL (d_out_src nullable); *nnz (host) when nnz != NULL, which
+ * synchronises `stream` -- call once with d_out_col == NULL and nnz to size the arrays, or pass the known
+ * nnz (nb^2 x the ss/nn element-face pairs, plus nb^2 |ss| for ss == nn) and stay asynchronous. */
+int hdd_block_operator_map_device(hdd_ctx* ctx, const hdd_csr* pattern, int64_t row_begin, int64_t row_end,
+                                  int64_t col_begin, int64_t col_end, int64_t* d_out_row_ptr, int32_t* d_out_col,
+                                  int64_t* d_out_src, int64_t* nnz, void* stream);
+/* the operator's values of n_comp value arrays on `pattern` (d_out_row_ptr from the map call): no index map */
+int hdd_block_operator_values_device(hdd_ctx* ctx, const hdd_csr* pattern, int64_t row_begin, int64_t row_end,
+                                     int64_t col_begin, int64_t col_end, const int64_t* d_out_row_ptr,
+                                     const double* const* d_vals, int32_t n_comp, double* const* d_out, void* stream);
 
 /* ---------------------------------------------------------------------------------------------- */
 /* sharded BlockSWIPDG (SURVEY.md 8(b) hdd_block_assemble_sharded, 8(e)): one process (or thread) per  */

@@ -32,6 +32,7 @@
 #include <limits>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <ostream>
 #include <set>
 #include <stdexcept>
@@ -275,13 +276,14 @@ namespace Problems {
 // device at quadrature points; Checkerboard / Indicator (order 0, entity-centre based) are evaluated at the
 // element barycentres on the host and uploaded as per-element values
 struct ScalarFunction {
-  enum Host { DEVICE = 0, CHECKERBOARD = 1, INDICATOR = 2 };
+  enum Host { DEVICE = 0, CHECKERBOARD = 1, INDICATOR = 2, INDICATOR_SUM = 3 };
   int kind = HDD_FN_CONST;
   int host = DEVICE;
   int order = 0;
   double c = 1.0, b = 0.0, kx = 0.0, ky = 0.0;
   std::vector<double> per_element;   // PER_ELEM: global element order
-  // CHECKERBOARD: cells (x fastest) on [lower, upper]; INDICATOR: boxes [5k..5k+4] = lx, ly, ux, uy, value
+  // CHECKERBOARD: cells (x fastest) on [lower, upper]; INDICATOR(_SUM): boxes [5k..5k+4] = lx, ly, ux, uy, value;
+  // FLATTOP (device kind): boxes [7k..7k+6] = lx, ly, ux, uy, layer_x, layer_y, value
   std::array<double, 2> lower{{0.0, 0.0}}, upper{{1.0, 1.0}};
   int ncx = 1, ncy = 1;
   std::vector<double> table;
@@ -315,6 +317,28 @@ struct ScalarFunction {
   {
     ScalarFunction f; f.kind = HDD_FN_PER_ELEM; f.host = INDICATOR;
     for (const auto& bx : boxes) f.table.insert(f.table.end(), bx.begin(), bx.end());
+    return f;
+  }
+  // c + b * (sum of one-box Indicators): Stuff::Functions::make_sum of the Spe10 channel's per-box Indicators
+  // (problems/spe10.hh:139-148 with channel_boundary_layer == 0), evaluated at the entity centre
+  static ScalarFunction indicator_sum(std::vector<std::array<double, 5>> boxes, double c = 0.0, double b = 1.0)
+  {
+    ScalarFunction f; f.kind = HDD_FN_PER_ELEM; f.host = INDICATOR_SUM; f.c = c; f.b = b;
+    for (const auto& bx : boxes) f.table.insert(f.table.end(), bx.begin(), bx.end());
+    return f;
+  }
+  // c + b * (sum of dune-stuff FlatTop functions), the Spe10 channel with channel_boundary_layer != 0
+  // (problems/spe10.hh:213-222); evaluated on the device at quadrature points (HDD_FN_FLATTOP).  order: the
+  // integration order (restated assumption: 3, the degree of the transitions per coordinate)
+  static ScalarFunction flattop_sum(std::vector<std::array<double, 7>> boxes, double c = 0.0, double b = 1.0,
+                                    int order = 3)
+  {
+    ScalarFunction f; f.kind = HDD_FN_FLATTOP; f.c = c; f.b = b; f.order = order;
+    for (const auto& bx : boxes) {
+      if (!(bx[4] > 0.0 && bx[5] > 0.0))
+        throw Stuff::Exceptions::wrong_input_given("FlatTop: the boundary layer must be positive (0: Indicator)");
+      f.table.insert(f.table.end(), bx.begin(), bx.end());
+    }
     return f;
   }
   bool is_zero() const { return kind == HDD_FN_CONST && host == DEVICE && c == 0.0; }
@@ -413,27 +437,37 @@ inline Problem OS2014()
   return p;
 }
 
+// the FlatTop default boundary layer the Spe10::Model1 default config takes (problems/spe10.hh:86:
+// FlatTopFunctionType::default_config()["boundary_layer"]); dune-stuff is absent here, so this is the
+// restated default (1e-1 per coordinate), unverifiable
+inline std::array<double, 2> flattop_default_boundary_layer() { return {{0.1, 0.1}}; }
+
 // Spe10::Model1 (problems/spe10.hh:131-185): A = permeability checkerboard (100 x 20 cells on [0,5]x[0,1]),
-// force = Indicator(force boxes), g_D = g_N = 0; diffusion factor 1 + 0.9 channel, or with
-// parametric_channel the affine part 1 + channel and the component channel with theta = -1.0*mu
-// (problems/spe10.hh:160-172).  The channel is an Indicator (channel_boundary_layer = 0,
-// testcases/spe10.hh:257; FlatTop layers are not supported).
+// force = Indicator(force boxes), g_D = g_N = 0; the channel is the sum of one function per channel box
+// (139-148): an Indicator when channel_boundary_layer == 0 (the parametric test case, testcases/spe10.hh:257),
+// else a FlatTop with that boundary layer (213-222); diffusion factor 1 + 0.9 channel (175-179), or with
+// parametric_channel the affine part 1 + channel and the component channel with theta = -1.0*mu (160-172).
+// Integration order of a FlatTop channel: flattop_order (restated assumption 3, see ScalarFunction::flattop_sum).
 inline Problem Spe10Model1(std::vector<double> permeability, std::vector<std::array<double, 5>> channel,
-                           std::vector<std::array<double, 5>> forces, bool parametric_channel)
+                           std::vector<std::array<double, 5>> forces, bool parametric_channel,
+                           std::array<double, 2> channel_boundary_layer = flattop_default_boundary_layer(),
+                           int flattop_order = 3)
 {
   Problem p;
   p.diffusion_tensor = TensorFunction::spe10_model1(std::move(permeability));
   p.force = ScalarFunction::indicator(std::move(forces));
-  if (channel.empty()) return p;   // no channel: diffusion factor 1 (problems/spe10.hh:141-142)
-  std::vector<std::array<double, 5>> one_plus = channel, scaled = channel;
-  for (auto& bx : one_plus) bx[4] = 1.0 + bx[4];    // 1 + channel (boxes disjoint, 1 outside)
-  for (auto& bx : scaled) bx[4] = 1.0 + 0.9 * bx[4];
-  auto affine = ScalarFunction::indicator(parametric_channel ? one_plus : scaled);
-  affine.table.insert(affine.table.end(), {-1e300, -1e300, 1e300, 1e300, 1.0});   // outside the channel: 1
-  p.diffusion_factor.affine_part = affine;
+  if (channel.empty()) return p;   // no channel: diffusion factor 1 + 0.9 * 0 (problems/spe10.hh:141-142)
+  const bool indicator = channel_boundary_layer[0] == 0.0 && channel_boundary_layer[1] == 0.0;
+  auto channel_fn = [&](double c, double b) {
+    if (indicator) return ScalarFunction::indicator_sum(channel, c, b);
+    std::vector<std::array<double, 7>> ft;
+    for (const auto& bx : channel)
+      ft.push_back({{bx[0], bx[1], bx[2], bx[3], channel_boundary_layer[0], channel_boundary_layer[1], bx[4]}});
+    return ScalarFunction::flattop_sum(ft, c, b, flattop_order);
+  };
+  p.diffusion_factor.affine_part = parametric_channel ? channel_fn(1.0, 1.0) : channel_fn(1.0, 0.9);
   if (parametric_channel)
-    p.diffusion_factor.register_component(ScalarFunction::indicator(std::move(channel)),
-                                          Pymor::ParameterFunctional("mu", "-1.0*mu", -1.0));
+    p.diffusion_factor.register_component(channel_fn(0.0, 1.0), Pymor::ParameterFunctional("mu", "-1.0*mu", -1.0));
   return p;
 }
 }  // namespace Problems
@@ -479,15 +513,38 @@ class Communicator {
 
 namespace Discretizations {
 
-// CSR pattern resident on the device (host copy kept for operator extraction)
+// CSR pattern resident on the device.  Patterns are built and block operators extracted on the device
+// (hdd_pattern_*_device, hdd_block_operator_map_device); host copies of row_ptr / col are downloaded only
+// when a caller asks for them (at C5 scale the column array alone is tens of GB).
 class Pattern {
  public:
   int64_t rows = 0, cols = 0, nnz = 0;
-  std::vector<int64_t> row_ptr, elem_ptr;
-  std::vector<int32_t> col;
   internal::DeviceArray<int64_t> d_row_ptr, d_elem_ptr;
   internal::DeviceArray<int32_t> d_col;
   hdd_csr csr() const { return hdd_csr{rows, cols, nnz, d_row_ptr.get(), d_col.get(), d_elem_ptr.get()}; }
+  const std::vector<int64_t>& row_ptr() const
+  {
+    std::lock_guard<std::mutex> lock(m_);
+    if (h_row_ptr_.size() != size_t(rows + 1)) {
+      h_row_ptr_ = d_row_ptr.download();
+      h_row_ptr_.resize(size_t(rows + 1));
+    }
+    return h_row_ptr_;
+  }
+  const std::vector<int32_t>& col() const
+  {
+    std::lock_guard<std::mutex> lock(m_);
+    if (h_col_.size() != size_t(nnz)) {
+      h_col_ = d_col.download();
+      h_col_.resize(size_t(nnz));
+    }
+    return h_col_;
+  }
+
+ private:
+  mutable std::mutex m_;
+  mutable std::vector<int64_t> h_row_ptr_;
+  mutable std::vector<int32_t> h_col_;
 };
 
 // AffinelyDecomposedContainer<Matrix>: components on one shared pattern (values on the device)
@@ -586,14 +643,20 @@ struct ElementView {
 inline std::vector<double> localize(const Problems::ScalarFunction& f, const ElementView& v)
 {
   std::vector<double> h(static_cast<size_t>(v.n));
-  if (f.host == Problems::ScalarFunction::CHECKERBOARD || f.host == Problems::ScalarFunction::INDICATOR) {
+  if (f.host == Problems::ScalarFunction::CHECKERBOARD || f.host == Problems::ScalarFunction::INDICATOR ||
+      f.host == Problems::ScalarFunction::INDICATOR_SUM) {
     if (v.dim != 2) throw NotImplemented("Checkerboard / Indicator functions are 2d");
     if (f.host == Problems::ScalarFunction::CHECKERBOARD)
       internal::check(hdd_checkerboard(v.n, v.centers, f.lower.data(), f.upper.data(), f.ncx, f.ncy, f.table.data(),
                                        h.data()), "hdd_checkerboard");
-    else
+    else if (f.host == Problems::ScalarFunction::INDICATOR)
       internal::check(hdd_indicator(v.n, v.centers, int32_t(f.table.size() / 5), f.table.data(), h.data()),
                       "hdd_indicator");
+    else {   // INDICATOR_SUM: c + b * sum of the boxes' values
+      internal::check(hdd_indicator_sum(v.n, v.centers, int32_t(f.table.size() / 5), f.table.data(), h.data()),
+                      "hdd_indicator_sum");
+      for (auto& x : h) x = f.c + f.b * x;
+    }
   } else {
     if (int64_t(f.per_element.size()) != v.n_global)
       throw Stuff::Exceptions::wrong_input_given("per-element function: " + std::to_string(f.per_element.size()) +
@@ -609,12 +672,17 @@ inline std::vector<double> localize(const Problems::ScalarFunction& f, const Ele
 // a scalar function bound to the device (per-element values uploaded, kept alive with the descriptor)
 struct DeviceFn {
   hdd_scalar_fn fn{};
-  std::shared_ptr<internal::DeviceArray<double>> pe;
+  std::shared_ptr<internal::DeviceArray<double>> pe, table;
   DeviceFn() = default;
   DeviceFn(const Problems::ScalarFunction& f, const ElementView& v)
   {
     if (f.kind == HDD_FN_PER_ELEM) pe = std::make_shared<internal::DeviceArray<double>>(localize(f, v));
-    fn = hdd_scalar_fn{f.kind, f.order, f.c, f.b, f.kx, f.ky, pe ? pe->get() : nullptr};
+    if (f.kind == HDD_FN_FLATTOP) {
+      if (v.dim != 2) throw NotImplemented("FlatTop functions are 2d");
+      table = std::make_shared<internal::DeviceArray<double>>(f.table.empty() ? std::vector<double>(1, 0.0) : f.table);
+    }
+    fn = hdd_scalar_fn{f.kind, f.order, f.c, f.b, f.kx, f.ky, pe ? pe->get() : nullptr,
+                       table ? table->get() : nullptr, int32_t(f.table.size() / HDD_FLATTOP_REC), 0};
   }
 };
 
@@ -844,39 +912,53 @@ class SWIPDG {
     view_ = detail::ElementView{n, ob, oe, info_.dim, centers_.data(), gid_.data(), info_.n_elements, false};
   }
 
-  std::shared_ptr<Pattern> host_pattern(int n_faces) const
+  // EllipticSWIPDG::pattern (swipdg.hh:169) on the device: hdd_pattern_elem_ptr_device + hdd_pattern_fill_device
+  // over the neighbour codes with the boundary info applied, columns through cols_ (global ids, or the
+  // subdomain's own numbering for the local layer).  volume: the element-diagonal pattern of the l2 / h1 /
+  // elliptic / boundary products (no face neighbours: every neighbour code is a boundary code)
+  std::shared_ptr<Pattern> device_pattern(bool volume) const
   {
     auto P = std::make_shared<Pattern>();
-    const int64_t n = linfo_.n_local;
-    internal::check(hdd_dg_pattern_count(n_faces, info_.nb, n, linfo_.own_begin, linfo_.own_end, nbrs_.data(), &P->nnz),
-                    "hdd_dg_pattern_count");
-    const int64_t own = linfo_.own_end - linfo_.own_begin;
+    const int64_t n = linfo_.n_local, own = linfo_.own_end - linfo_.own_begin;
+    internal::DeviceArray<int32_t> none;
+    const int32_t* nb = d_nbrs_.get();
+    if (volume) {
+      none = internal::DeviceArray<int32_t>(size_t(info_.nfaces * n) + 1);
+      internal::hip_check(hipMemset(none.get(), 0xff, none.size() * sizeof(int32_t)), "device_pattern");   // -1
+      nb = none.get();
+    }
+    const hdd_mesh m{info_.elem_type, degree_, n, linfo_.own_begin, linfo_.own_end, nullptr, nb, nullptr, nullptr, nullptr};
     P->rows = own * info_.nb;
     P->cols = n_cols_;
-    P->row_ptr.resize(size_t(P->rows + 1));
-    P->col.resize(size_t(P->nnz));
-    P->elem_ptr.resize(size_t(own + 1));
-    internal::check(hdd_dg_pattern_fill(n_faces, info_.nb, n, linfo_.own_begin, linfo_.own_end, nbrs_.data(),
-                                        cols_.data(), P->row_ptr.data(), P->col.data(), P->elem_ptr.data()),
-                    "hdd_dg_pattern_fill");
-    P->d_row_ptr = internal::DeviceArray<int64_t>(P->row_ptr);
-    P->d_col = internal::DeviceArray<int32_t>(P->col);
-    P->d_elem_ptr = internal::DeviceArray<int64_t>(P->elem_ptr);
+    P->d_elem_ptr = internal::DeviceArray<int64_t>(size_t(own + 1));
+    internal::check(hdd_pattern_elem_ptr_device(ctx_, &m, info_.nb, P->d_elem_ptr.get(), &P->nnz, nullptr),
+                    "hdd_pattern_elem_ptr_device");
+    P->d_row_ptr = internal::DeviceArray<int64_t>(size_t(P->rows + 1));
+    P->d_col = internal::DeviceArray<int32_t>(size_t(std::max<int64_t>(P->nnz, 1)));
+    internal::check(hdd_pattern_fill_device(ctx_, &m, info_.nb, d_cols_.get(), P->d_elem_ptr.get(), P->d_row_ptr.get(),
+                                            P->d_col.get(), nullptr), "hdd_pattern_fill_device");
+    internal::hip_check(hipDeviceSynchronize(), "device_pattern");
     return P;
   }
 
-  void build_pattern() { pattern_ = host_pattern(info_.nfaces); }
+  void build_pattern()
+  {
+    const auto t0 = internal::Timer::now();
+    d_nbrs_ = internal::DeviceArray<int32_t>(nbrs_);
+    d_cols_ = internal::DeviceArray<int64_t>(cols_);
+    pattern_ = device_pattern(false);
+    pattern_seconds_ = internal::seconds_since(t0);
+  }
 
   std::shared_ptr<const Pattern> volume_pattern()
   {
-    if (!volume_pattern_) volume_pattern_ = host_pattern(0);
+    if (!volume_pattern_) volume_pattern_ = device_pattern(true);
     return volume_pattern_;
   }
 
   void upload_mesh()
   {
-    d_coords_ = internal::DeviceArray<double>(coords_);
-    d_nbrs_ = internal::DeviceArray<int32_t>(nbrs_);
+    d_coords_ = internal::DeviceArray<double>(coords_);   // (d_nbrs_: uploaded with the pattern build)
     d_finfo_ = internal::DeviceArray<uint32_t>(finfo_);
     if (info_.dim == 2) {   // vertex-indexed geometry: what the P1 / Q1 stiffness kernels read
       int64_t nv = 0;
@@ -1031,12 +1113,14 @@ class SWIPDG {
   internal::DeviceArray<int32_t> d_ev_;
   internal::DeviceArray<double> d_vxy_;
   internal::DeviceArray<int32_t> d_nbrs_;
+  internal::DeviceArray<int64_t> d_cols_;
   internal::DeviceArray<uint32_t> d_finfo_;
   detail::DeviceTensor tensor_;
   hdd_mesh mesh_{};
   hdd_swipdg_params prm_{};
   int degree_ = 1;
   bool purely_neumann_ = false;
+  double pattern_seconds_ = 0.0;   // measured time of the pattern build at construction
   AffinelyDecomposedMatrix matrix_;
   AffinelyDecomposedVector rhs_;
   std::map<std::string, std::shared_ptr<AffinelyDecomposedMatrix>> products_;
@@ -1044,8 +1128,11 @@ class SWIPDG {
 };
 
 namespace detail {
-// face-neighbour subdomains of every subdomain (MsGrid::neighborsOf), one pass over the grid
-inline std::vector<std::set<int>> subdomain_neighbours(const hdd_grid* g, const hdd_grid_info& gi)
+// face-neighbour subdomains of every subdomain (MsGrid::neighborsOf), one pass over the grid; `pairs`
+// (optional) counts the (element of ss, face neighbour in nn) pairs of every subdomain pair -- nb^2 times that
+// (plus nb^2 |ss| on the diagonal) is the nnz of the block operator (ss, nn)
+inline std::vector<std::set<int>> subdomain_neighbours(const hdd_grid* g, const hdd_grid_info& gi,
+                                                       std::map<std::pair<int, int>, int64_t>* pairs = nullptr)
 {
   std::vector<std::set<int>> nb(size_t(gi.n_subdomains));
   hdd_local* l = nullptr;
@@ -1059,7 +1146,9 @@ inline std::vector<std::set<int>> subdomain_neighbours(const hdd_grid* g, const 
   for (int f = 0; f < gi.nfaces; ++f)
     for (int64_t e = 0; e < li.n_local; ++e) {
       const int32_t n = nbrs[size_t(f * li.n_local + e)];
-      if (n >= 0 && sd[size_t(n)] != sd[size_t(e)]) nb[size_t(sd[size_t(e)])].insert(sd[size_t(n)]);
+      if (n < 0) continue;
+      if (sd[size_t(n)] != sd[size_t(e)]) nb[size_t(sd[size_t(e)])].insert(sd[size_t(n)]);
+      if (pairs) ++(*pairs)[{sd[size_t(e)], sd[size_t(n)]}];
     }
   return nb;
 }
@@ -1097,10 +1186,13 @@ class BlockSWIPDG : public SWIPDG {
   void init(std::ostream& out = Stuff::Common::devnull(), const std::string& prefix = "")
   {
     if (initialized_) return;
-    out << prefix << "walking subdomains for the first time... " << std::flush;
-    const auto t0 = internal::Timer::now();
-    out << "done (took " << internal::seconds_since(t0) << " sek)" << std::endl;
+    // the reference's first walk builds the local and coupling patterns (block-swipdg.hh:266-328): here the
+    // global block pattern was built once at construction, and its measured time is reported; the second walk
+    // (local, boundary and coupling matrices, 330-386) is the one-pass device assembly
+    out << prefix << "walking subdomains for the first time (block pattern, built at construction)... done (took "
+        << pattern_seconds_ << " sek)" << std::endl;
     out << prefix << "walking subdomains for the second time... " << std::flush;
+    const auto t0 = internal::Timer::now();
     SWIPDG::init();
     out << "done (took " << internal::seconds_since(t0) << " sek)" << std::endl;
   }
@@ -1255,7 +1347,7 @@ class BlockSWIPDG : public SWIPDG {
  private:
   void setup()
   {
-    neighbours_ = detail::subdomain_neighbours(grid_, info_);
+    neighbours_ = detail::subdomain_neighbours(grid_, info_, &face_pairs_);
     local_discretizations_.resize(size_t(info_.n_subdomains));
   }
 
@@ -1266,41 +1358,49 @@ class BlockSWIPDG : public SWIPDG {
                                                   " is not true for ss = " + std::to_string(ss) + "!");
   }
 
+  // block-swipdg.hh:625-676: rows of ss, columns of nn, both in local numbering -- extracted on the device from
+  // the assembled global matrix (hdd_block_operator_map_device / _values_device); the nnz is known from the
+  // face pairs counted at construction, so nothing synchronises until the caller reads the result
   AffinelyDecomposedMatrix extract(int ss, int nn) const
   {
     range_check(ss);
     range_check(nn);
     const auto& M = system_matrix();
-    int64_t nnz = 0;
-    internal::check(hdd_block_operator_map(grid_, ss, nn, pattern_->row_ptr.data(), pattern_->col.data(), nullptr,
-                                           nullptr, nullptr, &nnz), "hdd_block_operator_map");
     int64_t a, b, c, d;
     internal::check(hdd_grid_subdomain_range(grid_, ss, ss + 1, &a, &b), "range");
     internal::check(hdd_grid_subdomain_range(grid_, nn, nn + 1, &c, &d), "range");
+    const int64_t nb = info_.nb;
+    const auto fp = face_pairs_.find({ss, nn});
     auto P = std::make_shared<Pattern>();
-    P->rows = (b - a) * info_.nb;
-    P->cols = (d - c) * info_.nb;
-    P->nnz = nnz;
-    P->row_ptr.resize(size_t(P->rows + 1));
-    P->col.resize(size_t(nnz));
-    std::vector<int64_t> src(static_cast<size_t>(nnz));
-    internal::check(hdd_block_operator_map(grid_, ss, nn, pattern_->row_ptr.data(), pattern_->col.data(),
-                                           P->row_ptr.data(), P->col.data(), src.data(), &nnz), "hdd_block_operator_map");
-    P->d_row_ptr = internal::DeviceArray<int64_t>(P->row_ptr);
-    P->d_col = internal::DeviceArray<int32_t>(P->col);
-    internal::DeviceArray<int64_t> d_src(src);
+    P->rows = (b - a) * nb;
+    P->cols = (d - c) * nb;
+    P->nnz = nb * nb * ((fp == face_pairs_.end() ? 0 : fp->second) + (ss == nn ? b - a : 0));
+    P->d_row_ptr = internal::DeviceArray<int64_t>(size_t(P->rows + 1));
+    P->d_col = internal::DeviceArray<int32_t>(size_t(P->nnz) + 1);
+    const hdd_csr pat = pattern_->csr();
+    internal::check(hdd_block_operator_map_device(ctx_, &pat, a * nb, b * nb, c * nb, d * nb, P->d_row_ptr.get(),
+                                                  P->d_col.get(), nullptr, nullptr, nullptr),
+                    "hdd_block_operator_map_device");
     AffinelyDecomposedMatrix out;
     out.pattern = P;
     out.ctx = ctx_;
     out.coefficients = M.coefficients;
-    auto gather = [&](const internal::DeviceArray<double>& v) {
-      auto o = std::make_shared<internal::DeviceArray<double>>(size_t(nnz) + 1);
-      internal::check(hdd_gather_values(ctx_, v.get(), d_src.get(), nnz, o->get(), nullptr), "hdd_gather_values");
+    std::vector<const double*> in;
+    std::vector<double*> res;
+    auto slot = [&](const internal::DeviceArray<double>& v) {
+      auto o = std::make_shared<internal::DeviceArray<double>>(size_t(P->nnz) + 1);
+      in.push_back(v.get());
+      res.push_back(o->get());
       return o;
     };
-    if (M.affine) out.affine = gather(*M.affine);
-    for (const auto& q : M.comps) out.comps.push_back(gather(*q));
-    internal::hip_check(hipDeviceSynchronize(), "extract");
+    if (M.affine) out.affine = slot(*M.affine);
+    for (const auto& q : M.comps) out.comps.push_back(slot(*q));
+    for (size_t i0 = 0; i0 < in.size(); i0 += HDD_MAX_COMP) {
+      const int32_t k = int32_t(std::min<size_t>(HDD_MAX_COMP, in.size() - i0));
+      internal::check(hdd_block_operator_values_device(ctx_, &pat, a * nb, b * nb, c * nb, d * nb, P->d_row_ptr.get(),
+                                                       in.data() + i0, k, res.data() + i0, nullptr),
+                      "hdd_block_operator_values_device");
+    }
     return out;
   }
 
@@ -1326,6 +1426,7 @@ class BlockSWIPDG : public SWIPDG {
   int device_ = 0;
   int oversampling_layers_ = 0;
   std::vector<std::set<int>> neighbours_;
+  std::map<std::pair<int, int>, int64_t> face_pairs_;   // (ss, nn) -> element-face pairs (operator nnz / nb^2)
   mutable std::vector<std::shared_ptr<SWIPDG>> local_discretizations_;
   mutable std::map<std::pair<int, std::string>, std::shared_ptr<SWIPDG>> oversampled_;
 };
@@ -1391,8 +1492,6 @@ class ShardedBlockSWIPDG {
     P->d_elem_ptr = internal::DeviceArray<int64_t>(size_t(sinfo_.own_end - sinfo_.own_begin + 1));
     internal::check(hdd_shard_pattern_fill(ctx_, shard_, P->d_row_ptr.get(), P->d_col.get(), P->d_elem_ptr.get(),
                                            nullptr), "hdd_shard_pattern_fill");
-    P->row_ptr = P->d_row_ptr.download();
-    P->col = P->d_col.download();
     pattern_ = P;
     tensor_ = detail::DeviceTensor(problem_.diffusion_tensor, view_);
     prm_ = detail::swipdg_params(detail::degree_of(info_), info_.dim);
@@ -1418,17 +1517,35 @@ class ShardedBlockSWIPDG {
 
   // one sharded LHS step for every component: pack -> exchange -> interior tiles -> unpack -> boundary tiles
   // (hdd_block_assemble_sharded); flags HDD_SHARD_* (NO_HALO once the ghost coefficients are current)
+  // One kernel serves diffusion-factor parts of one integration order, so the parts are grouped by order
+  // (at most HDD_MAX_COMP per call), one sharded call per group.  The first call exchanges the halo; a later
+  // call exchanges again only if it carries per-element parts (their ghost columns are filled by its own
+  // unpack), otherwise the ghost tensor columns are current and it runs with HDD_SHARD_NO_HALO.
   void assemble(uint32_t flags = 0, hipStream_t stream = nullptr)
   {
-    std::vector<hdd_scalar_fn> k;
-    std::vector<double*> v;
+    std::map<int, std::vector<size_t>> by_order;
     for (size_t q = 0; q < kappas_.size(); ++q) {
-      k.push_back(kappas_[q].fn);
-      v.push_back(q < matrix_.comps.size() ? matrix_.comps[q]->get() : matrix_.affine->get());
+      const hdd_scalar_fn& f = kappas_[q].fn;
+      by_order[f.kind == HDD_FN_CONST || f.kind == HDD_FN_PER_ELEM ? 0 : f.order].push_back(q);
     }
     const hdd_csr pat = pattern_->csr();
-    internal::check(hdd_block_assemble_sharded(ctx_, shard_, comm_.get(), k.data(), int32_t(k.size()), &tensor_.fn, &prm_,
-                                               &pat, v.data(), flags, stream), "hdd_block_assemble_sharded");
+    bool exchanged = false;
+    for (const auto& g : by_order)
+      for (size_t i0 = 0; i0 < g.second.size(); i0 += HDD_MAX_COMP) {
+        std::vector<hdd_scalar_fn> k;
+        std::vector<double*> v;
+        bool per_elem = false;
+        for (size_t i = i0; i < std::min(g.second.size(), i0 + HDD_MAX_COMP); ++i) {
+          const size_t q = g.second[i];
+          k.push_back(kappas_[q].fn);
+          per_elem = per_elem || kappas_[q].fn.kind == HDD_FN_PER_ELEM;
+          v.push_back(q < matrix_.comps.size() ? matrix_.comps[q]->get() : matrix_.affine->get());
+        }
+        const uint32_t f = (exchanged && !per_elem) ? (flags | HDD_SHARD_NO_HALO) : flags;
+        internal::check(hdd_block_assemble_sharded(ctx_, shard_, comm_.get(), k.data(), int32_t(k.size()), &tensor_.fn,
+                                                   &prm_, &pat, v.data(), f, stream), "hdd_block_assemble_sharded");
+        exchanged = true;
+      }
   }
 
   const AffinelyDecomposedMatrix& system_matrix() const { ready(); return matrix_; }   // owned rows, global columns
@@ -1452,40 +1569,36 @@ class ShardedBlockSWIPDG {
     int64_t a, b, c, d;
     internal::check(hdd_grid_subdomain_range(grid_, ss, ss + 1, &a, &b), "range");
     internal::check(hdd_grid_subdomain_range(grid_, nn, nn + 1, &c, &d), "range");
-    const int nb = info_.nb;
+    const int64_t nb = info_.nb;
     const int64_t r0 = (a - sinfo_.global_first) * nb, r1 = (b - sinfo_.global_first) * nb;
     auto P = std::make_shared<Pattern>();
     P->rows = r1 - r0;
     P->cols = (d - c) * nb;
-    P->row_ptr.assign(1, 0);
-    std::vector<int64_t> src;
-    for (int64_t r = r0; r < r1; ++r) {
-      for (int64_t q = pattern_->row_ptr[size_t(r)]; q < pattern_->row_ptr[size_t(r + 1)]; ++q) {
-        const int64_t col = pattern_->col[size_t(q)];
-        if (col < c * nb || col >= d * nb) continue;
-        P->col.push_back(int32_t(col - c * nb));
-        src.push_back(q);
-      }
-      P->row_ptr.push_back(int64_t(P->col.size()));
-    }
-    P->nnz = int64_t(P->col.size());
+    P->d_row_ptr = internal::DeviceArray<int64_t>(size_t(P->rows + 1));
+    const hdd_csr pat = pattern_->csr();
+    // device extraction (hdd_block_operator_map_device): count + scan first (synchronises for the nnz)
+    internal::check(hdd_block_operator_map_device(ctx_, &pat, r0, r1, c * nb, d * nb, P->d_row_ptr.get(), nullptr,
+                                                  nullptr, &P->nnz, nullptr), "hdd_block_operator_map_device");
     if (P->nnz == 0 && nn != ss)
       throw Stuff::Exceptions::index_out_of_range("Subdomain " + std::to_string(nn) + " is not a neighbour of subdomain " +
                                                   std::to_string(ss));
-    P->d_row_ptr = internal::DeviceArray<int64_t>(P->row_ptr);
-    P->d_col = internal::DeviceArray<int32_t>(P->col);
-    internal::DeviceArray<int64_t> d_src(src);
+    P->d_col = internal::DeviceArray<int32_t>(size_t(P->nnz) + 1);
+    internal::check(hdd_block_operator_map_device(ctx_, &pat, r0, r1, c * nb, d * nb, P->d_row_ptr.get(), P->d_col.get(),
+                                                  nullptr, nullptr, nullptr), "hdd_block_operator_map_device");
     AffinelyDecomposedMatrix out;
     out.pattern = P;
     out.ctx = ctx_;
     out.coefficients = matrix_.coefficients;
-    auto gather = [&](const internal::DeviceArray<double>& v) {
+    auto extract = [&](const internal::DeviceArray<double>& v) {
       auto o = std::make_shared<internal::DeviceArray<double>>(size_t(P->nnz) + 1);
-      internal::check(hdd_gather_values(ctx_, v.get(), d_src.get(), P->nnz, o->get(), nullptr), "hdd_gather_values");
+      const double* in = v.get();
+      double* res = o->get();
+      internal::check(hdd_block_operator_values_device(ctx_, &pat, r0, r1, c * nb, d * nb, P->d_row_ptr.get(), &in, 1,
+                                                       &res, nullptr), "hdd_block_operator_values_device");
       return o;
     };
-    if (matrix_.affine) out.affine = gather(*matrix_.affine);
-    for (const auto& q : matrix_.comps) out.comps.push_back(gather(*q));
+    if (matrix_.affine) out.affine = extract(*matrix_.affine);
+    for (const auto& q : matrix_.comps) out.comps.push_back(extract(*q));
     internal::hip_check(hipDeviceSynchronize(), "get_operator_block");
     return out;
   }

@@ -36,7 +36,8 @@ class MeshT(C.Structure):
 
 class ScalarT(C.Structure):
     _fields_ = [("kind", C.c_int32), ("order", C.c_int32), ("c", C.c_double), ("b", C.c_double),
-                ("kx", C.c_double), ("ky", C.c_double), ("per_elem", C.c_void_p)]
+                ("kx", C.c_double), ("ky", C.c_double), ("per_elem", C.c_void_p), ("table", C.c_void_p),
+                ("n_table", C.c_int32), ("pad", C.c_int32)]
 
 
 class TensorT(C.Structure):
@@ -135,6 +136,16 @@ def indicator(points, boxes):
     return out
 
 
+def indicator_sum(points, boxes):
+    """The Spe10 channel at channel_boundary_layer = 0 (problems/spe10.hh:139-148): make_sum of one-box
+    Indicators, i.e. per entity the sum of the values of every closed box containing the entity centre."""
+    out = np.zeros(points.shape[0])
+    for lx, ly, ux, uy, v in np.asarray(boxes, np.float64).reshape(-1, 5):
+        m = (points[:, 0] >= lx) & (points[:, 0] <= ux) & (points[:, 1] >= ly) & (points[:, 1] <= uy)
+        out[m] += v
+    return out
+
+
 def spe10_channel_boxes():
     """The parametric SPE10 channel of testcases/spe10.hh:38-251 (105 boxes, channel_boundary_layer = 0, so
     Indicator functions: problems/spe10.hh:213-218) and the three force boxes (testcases/spe10.hh:31-37),
@@ -191,10 +202,24 @@ class Grid:
         return row_ptr, col
 
 
-def scalar(kind=FN_CONST, c=1.0, b=0.0, kx=0.0, ky=0.0, per_elem=None, order=0):
-    s = ScalarT(kind, order, c, b, kx, ky, _ptr(per_elem))
-    s._keep = per_elem
+def scalar(kind=FN_CONST, c=1.0, b=0.0, kx=0.0, ky=0.0, per_elem=None, order=0, table=None):
+    tab = None if table is None else np.ascontiguousarray(table, np.float64).reshape(-1, 7)
+    s = ScalarT(kind, order, c, b, kx, ky, _ptr(per_elem), _ptr(tab), 0 if tab is None else tab.shape[0], 0)
+    s._keep = (per_elem, tab)
     return s
+
+
+def flattop(boxes, c=0.0, b=1.0, order=3):
+    """c + b * sum of dune-stuff FlatTop functions (or_flattop; boxes [k][7] = lx, ly, ux, uy, dx, dy, value)."""
+    return scalar(FN_FLATTOP, c, b, order=order, table=boxes)
+
+
+def flattop_at(box, x, y):
+    L = lib()
+    L.or_flattop.restype = C.c_double
+    L.or_flattop.argtypes = [C.c_void_p, C.c_double, C.c_double]
+    b = np.ascontiguousarray(box, np.float64)
+    return L.or_flattop(_ptr(b), float(x), float(y))
 
 
 def tensor(kind=TENSOR_CONST, c=(1.0, 0.0, 1.0), per_elem=None):
@@ -396,6 +421,7 @@ def qp_esv2007_errors(grid, elem_index=None):
 # right-hand sides (SWIPDG::init() functionals, swipdg.hh:251-347)
 # ------------------------------------------------------------------------------------------------------
 FN_COS_PRODUCT = 3
+FN_FLATTOP = 4
 
 
 def esv2007_force(dim=2):

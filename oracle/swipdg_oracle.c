@@ -292,9 +292,41 @@ static void map_grad(const geom_t* G, const double* gh, double* gp)
 /* ------------------------------------------------------------------------------------------------ */
 /* Coefficient evaluation (dune-stuff local functions)                                               */
 /* ------------------------------------------------------------------------------------------------ */
+/* dune-stuff Functions::FlatTop (dune/stuff/functions/flattop.hh -- third-party, absent from /root/reference;
+ * restated from its published definition, the Brenner & Scott flat-top): per coordinate 1 on [l + d, u - d],
+ * 0 outside [l - d, u + d], and C^1 cubic transitions centred on the box faces,
+ *   (1 + t)^2 (1 - 2t),  t = (x - (l + d)) / 2d in [-1, 0)      (left layer)
+ *   (1 - t)^2 (1 + 2t),  t = (x - (u - d)) / 2d in [0, 1)       (right layer),
+ * times the box value.  The Spe10::Model1 channel is the sum of one FlatTop per channel box when
+ * channel_boundary_layer != 0 (problems/spe10.hh:139-148, 213-222).  Parity for it is unpinned. */
+static double flattop1(double x, double l, double u, double d)
+{
+  if (x < l - d) return 0.0;
+  if (x < l + d) {
+    const double t = (x - (l + d)) / (2.0 * d);
+    return (1.0 + t) * (1.0 + t) * (1.0 - 2.0 * t);
+  }
+  if (x < u - d) return 1.0;
+  if (x < u + d) {
+    const double t = (x - (u - d)) / (2.0 * d);
+    return (1.0 - t) * (1.0 - t) * (1.0 + 2.0 * t);
+  }
+  return 0.0;
+}
+
+double or_flattop(const double* r, double x, double y)
+{
+  return r[6] * flattop1(x, r[0], r[2], r[4]) * flattop1(y, r[1], r[3], r[5]);
+}
+
 static double eval_scalar(const or_scalar_t* s, int64_t e, const double* x)
 {
   switch (s->kind) {
+    case OR_FN_FLATTOP: {
+      double sum = 0.0;
+      for (int32_t k = 0; k < s->n_table; ++k) sum += or_flattop(s->table + 7 * k, x[0], x[1]);
+      return s->c + s->b * sum;
+    }
     case OR_FN_CONST: return s->c;
     case OR_FN_PER_ELEM: return s->per_elem[e];
     case OR_FN_SINUSOID: return s->c + s->b * sin(s->kx * x[0] + s->ky * x[1]);
@@ -317,7 +349,7 @@ static void eval_tensor(const or_tensor_t* t, int64_t e, double A[2][2])
 
 static int scalar_order(const or_scalar_t* s)
 {
-  return (s->kind == OR_FN_SINUSOID || s->kind == OR_FN_COS_PRODUCT) ? s->order : 0;
+  return (s->kind == OR_FN_SINUSOID || s->kind == OR_FN_COS_PRODUCT || s->kind == OR_FN_FLATTOP) ? s->order : 0;
 }
 static const int TENSOR_ORDER = 0;   /* all supported tensors are piecewise constant */
 

@@ -12,7 +12,7 @@ extern "C" {
 #endif
 
 enum { OR_SIMPLEX = 0, OR_CUBE = 1 };
-enum { OR_FN_CONST = 0, OR_FN_PER_ELEM = 1, OR_FN_SINUSOID = 2, OR_FN_COS_PRODUCT = 3 };
+enum { OR_FN_CONST = 0, OR_FN_PER_ELEM = 1, OR_FN_SINUSOID = 2, OR_FN_COS_PRODUCT = 3, OR_FN_FLATTOP = 4 };
 enum { OR_TENSOR_CONST = 0, OR_TENSOR_ISO_PER_ELEM = 1, OR_TENSOR_SYM_PER_ELEM = 2 };
 enum { OR_BOUNDARY_DIRICHLET = 0, OR_BOUNDARY_NEUMANN = 1 };
 
@@ -31,7 +31,13 @@ typedef struct {
   double c;                   /* constant value / sinusoid offset a */
   double b, kx, ky;           /* sinusoid: a + b*sin(kx*x + ky*y); cos product: a*cos(kx*x)*cos(ky*y)[*cos(b*z)] */
   const double* per_elem;     /* OR_FN_PER_ELEM: [n_elements] */
+  const double* table;        /* OR_FN_FLATTOP: [n_table][7] = lx, ly, ux, uy, layer_x, layer_y, value */
+  int32_t n_table;
+  int32_t pad;
 } or_scalar_t;
+
+/* dune-stuff FlatTop of one box (restated, see swipdg_oracle.c) at x: exposed for the CPU tests */
+double or_flattop(const double* box, double x, double y);
 
 typedef struct {
   int32_t kind;               /* OR_TENSOR_* */

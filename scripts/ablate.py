@@ -1,7 +1,9 @@
 """A/B timing of kernel ablations (HDD_DEBUG_FLAGS) in ONE process, interleaved rounds, several workloads
 side by side (one of them unchanged serves as the control for box-to-box clock differences).
-Flags (swipdg_persistent_kernel): 1 = skip compute, 2 = drop the value stores (range 0), 4 = skip the
-neighbour gathers, 8 = interleave the waves' store chunks, 16 = one wave per tile (RS = 1).
+Flags (swipdg_persistent_kernel, HDD_ABLATION builds: HDD_AMD_LIB=dune-hdd_amd/lib_ab/libhdd_abl.so): 1 = skip
+compute, 2 = drop the value stores (range 0), 4 = skip the neighbour gathers, 32 = each wave a contiguous block
+of its XCD's tiles, 64 = global round-robin tiles, 128 / 256 = half / all of a tile's stores before the next
+tile's gathers.
 usage: python scripts/ablate.py c2:0,1 c4:0,8,16 c3:0"""
 import os, sys, math
 import numpy as np

@@ -22,8 +22,8 @@
       the algorithmic ones: outputs written once + the element records read.
   ops BlockSWIPDG operator extraction (get_local_operator / get_coupling_operator, block-swipdg.hh:612-690)
       on the C4 layout (Q1, 8 x 8 subdomains; --n sets nx, default 3520): every local and every coupling
-      operator's values gathered from the assembled global matrix in one hdd_gather_values pass (maps
-      built once on the host by hdd_block_operator_map); bytes = 8 read + 8 index + 8 written per value.
+      operator extracted on the device from the assembled global matrix (hdd_block_operator_map_device +
+      hdd_block_operator_values_device), end to end; the round-2 host maps timed beside it.
 Prints one JSON line per config."""
 import argparse
 import json
@@ -156,44 +156,62 @@ def f(args):
 
 
 def ops(args):
+    """all local + coupling operators of the C4 layout: (i) the device path -- hdd_block_operator_map_device +
+    hdd_block_operator_values_device per operator from the device pattern, end to end (every launch, the nnz
+    read-back of each map included), and with the nnz known in advance (block_operator_nnz, one host pass per
+    mesh, timed separately): no synchronisation inside; (ii) the round-2 host maps (hdd_block_operator_map)
+    for comparison, timed once."""
     import torch
     import hdd_amd as H
     nx = args.n or 3520
     ny = nx * 1200 // 3520
     grid = H.Grid.structured(H.CUBE, nx, ny, (0, 0), (5, 1), px=8, py=8)
     loc = grid.local()
-    rp, col, _ = loc.pattern()
-    t0 = time.perf_counter()
-    srcs, n_ops = [], 0
-    for ss in range(64):
-        sx, sy = divmod(ss, 8)
-        for nn in [ss] + [(sx + dx) * 8 + sy + dy for dx, dy in ((-1, 0), (1, 0), (0, -1), (0, 1))
-                          if 0 <= sx + dx < 8 and 0 <= sy + dy < 8]:
-            nnz = H.C.c_int64()
-            H._check(H.lib().hdd_block_operator_map(grid.h, ss, nn, H._p(rp), H._p(col), None, None, None,
-                                                    H.C.byref(nnz)))
-            src = np.empty(nnz.value, np.int64)
-            ocol = np.empty(nnz.value, np.int32)
-            orp = np.empty(4 * grid.ne + 1, np.int64)   # upper bound of the operator's rows + 1
-            H._check(H.lib().hdd_block_operator_map(grid.h, ss, nn, H._p(rp), H._p(col), H._p(orp), H._p(ocol),
-                                                    H._p(src), H.C.byref(nnz)))
-            srcs.append(src)
-            n_ops += 1
-    t_map = time.perf_counter() - t0
-    src = torch.from_numpy(np.concatenate(srcs)).cuda()
     ctx = H.Context(0)
     dm, dp = H.DeviceMesh(loc), H.DevicePattern(loc)
     rng = np.random.default_rng(10)
     k = torch.from_numpy(loc.checkerboard((0, 0), (5, 1), 100, 20, 10.0 ** rng.uniform(-3, 3, 2000))).cuda()
     (vals,) = H.assemble(ctx, dm, dp, [H.scalar_fn(H.FN_CONST, 1.0)], H.tensor_fn(H.TENSOR_ISO_PER_ELEM, per_elem=k))
-    out = torch.empty(src.numel(), dtype=torch.float64, device="cuda")
-    s = torch.cuda.current_stream().cuda_stream
-    fn = lambda: H._check(H.lib().hdd_gather_values(ctx.h, H.C.c_void_p(vals.data_ptr()), H.C.c_void_p(src.data_ptr()),
-                                                    src.numel(), H.C.c_void_p(out.data_ptr()), H.C.c_void_p(s)))
-    t = timed(fn, args.steps, args.warmup)
-    n = src.numel()
-    return dict(config="ops_block_swipdg_q1_%dx%d_8x8" % (nx, ny), operators=n_ops, values=n, global_nnz=dp.nnz,
-                host_map_s=t_map, gather_ms=t * 1e3, gather_GBps=24 * n / t / 1e9)
+    pairs = []
+    for ss in range(64):
+        sx, sy = divmod(ss, 8)
+        pairs += [(ss, nn) for nn in [ss] + [(sx + dx) * 8 + sy + dy for dx, dy in ((-1, 0), (1, 0), (0, -1), (0, 1))
+                                             if 0 <= sx + dx < 8 and 0 <= sy + dy < 8]]
+    t0 = time.perf_counter()
+    nnz_of = H.block_operator_nnz(loc)
+    t_nnz = time.perf_counter() - t0
+
+    def run(known):
+        out = [H.block_operator(ctx, grid, dp, [vals], ss, nn, nnz=nnz_of[(ss, nn)] if known else None)
+               for ss, nn in pairs]
+        torch.cuda.synchronize()
+        return out
+
+    res = {}
+    for known in (False, True):
+        run(known)   # warm-up (allocator, scan scratch)
+        ts = []
+        for _ in range(max(3, args.steps // 4)):
+            t0 = time.perf_counter()
+            out = run(known)
+            ts.append(time.perf_counter() - t0)
+        res["device_ms_" + ("known_nnz" if known else "sync_nnz")] = float(np.median(ts)) * 1e3
+    n = sum(int(o[1].numel()) for o in out)
+    assert n == sum(nnz_of[p] for p in pairs)
+    rp, col, _ = dp.host
+    t0 = time.perf_counter()
+    for ss, nn in pairs:
+        c = H.C.c_int64()
+        H._check(H.lib().hdd_block_operator_map(grid.h, ss, nn, H._p(rp), H._p(col), None, None, None, H.C.byref(c)))
+        src = np.empty(c.value, np.int64)
+        ocol = np.empty(c.value, np.int32)
+        orp = np.empty(4 * grid.ne + 1, np.int64)
+        H._check(H.lib().hdd_block_operator_map(grid.h, ss, nn, H._p(rp), H._p(col), H._p(orp), H._p(ocol), H._p(src),
+                                                H.C.byref(c)))
+    t_host = time.perf_counter() - t0
+    return dict(config="ops_block_swipdg_q1_%dx%d_8x8" % (nx, ny), operators=len(pairs), values=n, global_nnz=dp.nnz,
+                nnz_host_pass_s=t_nnz, host_map_s=t_host, **res,
+                device_GBps_known_nnz=(8 + 8 + 4) * n / (res["device_ms_known_nnz"] * 1e-3) / 1e9)
 
 
 def c5(args):

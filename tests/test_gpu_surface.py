@@ -121,7 +121,8 @@ def test_cpp_reference_ctor_init_products(surface_run):
     assert "before init: The user has to call init() before calling any other method!" in out
     assert "no products: Do not call get_product() if available_products() is empty!" in out
     assert "bad level: level 5 not in [0, 2)" in out
-    assert "  [block] walking subdomains for the first time... done" in out
+    assert "  [block] walking subdomains for the first time (block pattern, built at construction)... done (took " in out
+    assert "  [block] walking subdomains for the second time... done (took " in out
     og = O.Grid(*O.kuhn_grid(16, 16, (-1, -1), (1, 1)))
     rp, col, val = O.assemble(og, O.scalar(), O.tensor(), O.params())
     assert np.array_equal(_ld(d, "lvl1_row_ptr", np.int64), rp)
@@ -169,7 +170,7 @@ def test_cpp_parametric_spe10(surface_run):
     og = O.Grid(et, c, ev)
     cen = O.element_centers(c, ev)
     ch, fo = O.spe10_channel_boxes()
-    chan = O.indicator(cen, ch)
+    chan = O.indicator_sum(cen, ch)     # make_sum of one-box Indicators (problems/spe10.hh:139-148)
     k_aff, k_1 = 1.0 + chan, chan
     perm = _ld(d, "spe10_perm")
     A = O.tensor(O.TENSOR_ISO_PER_ELEM, per_elem=O.checkerboard(cen, (0, 0), (5, 1), 100, 20, perm))
@@ -194,6 +195,27 @@ def test_cpp_parametric_spe10(surface_run):
     assert not _ld(d, "spe10_rhs_comp0").any()       # kappa_1 x (g_D = 0)
     _, _, e1 = O.product(og, O.PRODUCT_ELLIPTIC, kappa=pe(k_1), A=A)
     assert np.max(np.abs(_ld(d, "spe10_elliptic_comp0") - e1)) <= 1e-12 * np.max(np.abs(e1))
+
+
+@pytest.mark.gpu
+def test_cpp_spe10_flattop_channel(surface_run):
+    """Spe10Model1 with the reference's default channel_boundary_layer (problems/spe10.hh:86: FlatTop's
+    default, restated as 0.1): the channel is a sum of FlatTop functions (213-222) -- 1 + 0.9 channel, and the
+    parametric split 1 + channel / channel -- against the oracle's FlatTop restatement at 1e-12 (parity
+    unpinned: FlatTop is third-party)."""
+    r, d = surface_run
+    assert "spe10 flattop channel: components 1 order 3" in r.stdout
+    et, c, ev = O.kuhn_grid(100, 20, (0, 0), (5, 1))
+    og = O.Grid(et, c, ev)
+    cen = O.element_centers(c, ev)
+    ch, _ = O.spe10_channel_boxes()
+    boxes = np.column_stack([ch[:, :4], np.full((len(ch), 2), 0.1), ch[:, 4]])
+    A = O.tensor(O.TENSOR_ISO_PER_ELEM, per_elem=O.checkerboard(cen, (0, 0), (5, 1), 100, 20, _ld(d, "spe10_perm")))
+    for name, (cc, bb) in [("spe10ft_affine", (1.0, 0.9)), ("spe10ftp_affine", (1.0, 1.0)), ("spe10ftp_comp0", (0.0, 1.0))]:
+        rp, col, ref = O.assemble(og, O.flattop(boxes, cc, bb), A, O.params())
+        assert compare_rows(rp, _ld(d, name), ref, 1e-12)[1], name
+    # the layer matters: the FlatTop channel is not the Indicator channel
+    assert not np.allclose(_ld(d, "spe10ftp_comp0"), _ld(d, "spe10_comp0"))
 
 
 @pytest.mark.gpu
@@ -247,3 +269,63 @@ def test_cpp_block_oversampled_discretization(surface_run):
         assert compare_rows(rp, _ld(d, "os0_%s_affine" % bt), val, 1e-12)[1]
         b = O.rhs_swipdg(sg, force=O.esv2007_force(), prm=prm)
         assert np.max(np.abs(_ld(d, "os0_%s_rhs" % bt) - b)) <= 1e-12 * np.max(np.abs(b))
+
+
+def _checksum(t):
+    """sum_k bits[k] * (2k + 1) mod 2^64 over a device tensor (examples/surface_main.cpp: checksum)"""
+    import torch
+    bits = t.contiguous().view(torch.int64) if t.dtype == torch.float64 else t.to(torch.int64)
+    h, chunk = 0, 1 << 26
+    for k0 in range(0, bits.numel(), chunk):
+        b = bits[k0:k0 + chunk]
+        w = torch.arange(k0, k0 + b.numel(), device=b.device, dtype=torch.int64) * 2 + 1
+        h = (h + int((b * w).sum().item())) % (1 << 64)
+    return h
+
+
+def _big(which, *extra):
+    r = subprocess.run([EXE, "big", which, *extra], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    line = [l for l in r.stdout.splitlines() if l.startswith("big ")][-1]
+    f = line.split()
+    kv = {f[i]: f[i + 1] for i in range(2, len(f) - 1, 2)}
+    return kv
+
+
+@pytest.mark.gpu
+def test_cpp_full_size_c2_swipdg_device_pattern():
+    """The reference-signature SWIPDG (swipdg.hh:159-163) at the full C2 size (3200 x 640 Kuhn, SPE10 checkerboard
+    tensor): pattern built on the device, never downloaded; pattern and values bit-identical to the Python
+    front-end's device pattern + assembly (checksums of the bit patterns)."""
+    import torch
+    kv = _big("c2")
+    grid = H.Grid.structured(H.SIMPLEX, 3200, 640, (0, 0), (5, 1))
+    loc = grid.local()
+    perm = np.array([math.pow(10.0, -3.0 + 6.0 * math.fmod(0.618033988749895 * i, 1.0)) for i in range(2000)])
+    k = torch.from_numpy(loc.checkerboard((0, 0), (5, 1), 100, 20, perm)).cuda()
+    ctx = H.Context(0)
+    dm = H.DeviceMesh(loc)
+    dp = H.DevicePattern(loc, ctx=ctx, dmesh=dm, on_device=True)
+    (v,) = H.assemble(ctx, dm, dp, [H.scalar_fn(H.FN_CONST, 1.0)], H.tensor_fn(H.TENSOR_ISO_PER_ELEM, per_elem=k))
+    torch.cuda.synchronize()
+    assert int(kv["nnz"]) == dp.nnz == 147386880
+    assert int(kv["col_hash"]) == _checksum(dp.col)
+    assert int(kv["val_hash"]) == _checksum(v)
+
+
+@pytest.mark.gpu
+def test_cpp_full_size_hex_q3_swipdg_device_pattern():
+    """The same surface on ESV2007 3d, Q3 on 32^3 hexahedra (940 M nnz: the pattern exists only on the device)."""
+    import torch
+    n = 32
+    kv = _big("hex", str(n))
+    g = H.Grid.structured3d((n, n, n), (-1, -1, -1), (1, 1, 1), degree=3)
+    loc = g.local()
+    ctx = H.Context(0)
+    dm = H.DeviceMesh(loc)
+    dp = H.DevicePattern(loc, ctx=ctx, dmesh=dm, on_device=True)
+    (v,) = H.assemble(ctx, dm, dp, [H.scalar_fn(H.FN_CONST, 1.0)], H.tensor_fn(dim=3))
+    torch.cuda.synchronize()
+    assert int(kv["order"]) == 3 and int(kv["nnz"]) == dp.nnz
+    assert int(kv["col_hash"]) == _checksum(dp.col)
+    assert int(kv["val_hash"]) == _checksum(v)

@@ -194,10 +194,13 @@ def test_rccl_self_exchange():
 @pytest.mark.gpu
 def test_cpp_example_thread_ranks():
     """examples/sharded_main threads 3: ShardedBlockSWIPDG on 3 thread ranks (in-process mailbox transport)
-    == single-GPU BlockSWIPDG bit for bit, P1 and Q1, parametric SPE10 structure (2 components)."""
+    == single-GPU BlockSWIPDG bit for bit, P1 and Q1, parametric SPE10 structure (2 components), and diffusion-
+    factor parts of different integration orders (per-element affine part + sinusoid component: one sharded
+    call per order, the second without a halo exchange)."""
     r = subprocess.run([EXAMPLE, "threads", "3"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "sharded threads ok" in r.stdout, r.stdout
+    assert r.stdout.count("mismatches vs single-GPU BlockSWIPDG: 0") == 4, r.stdout
 
 
 @pytest.mark.gpu
