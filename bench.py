@@ -47,7 +47,7 @@ def parse():
     ap.add_argument("--ny", type=int, default=0, help="c2: 640; c4: 1200")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU work of the baseline sample")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r02", "traffic.json"),
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r03", "traffic.json"),
                     help="PMC traffic summary (scripts/traffic_summary.py); used only when its build_id matches the "
                          "timed libhdd_amd.so")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
@@ -274,14 +274,15 @@ def main():
         achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
         traffic, traffic_src = None, None
         bid = lib_build_id()
-        if os.path.exists(args.traffic_json):
+        if os.path.exists(args.traffic_json) and world == 1:
             try:
                 tj = json.load(open(args.traffic_json))
-                if (not c4 and world == 1 and tj.get("workload") == "spe10_swipdg_p1_kuhn_%dx%d" % (nx // world, ny)
-                        and tj.get("build_id") == bid):
-                    traffic = tj.get("hbm_bytes_per_launch")
+                wl = ("spe10_block_swipdg_q1_%dx%d_8x8_subdomains" % (nx, ny) if c4
+                      else "spe10_swipdg_p1_kuhn_%dx%d" % (nx, ny))
+                if tj.get("build_id") == bid and wl in tj.get("workloads", {}):
+                    traffic = tj["workloads"][wl]["hbm_bytes_per_launch"]
                     traffic_src = os.path.relpath(args.traffic_json, ROOT)
-            except (OSError, ValueError):
+            except (OSError, ValueError, KeyError):
                 traffic = None
         halo_desc = ""
         if world > 1 and args.halo == "once":
@@ -318,8 +319,12 @@ def main():
                         "parallelism": "block-swipdg strips x%d, owner-computes%s" % (world, halo_desc)
                         if world > 1 else "single GPU"}),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                         "build_id": bid,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         # the physical figure: HBM bytes the kernel really moves (PMC, same build) per second,
+                         # over the same peak -- below `frac` because the layout reads less than SURVEY 8(d) prices
+                         "traffic_frac": (traffic / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if traffic else None,
+                         "traffic_gbs": (traffic / (kernel_ms * 1e-3) / 1e9) if traffic else None,
+                         "traffic_source": traffic_src, "build_id": bid,
                          "kernel": "swipdg_persistent_kernel<%s<1, 0, false>, %s>"
                                    % ("Q1PwcPolicy" if c4 else "P1PwcPolicy", "true" if per_step else "false"),
                          "kernel_ms_avg": kernel_ms, "kernel_ms_avg_max_rank": kernel_ms_max,
@@ -327,11 +332,9 @@ def main():
                          # measured on this box in this run: device copy (read + write) and fill (write)
                          "attainable": dict(att, source="torch copy_ / fill_ of 1 GiB, HIP events"),
                          "frac_of_torch_copy": achieved / att["copy_gbs"],
-                         # the algorithmic count prices element-major coordinates (48 B per
-                         # triangle); the kernel reads the vertex-indexed geometry instead, so its measured HBM
-                         # traffic (PMC, same build) is below it -- the rate of that traffic:
-                         "traffic_gbs": (traffic / (kernel_ms * 1e-3) / 1e9) if traffic else None,
-                         "traffic_frac": (traffic / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if traffic else None},
+                         "frac_note": "frac = SURVEY 8(d) algorithmic bytes (element-major coordinates, 48 B per "
+                                      "triangle) / kernel time; traffic_frac = PMC-measured HBM bytes of this build "
+                                      "(the vertex-indexed layout reads less) / kernel time, the physical rate"},
             "cpu_baseline": cpu,
         }
         out["config"]["entry"] = "hdd_block_assemble_sharded (C ABI)"

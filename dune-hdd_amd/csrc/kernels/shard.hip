@@ -712,20 +712,40 @@ extern "C" int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm*
   h.buf = sh->d_sbuf;
   e = launch_halo(true, h, s);
   if (e != hipSuccess) return hip_fail(e, "hdd_block_assemble_sharded: pack");
-  // 2. post the exchange
-  std::vector<const double*> sp(size_t(h.n_peers));
-  std::vector<double*> rp(size_t(h.n_peers));
-  std::vector<int64_t> sn(size_t(h.n_peers)), rn(size_t(h.n_peers));
-  for (int k = 0; k < h.n_peers; ++k) {
-    sp[k] = sh->d_sbuf + int64_t(R) * sh->send_prefix[k];
-    sn[k] = int64_t(R) * (sh->send_prefix[k + 1] - sh->send_prefix[k]);
-    rp[k] = sh->d_rbuf + int64_t(R) * sh->recv_prefix[k];
-    rn[k] = int64_t(R) * (sh->recv_prefix[k + 1] - sh->recv_prefix[k]);
-  }
+  // 2. post the exchange.  The receives land straight in the ghost columns: the ghosts of one owner are
+  // contiguous (recv_col0), so peer k's message is R row messages [row r][count_k], each received into
+  // arr(r)[row(r) ld + recv_col0[k] ...] -- no receive buffer, no unpack launch.  Sender and receiver list the
+  // rows in the same order (the layout depends on the kinds only), which is how RCCL / the host transports
+  // match repeated (peer) messages.
   int rc = HDD_OK;
   if (transfer) {
-    rc = hdd_comm_post(comm, h.n_peers, sh->peers.data(), sp.data(), sn.data(), rp.data(), rn.data(), stream);
+    std::vector<int32_t> mp;
+    std::vector<const double*> ms;
+    std::vector<double*> mr;
+    std::vector<int64_t> mn, mrn;
+    for (int k = 0; k < h.n_peers; ++k) {
+      const int64_t scnt = sh->send_prefix[k + 1] - sh->send_prefix[k];
+      const int64_t rcnt = sh->recv_prefix[k + 1] - sh->recv_prefix[k];
+      for (int32_t r = 0, a = 0; r < R; ++r) {
+        while (a + 1 < h.n_arrays && h.row_first[a + 1] <= r) ++a;
+        mp.push_back(sh->peers[size_t(k)]);
+        ms.push_back(sh->d_sbuf + int64_t(R) * sh->send_prefix[k] + int64_t(r) * scnt);
+        mn.push_back(scnt);
+        mr.push_back(h.arr[a] + int64_t(r - h.row_first[a]) * h.ld + sh->recv_col0[k]);
+        mrn.push_back(rcnt);
+      }
+    }
+    rc = hdd_comm_post(comm, int32_t(mp.size()), mp.data(), ms.data(), mn.data(), mr.data(), mrn.data(), stream);
   } else {   // timing studies: the receive buffers get this rank's own messages (stream-ordered device copies)
+    std::vector<const double*> sp(size_t(h.n_peers));
+    std::vector<double*> rp(size_t(h.n_peers));
+    std::vector<int64_t> sn(size_t(h.n_peers)), rn(size_t(h.n_peers));
+    for (int k = 0; k < h.n_peers; ++k) {
+      sp[k] = sh->d_sbuf + int64_t(R) * sh->send_prefix[k];
+      sn[k] = int64_t(R) * (sh->send_prefix[k + 1] - sh->send_prefix[k]);
+      rp[k] = sh->d_rbuf + int64_t(R) * sh->recv_prefix[k];
+      rn[k] = int64_t(R) * (sh->recv_prefix[k + 1] - sh->recv_prefix[k]);
+    }
     for (int k = 0; k < h.n_peers && rc == HDD_OK; ++k) {
       const int64_t n = std::min(sn[k], rn[k]);
       if (n > 0 && hipMemcpyAsync(rp[k], sp[k], size_t(n) * sizeof(double), hipMemcpyDeviceToDevice, s) != hipSuccess)
@@ -744,15 +764,18 @@ extern "C" int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm*
       return rc;
     }
   }
-  // 4. ghost columns after the receives
-  if (transfer) rc = hdd_comm_wait(comm, stream);
-  if (rc) return rc;
-  for (int k = 0; k <= h.n_peers; ++k) h.prefix[k] = sh->recv_prefix[k];
-  for (int k = 0; k < h.n_peers; ++k) h.col0[k] = sh->recv_col0[k];
-  h.idx = nullptr;
-  h.buf = sh->d_rbuf;
-  e = launch_halo(false, h, s);
-  if (e != hipSuccess) return hip_fail(e, "hdd_block_assemble_sharded: unpack");
+  // 4. ghost columns after the receives (transfers receive in place; the loopback study unpacks)
+  if (transfer) {
+    rc = hdd_comm_wait(comm, stream);
+    if (rc) return rc;
+  } else {
+    for (int k = 0; k <= h.n_peers; ++k) h.prefix[k] = sh->recv_prefix[k];
+    for (int k = 0; k < h.n_peers; ++k) h.col0[k] = sh->recv_col0[k];
+    h.idx = nullptr;
+    h.buf = sh->d_rbuf;
+    e = launch_halo(false, h, s);
+    if (e != hipSuccess) return hip_fail(e, "hdd_block_assemble_sharded: unpack");
+  }
   // 5. the tiles that read a ghost (or everything without overlap)
   if (overlap)
     return hdd_swipdg_assemble_tiles(ctx, &m, kappa, n_comp, tensor, params, pattern, d_vals, sh->d_tiles_bd, sh->n_bd,

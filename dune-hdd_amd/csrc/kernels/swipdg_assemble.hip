@@ -9,6 +9,16 @@ namespace dev {
 // per-element, ...) -- the kinds are compile-time inside the kernels
 static hipError_t launch_components(const AssembleArgs& a, int nqv, int nqf, hipStream_t s, bool* supported)
 {
+  // C3: sinusoid components sharing one phase (OS2014's affine part and mu-component) -> one fused launch that
+  // evaluates the sines once per element (P1, vertex-indexed geometry; HDD_DEBUG_FLAGS bit 4096: per component)
+  if (a.elem_type == HDD_SIMPLEX && nqv == 6 && nqf == 3 && a.ev && a.n_comp > 1 &&
+      !(a.debug_flags & 4096)) {
+    bool same = true;
+    for (int c = 0; c < a.n_comp; ++c)
+      same = same && a.kappa[c].kind == HDD_FN_SINUSOID && a.kappa[c].kx == a.kappa[0].kx &&
+             a.kappa[c].ky == a.kappa[0].ky;
+    if (same) return launch_p1_smooth_fused(a, s);
+  }
   for (int c = 0; c < a.n_comp; ++c) {
     AssembleArgs ac = a;
     ac.n_comp = 1;
@@ -77,6 +87,7 @@ hipError_t launch_assemble(const AssembleArgs& a, int nqv, int nqf, hipStream_t 
     if (nqv == 1 && nqf == 2) return pwc ? launch_t<Simplex, 1, 2, true>(a, s) : launch_t<Simplex, 1, 2, false>(a, s);
     if (nqv == 6 && nqf == 3) return launch_t<Simplex, 6, 3, false>(a, s);
     if (nqv == 3 && nqf == 2) return launch_t<Simplex, 3, 2, false>(a, s);
+    if (nqv == 3 && nqf == 3) return launch_t<Simplex, 3, 3, false>(a, s);   // smooth kappa of order 2
   } else {
     if (nqv == 1 && nqf == 2) return launch_t<Cube, 1, 2, false>(a, s);
     if (nqv == 4 && nqf == 3) return launch_t<Cube, 4, 3, false>(a, s);

@@ -1344,12 +1344,28 @@ struct P1SmoothPolicy {
 
   __device__ static void compute(const AssembleArgs& a, int64_t e, const Own& o, const Gat& gt, double* img)
   {
-    using E = Simplex;
     const KappaArg& K = a.kappa[0];
     auto kap = [&](double x, double y) {
       if constexpr (KK == HDD_FN_FLATTOP) return flattop_sum(K.table, K.n_table, K.c, K.b, x, y);
       return K.c + K.b * sin_phase(K.kx * x + K.ky * y);
     };
+    const double j00 = o.X[1] - o.X[0], j01 = o.X[2] - o.X[0], j10 = o.Y[1] - o.Y[0], j11 = o.Y[2] - o.Y[0];
+    double kv = 0.0;   // sum_q w_q kappa(x_q), Dunavant 6
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+      const double xh = VolRule<Simplex, 6>::x(q), yh = VolRule<Simplex, 6>::y(q);
+      kv += VolRule<Simplex, 6>::w(q) * kap(o.X[0] + j00 * xh + j01 * yh, o.Y[0] + j10 * xh + j11 * yh);
+    }
+    emit(a, e, o, gt, img, kv, [&](int f, double x, double y, int) { return kap(x, y); });
+  }
+
+  // the entries from the volume moment kv = sum_q w_q kappa(x_q) and kappa at the face Gauss points,
+  // KF(f, x, y, q) (point q of face f at (x, y), from vertex a to b)
+  template <class KFace>
+  __device__ static void emit(const AssembleArgs& a, int64_t e, const Own& o, const Gat& gt, double* img, double kv,
+                              KFace KF)
+  {
+    using E = Simplex;
     const double j00 = o.X[1] - o.X[0], j01 = o.X[2] - o.X[0], j10 = o.Y[1] - o.Y[0], j11 = o.Y[2] - o.Y[0];
     const double det = j00 * j11 - j01 * j10;
     const double id = rcp_nr(det);
@@ -1380,12 +1396,6 @@ struct P1SmoothPolicy {
       pos[f] = p;
     }
     const int rowlen = nblk * 3;
-    double kv = 0.0;   // sum_q w_q kappa(x_q), Dunavant 6
-#pragma unroll
-    for (int q = 0; q < 6; ++q) {
-      const double xh = VolRule<Simplex, 6>::x(q), yh = VolRule<Simplex, 6>::y(q);
-      kv += VolRule<Simplex, 6>::w(q) * kap(o.X[0] + j00 * xh + j01 * yh, o.Y[0] + j10 * xh + j11 * yh);
-    }
     double S[3][3];
 #pragma unroll
     for (int i = 0; i < 3; ++i)
@@ -1413,7 +1423,7 @@ struct P1SmoothPolicy {
 #pragma unroll
       for (int q = 0; q < 3; ++q) {
         const double sq = Gauss01<3>::s(q), wq = Gauss01<3>::w(q) * len;
-        const double k = kap(Ax + sq * tx, Ay + sq * ty);
+        const double k = KF(f, Ax + sq * tx, Ay + sq * ty, q);
         const double kk = inner ? k * k : k;
         k1a += wq * k * (1.0 - sq);
         k1b += wq * k * sq;
@@ -1467,6 +1477,57 @@ struct P1SmoothPolicy {
     for (int i = 0; i < 3; ++i)
 #pragma unroll
       for (int j = 0; j < 3; ++j) img[i * rowlen + pos_self * 3 + j] = S[i][j];
+  }
+};
+
+// C3 fused: the affine part and the components of an OS2014-type diffusion factor share the phase of their
+// sinusoid (kappa_c = a_c + b_c sin(kx x + ky y), problems/OS2014.hh:63-76), so one launch evaluates the 15
+// sines of an element ONCE and emits every component from them: per tile, the sines (the volume sum
+// sum_q w_q sin and the 3 x 3 face values) stay in registers and the component loop of the persistent
+// driver builds each component's LDS image and streams it to that component's value array.  The mesh and
+// the gathers are read once instead of once per component.  Entries equal the per-component kernel's up to
+// rounding (kappa's volume sum is a_c sum w + b_c sum w sin instead of sum w (a_c + b_c sin)).
+template <int TK, bool VX = false>
+struct P1SmoothFusedPolicy : P1SmoothPolicy<TK, VX> {
+  using Base = P1SmoothPolicy<TK, VX>;
+  using Own = typename Base::Own;
+  using Gat = typename Base::Gat;
+  static constexpr bool FUSED = true;
+  struct Shared {
+    double sv, wv;        // sum_q w_q sin(phase(x_q)), sum_q w_q (Dunavant 6)
+    double sf[3][3];      // sin at the Gauss 3 points of every face
+  };
+  __device__ static void prepare(const AssembleArgs& a, const Own& o, Shared& sh)
+  {
+    using E = Simplex;
+    const KappaArg& K = a.kappa[0];   // the phase (kx, ky) every fused component shares
+    const double j00 = o.X[1] - o.X[0], j01 = o.X[2] - o.X[0], j10 = o.Y[1] - o.Y[0], j11 = o.Y[2] - o.Y[0];
+    sh.sv = 0.0;
+    sh.wv = 0.0;
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+      const double xh = VolRule<Simplex, 6>::x(q), yh = VolRule<Simplex, 6>::y(q);
+      const double x = o.X[0] + j00 * xh + j01 * yh, y = o.Y[0] + j10 * xh + j11 * yh;
+      sh.sv += VolRule<Simplex, 6>::w(q) * sin_phase(K.kx * x + K.ky * y);
+      sh.wv += VolRule<Simplex, 6>::w(q);
+    }
+#pragma unroll
+    for (int f = 0; f < 3; ++f) {
+      const int fa = E::fv(f, 0), fb = E::fv(f, 1);
+      const double Ax = o.X[fa], Ay = o.Y[fa], tx = o.X[fb] - Ax, ty = o.Y[fb] - Ay;
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const double sq = Gauss01<3>::s(q);
+        sh.sf[f][q] = sin_phase(K.kx * (Ax + sq * tx) + K.ky * (Ay + sq * ty));
+      }
+    }
+  }
+  __device__ static void emit_component(const AssembleArgs& a, int c, int64_t e, const Own& o, const Gat& gt,
+                                        const Shared& sh, double* img)
+  {
+    const KappaArg& K = a.kappa[c];
+    Base::emit(a, e, o, gt, img, K.c * sh.wv + K.b * sh.sv,
+               [&](int f, double, double, int q) { return K.c + K.b * sh.sf[f][q]; });
   }
 };
 
@@ -1631,10 +1692,22 @@ __device__ __forceinline__ int tile_offset(int c, bool active)
 // neighbour gathers of a tile are issued a whole compute phase before they are needed (the default issues
 // them right after the previous compute, and with one wave per SIMD -- Q1 tiles -- their L2 / MALL latency
 // is exposed at the next compute).  Costs the registers of one more tile of own data and gathers in flight.
+// FUSED policies emit several components per tile from one prepare() (P1SmoothFusedPolicy): the driver
+// builds and streams one LDS image per component (a.n_comp of them, into a.vals[c])
+template <class P, class = void>
+struct fused_of : std::false_type {
+  struct Shared {};
+};
+template <class P>
+struct fused_of<P, std::void_t<decltype(P::FUSED)>> : std::bool_constant<P::FUSED> {
+  using Shared = typename P::Shared;
+};
+
 template <class P, bool TL, bool DEEP = false>   // TL: tiles come from a.tile_list, else 0..n_tiles-1
 __global__ void __launch_bounds__(64, P::MINW)
 swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
 {
+  constexpr bool FUSED = fused_of<P>::value;
   constexpr int RB = P::RB;
   constexpr int IMG = 64 * RB;
   constexpr int STORES = (IMG / 2 + 63) / 64;
@@ -1709,6 +1782,7 @@ swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
   // on entry only the back edge counts, and that wait skips the stores (in-order vmcnt).
   __builtin_amdgcn_s_waitcnt(0);
   double* out = a.vals[0];
+  [[maybe_unused]] typename fused_of<P>::Shared shv;
   for (;;) {
     const bool has_next = t + t_step < t_end;
     const int64_t tn = has_next ? t + t_step : t;
@@ -1737,7 +1811,12 @@ swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
       if (!HDD_ABL(a, 1)) P::compute(a, e, own, gat, img);
     } else {
       double* img = active ? lds + off : scratch;
-      if (!HDD_ABL(a, 1)) P::compute(a, e, own, gat, img);
+      if constexpr (FUSED) {   // the shared part once, then component 0 (the others after its stores)
+        P::prepare(a, own, shv);
+        if (!HDD_ABL(a, 1)) P::emit_component(a, 0, e, own, gat, shv, img);
+      } else {
+        if (!HDD_ABL(a, 1)) P::compute(a, e, own, gat, img);
+      }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -1808,6 +1887,19 @@ swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
       if (!HDD_ABL(a, 4)) P::load_gat(a, en, own_n, gat_n);
     }
     stores(false);
+    if constexpr (FUSED) {   // the other components: same image slots, their own value arrays
+      for (int c = 1; c < a.n_comp; ++c) {
+        double* img = active ? lds + off : scratch;
+        if (!HDD_ABL(a, 1)) P::emit_component(a, c, e, own, gat, shv, img);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        out = a.vals[c];
+        rsrc = __builtin_amdgcn_make_buffer_rsrc(out + start, (short)0, nbytes, 0x00020000);
+        stores(false);
+      }
+      out = a.vals[0];
+    }
     // second gather stage of tile t+1 (vertex-indexed geometry: the neighbours' off-face vertices by the
     // ids the first stage brought): its wait covers the first stage only, which was issued before the
     // stores of tile t (vmcnt is in order), so it never waits for those stores
@@ -1871,11 +1963,14 @@ static hipError_t launch_persistent(const AssembleArgs& a, hipStream_t s)
   int wgcu = a.wgcu > 0 ? a.wgcu : P::WGCU;
   wgcu = std::max(1, std::min<int>(wgcu, int((160 * 1024) / lds)));   // resident by LDS (Q1 tiles: 3 per CU)
   const int64_t G = std::min<int64_t>(tiles, int64_t(cus) * wgcu);
-  for (int c = 0; c < a.n_comp; ++c) {
+  const int n_launch = fused_of<P>::value ? 1 : a.n_comp;   // a FUSED policy emits every component per tile
+  for (int c = 0; c < n_launch; ++c) {
     AssembleArgs ac = a;
-    ac.n_comp = 1;
-    ac.kappa[0] = a.kappa[c];
-    ac.vals[0] = a.vals[c];
+    if (!fused_of<P>::value) {
+      ac.n_comp = 1;
+      ac.kappa[0] = a.kappa[c];
+      ac.vals[0] = a.vals[c];
+    }
     const bool deep = P::DEEP_OK && (a.debug_flags & 2048);
     if (a.tile_list) {
       if (deep) hipLaunchKernelGGL((swipdg_persistent_kernel<P, true, P::DEEP_OK>), dim3(unsigned(G)), dim3(64), lds, s, ac, tiles);
@@ -1952,6 +2047,7 @@ template <int TK, int KK, bool VX> using P1Smooth3 = GenericPolicy<Simplex, 6, 3
 hipError_t launch_p1_pwc(const AssembleArgs& a, hipStream_t s);       // swipdg_p1.hip
 hipError_t launch_p1_smooth(const AssembleArgs& a, hipStream_t s);
 hipError_t launch_p1_penalty(const AssembleArgs& a, hipStream_t s);
+hipError_t launch_p1_smooth_fused(const AssembleArgs& a, hipStream_t s);   // all components in one launch
 hipError_t launch_q1_pwc(const AssembleArgs& a, hipStream_t s);       // swipdg_q1.hip
 hipError_t launch_q1_smooth(const AssembleArgs& a, hipStream_t s);
 hipError_t launch_q1_penalty(const AssembleArgs& a, hipStream_t s);

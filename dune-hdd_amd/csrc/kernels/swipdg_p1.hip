@@ -29,6 +29,13 @@ static hipError_t dispatch_smooth_p1(const AssembleArgs& a, hipStream_t s)
 
 hipError_t launch_p1_pwc(const AssembleArgs& a, hipStream_t s) { return dispatch_kinds<P1Pwc>(a, s, false); }
 hipError_t launch_p1_smooth(const AssembleArgs& a, hipStream_t s) { return dispatch_smooth_p1(a, s); }
+hipError_t launch_p1_smooth_fused(const AssembleArgs& a, hipStream_t s)
+{
+  const int tk = a.tkind;
+  if (tk == HDD_TENSOR_CONST) return launch_persistent<P1SmoothFusedPolicy<HDD_TENSOR_CONST, true>>(a, s);
+  if (tk == HDD_TENSOR_ISO_PER_ELEM) return launch_persistent<P1SmoothFusedPolicy<HDD_TENSOR_ISO_PER_ELEM, true>>(a, s);
+  return launch_persistent<P1SmoothFusedPolicy<HDD_TENSOR_SYM_PER_ELEM, true>>(a, s);
+}
 
 template <int TK, int KK> using P1Pen = P1PwcPolicy<TK, KK, true>;
 template <int TK, int KK> using P1PenVX = P1PwcPolicy<TK, KK, true, 1>;

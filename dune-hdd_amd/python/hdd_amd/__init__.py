@@ -467,8 +467,10 @@ def params_for(degree, dim, vol_order=-1, face_order=-1):
 
 class DeviceMesh:
     """Device copy of a LocalMesh (SoA arrays in HBM).  2d meshes also carry the vertex-indexed geometry
-    (elem_vertices, vertex_coords: what the P1 / Q1 stiffness kernels read) unless vertex_indexed=False or
-    zero_ghosts (ghost geometry then comes only from the halo exchange, into the element-major coords)."""
+    (elem_vertices, vertex_coords: what the P1 stiffness kernels read) unless vertex_indexed=False or
+    zero_ghosts (ghost geometry then comes only from the halo exchange, into the element-major coords).
+    Both representations must describe the same geometry: after changing `coords` in place (mesh motion,
+    caller-filled ghosts) call element_major_only(), so every kernel reads the updated coords."""
 
     def __init__(self, local, device=0, zero_ghosts=False, vertex_indexed=True):
         torch = _torch()
@@ -490,6 +492,13 @@ class DeviceMesh:
         self.t = MeshT(local.elem_type, local.degree, local.n_local, local.own_begin, local.own_end, self.coords.data_ptr(),
                        self.neighbors.data_ptr(), self.face_info.data_ptr(),
                        self.elem_vertices.data_ptr() if vx else None, self.vertex_coords.data_ptr() if vx else None)
+
+    def element_major_only(self):
+        """drop the vertex-indexed copies (hdd_mesh elem_vertices / vertex_coords = NULL)"""
+        self.elem_vertices = self.vertex_coords = None
+        self.t.elem_vertices = None
+        self.t.vertex_coords = None
+        return self
 
 
 class DevicePattern:

@@ -312,11 +312,14 @@ int main(int argc, char** argv)
     // the reference's default channel_boundary_layer (problems/spe10.hh:86, FlatTop's default): the channel is a
     // sum of FlatTop functions (213-222), evaluated at quadrature points; non-parametric 1 + 0.9 channel and
     // the parametric split
-    Discretizations::SWIPDG ft(provider, S::Grid::BoundaryInfos::AllDirichlet::default_config(),
+    // (on 97 x 21 squares: the 0.05-aligned channel boxes are narrower than two layers, so the FlatTop sum is
+    // discontinuous on lines y, x = 0.05 k; a mesh whose lines avoid them keeps every quadrature point off those)
+    S::Grid::Providers::Cube provider97(HDD_SIMPLEX, {0.0, 0.0}, {5.0, 1.0}, {97, 21});
+    Discretizations::SWIPDG ft(provider97, S::Grid::BoundaryInfos::AllDirichlet::default_config(),
                                Problems::Spe10Model1(perm, channel, forces, false));
     ft.init();
     dump(out + "/spe10ft_affine.bin", ft.system_matrix().affine_part());
-    Discretizations::SWIPDG ftp(provider, S::Grid::BoundaryInfos::AllDirichlet::default_config(),
+    Discretizations::SWIPDG ftp(provider97, S::Grid::BoundaryInfos::AllDirichlet::default_config(),
                                 Problems::Spe10Model1(perm, channel, forces, true));
     ftp.init();
     std::printf("spe10 flattop channel: components %d order %d\n", ftp.system_matrix().num_components(),

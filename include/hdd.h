@@ -206,7 +206,10 @@ typedef struct hdd_mesh_s {
    * P1 / Q1 stiffness kernels read each element's vertices through elem_vertices from vertex_coords and
    * the neighbour's off-face vertex through its vertex id, instead of the element-major coords (4 B per
    * element vertex instead of 16; the shared vertex rows stay cache resident).  coords stays required
-   * (right-hand sides, products, 3d, halo geometry). */
+   * (right-hand sides, products, 3d, halo geometry).  The two representations must describe the SAME
+   * geometry: a caller that moves the mesh or fills ghost coordinates itself must update vertex_coords too,
+   * or pass elem_vertices = vertex_coords = NULL (the sharded step does the latter with
+   * HDD_SHARD_HALO_GEOMETRY, whose ghost coordinates arrive in coords only). */
   const int32_t* elem_vertices;  /* [nvpe][n_local] */
   const double* vertex_coords;   /* [n_vertices][dim] */
 } hdd_mesh;
@@ -420,15 +423,17 @@ enum {
   HDD_SHARD_NO_OVERLAP = 1,     /* exchange, then assemble every tile (default: interior tiles overlap the halo) */
   HDD_SHARD_HALO_GEOMETRY = 2,  /* also send the ghost vertex coordinates (default: geometry is rank-local) */
   HDD_SHARD_NO_HALO = 4,        /* ghost columns already valid (static coefficients): no exchange at all */
-  HDD_SHARD_NO_TRANSFER = 8     /* timing studies only: pack, split tile launches and unpack as in an exchange,
-                                   but no transfer (comm may be NULL; the ghost columns receive the rank's own
-                                   send buffers, i.e. wrong values) -- the GPU-side cost of the sharded step */
+  HDD_SHARD_NO_TRANSFER = 8     /* timing studies only: pack and split tile launches as in an exchange, a
+                                   loopback copy + unpack kernel instead of the transfer (comm may be NULL; the
+                                   ghost columns receive the rank's own send buffers, i.e. wrong values) -- an
+                                   upper bound of the GPU-side cost of the sharded step */
 };
 /* One sharded assembly step -- the LHS of BlockSWIPDG::init() for the owned subdomains: pack the halo
  * records (per-element tensor / kappa rows, [+ coordinates]) of the elements the peers need -> post the
- * exchange -> interior tiles -> wait -> unpack into the ghost columns -> halo-boundary tiles.  The
- * per-element arrays of `kappa` / `tensor` must span n_local columns: their owned columns are read and
- * their GHOST COLUMNS ARE WRITTEN by the unpack.  comm may be NULL when the shard has no peers. */
+ * exchange, one message per (peer, halo row), received straight into the ghost columns (the ghosts of one
+ * owner are contiguous, recv_col0) -> interior tiles -> wait -> halo-boundary tiles.  The per-element arrays
+ * of `kappa` / `tensor` must span n_local columns: their owned columns are read and their GHOST COLUMNS ARE
+ * WRITTEN by the receives.  comm may be NULL when the shard has no peers. */
 int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm* comm, const hdd_scalar_fn* kappa,
                                int32_t n_comp, const hdd_tensor_fn* tensor, const hdd_swipdg_params* params,
                                const hdd_csr* pattern, double* const* d_vals, uint32_t flags, void* stream);

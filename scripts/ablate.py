@@ -19,7 +19,8 @@ def workload(cfg, ctx):
     if cfg == "c3":
         grid = H.Grid.structured(H.SIMPLEX, 1024, 1024, (-1, -1), (1, 1))
         local = grid.local()
-        kap = [H.scalar_fn(H.FN_SINUSOID, 1.0, 0.75, 4 * math.pi, 2 * math.pi, order=3)]
+        kap = [H.scalar_fn(H.FN_SINUSOID, 1.0, 0.75, 4 * math.pi, 2 * math.pi, order=3),   # OS2014 affine part
+               H.scalar_fn(H.FN_SINUSOID, 0.0, -0.75, 4 * math.pi, 2 * math.pi, order=3)]  # and mu-component
         ten = H.tensor_fn()
     else:
         et, nx, ny, p = (H.SIMPLEX, 3200, 640, 1) if cfg == "c2" else (H.CUBE, 3520, 1200, 8)
@@ -30,7 +31,7 @@ def workload(cfg, ctx):
         ten = H.tensor_fn(H.TENSOR_ISO_PER_ELEM, per_elem=k)
     dm = H.DeviceMesh(local)
     dp = H.DevicePattern(local)
-    vals = [torch.empty(dp.nnz, dtype=torch.float64, device="cuda")]
+    vals = [torch.empty(dp.nnz, dtype=torch.float64, device="cuda") for _ in kap]
     return lambda: H.assemble(ctx, dm, dp, kap, ten, vals=vals)
 
 

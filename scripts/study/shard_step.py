@@ -1,11 +1,15 @@
-"""GPU-side cost of the sharded C2 step on one card (what the N-GPU bench adds per rank on top
-of the assembly): rank r of an N-strip C2 weak-scaling decomposition (bench.py's layout: (3200 N) x 640 Kuhn
-squares), timed as
-  (a) NO_HALO       -- the whole owned range in one launch (ghost columns valid): the N = 1 step,
+"""GPU-side cost of the sharded step on one card (what the N-GPU bench adds per rank on top of
+the assembly), for rank r of an N-rank decomposition of
+  c2  bench.py's weak-scaling layout: (3200 N) x 640 Kuhn squares, one strip per rank;
+  c4  BASELINE's 8-GPU config: 3520 x 1200 Q1 quads, 8 x 8 subdomains, column strips of subdomains (strong
+      scaling: N = 8 gives each rank 440 x 1200 elements),
+timed as
+  (a) NO_HALO       -- the whole owned range in one launch (ghost columns valid): the kernel alone,
   (b) step          -- pack, loopback copy instead of the transfer (HDD_SHARD_NO_TRANSFER), interior tiles,
                        unpack, halo-boundary tiles: every launch of the real step, RCCL excluded,
-  (c) serial step   -- the same without the overlap split (one launch of all tiles after the unpack).
-usage: python scripts/study/shard_step.py [N ...]"""
+  (c) serial step   -- the same without the overlap split (one launch of all tiles after the unpack),
+  (d) step, graph   -- (b) captured once into a hipGraph (torch.cuda.CUDAGraph) and replayed.
+usage: python scripts/study/shard_step.py [c2|c4] [N ...]"""
 import os, sys
 import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -29,14 +33,24 @@ def timeit(fn, reps=50, rounds=4):
     return float(np.median(out)), float(np.min(out))
 
 
+def layout(workload, n):
+    if workload == "c4":
+        grid = H.Grid.structured(H.CUBE, 3520, 1200, (0.0, 0.0), (5.0, 1.0), px=8, py=8)
+        return grid, (0.0, 0.0), (5.0, 1.0), 100, 20, 2000
+    grid = H.Grid.structured(H.SIMPLEX, 3200 * n, 640, (0.0, 0.0), (5.0 * n, 1.0), px=n, py=1)
+    return grid, (0.0, 0.0), (5.0 * n, 1.0), 100 * n, 20, 2000 * n
+
+
 def main():
+    args = sys.argv[1:]
+    workload = args.pop(0) if args and args[0] in ("c2", "c4") else "c2"
     ctx = H.Context(0)
-    for n in [int(a) for a in sys.argv[1:]] or [2, 8]:
-        grid = H.Grid.structured(H.SIMPLEX, 3200 * n, 640, (0.0, 0.0), (5.0 * n, 1.0), px=n, py=1)
-        perm = 10.0 ** np.random.default_rng(10).uniform(-3.0, 3.0, size=100 * n * 20)
+    for n in [int(a) for a in args] or [2, 8]:
+        grid, lo, up, ncx, ncy, ncell = layout(workload, n)
+        perm = 10.0 ** np.random.default_rng(10).uniform(-3.0, 3.0, size=ncell)
         for rank in sorted({0, n // 2}):
             sh = H.Shard(ctx, grid, n, rank)
-            k = torch.from_numpy(sh.checkerboard((0.0, 0.0), (5.0 * n, 1.0), 100 * n, 20, perm)).cuda()
+            k = torch.from_numpy(sh.checkerboard(lo, up, ncx, ncy, perm)).cuda()
             _, _, _, pat = sh.pattern(ctx, 0)
             vals = [torch.empty(sh.info.nnz, dtype=torch.float64, device="cuda")]
             kap = [H.scalar_fn(H.FN_CONST, 1.0)]
@@ -48,12 +62,28 @@ def main():
             }
             res = {name: timeit(lambda f=f: H.assemble_sharded(ctx, sh, None, kap, ten, pat, vals, flags=f))
                    for name, f in runs.items()}
+            # (d) the step captured into a graph (side stream: capture needs a non-default stream)
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):
+                for _ in range(3):
+                    H.assemble_sharded(ctx, sh, None, kap, ten, pat, vals, flags=H.SHARD_NO_TRANSFER,
+                                       stream=s.cuda_stream)
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            try:
+                with torch.cuda.graph(g, stream=s):
+                    H.assemble_sharded(ctx, sh, None, kap, ten, pat, vals, flags=H.SHARD_NO_TRANSFER,
+                                       stream=s.cuda_stream)
+                res["d step, no transfer, hipGraph"] = timeit(g.replay)
+            except Exception as e:   # report, keep the other numbers
+                print("  graph capture failed: %s" % e)
             i = sh.info
-            print("N=%d rank %d: %d owned, %d ghosts, tiles %d interior + %d boundary, halo %d/%d elements"
-                  % (n, rank, sh.n_own, i.n_ghost, i.n_tiles_interior, i.n_tiles_boundary, i.halo_send, i.halo_recv))
+            print("%s N=%d rank %d: %d owned, %d ghosts, tiles %d interior + %d boundary, halo %d/%d elements"
+                  % (workload, n, rank, sh.n_own, i.n_ghost, i.n_tiles_interior, i.n_tiles_boundary, i.halo_send,
+                     i.halo_recv))
             base = res["a NO_HALO (one launch)"][0]
             for name, (med, mn) in res.items():
-                print("  %-28s median %.4f ms  min %.4f ms  (%+.1f %%)" % (name, med, mn, 100 * (med / base - 1)),
+                print("  %-32s median %.4f ms  min %.4f ms  (%+.1f %%)" % (name, med, mn, 100 * (med / base - 1)),
                       flush=True)
             del sh
 

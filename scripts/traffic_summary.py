@@ -30,16 +30,22 @@ for k, v in f.items():
 for k, v in w.items():
     if k.startswith("wr8"): cal["write_8B_lane"] = cal_bytes / (med(v) * KB)
     elif k.startswith("wr("): cal["write_16B_lane"] = cal_bytes / (med(v) * KB)
-bf = per_kernel(os.path.join(src, "bench_FETCH_SIZE", "run_counter_collection.csv"), "FETCH_SIZE")
-bw = per_kernel(os.path.join(src, "bench_WRITE_SIZE", "run_counter_collection.csv"), "WRITE_SIZE")
-kname = [k for k in bf if "swipdg" in k][0]
-fetch_kb, write_kb = med(bf[kname]), med([v for k, vs in bw.items() if "swipdg" in k for v in vs])
-# the kernel's reads are 8-byte lanes (coalesced SoA) + gathers; its writes are 16-byte lanes
-read_bytes = fetch_kb * KB * cal.get("read_8B_lane", 2.0)
-write_bytes = write_kb * KB * cal.get("write_16B_lane", 1.0)
-out = dict(workload="spe10_swipdg_p1_kuhn_3200x640", build_id=build_id, kernel=kname, fetch_size_kb=fetch_kb, write_size_kb=write_kb,
-           calibration_factors=cal, read_bytes=read_bytes, write_bytes=write_bytes,
-           hbm_bytes_per_launch=read_bytes + write_bytes,
+def kernel_traffic(prefix):
+    bf = per_kernel(os.path.join(src, prefix + "_FETCH_SIZE", "run_counter_collection.csv"), "FETCH_SIZE")
+    bw = per_kernel(os.path.join(src, prefix + "_WRITE_SIZE", "run_counter_collection.csv"), "WRITE_SIZE")
+    kname = [k for k in bf if "swipdg_persistent" in k][0]
+    fetch_kb, write_kb = med(bf[kname]), med([v for k, vs in bw.items() if "swipdg_persistent" in k for v in vs])
+    # the kernel's reads are 8-byte lanes (coalesced SoA) + gathers; its writes are 16-byte lanes
+    read_bytes = fetch_kb * KB * cal.get("read_8B_lane", 2.0)
+    write_bytes = write_kb * KB * cal.get("write_16B_lane", 1.0)
+    return dict(kernel=kname, fetch_size_kb=fetch_kb, write_size_kb=write_kb, read_bytes=read_bytes,
+                write_bytes=write_bytes, hbm_bytes_per_launch=read_bytes + write_bytes)
+
+
+workloads = {"spe10_swipdg_p1_kuhn_3200x640": kernel_traffic("bench")}
+if os.path.exists(os.path.join(src, "c4_FETCH_SIZE")):
+    workloads["spe10_block_swipdg_q1_3520x1200_8x8_subdomains"] = kernel_traffic("c4")
+out = dict(build_id=build_id, calibration_factors=cal, workloads=workloads,
            note="FETCH_SIZE/WRITE_SIZE medians over the profiled launches; factors = known bytes / counter "
                 "bytes measured on stream.hip kernels of the same lane width")
 os.makedirs(os.path.join(ROOT, "profiles", tag), exist_ok=True)

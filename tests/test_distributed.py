@@ -1,12 +1,13 @@
-"""Sharded (block-SWIPDG strip) assembly: world_size-2 process groups.
+"""Sharded (block-SWIPDG strip) assembly: world_size-2/3 process groups.
 
-CPU (gloo): the halo plan + exchange protocol of hdd_amd.halo.HaloExchange fills every ghost column with the
-owner's element record (pack / unpack emulated with torch indexing on CPU tensors -- test plumbing only;
-the product packs with the HIP hdd_soa_gather / hdd_soa_scatter kernels).
+CPU (gloo): host-only C++ shards (hdd_shard_create without a context): exchanging a per-element field
+through their halo plan fills every ghost column with the owner's value; the plans agree pairwise; the gloo
+host transport of hdd_amd.halo (several messages per peer, one per halo row) delivers them in order.
 
-GPU: two ranks share cuda:0 (gloo with host staging, since RCCL needs one GPU per rank); ghosts are zeroed
-on the device and arrive only through the exchange; each rank assembles its own rows with the HIP kernel;
-the concatenated rows equal the oracle's global block-SWIPDG matrix.
+GPU: two ranks share cuda:0 (the gloo host transport, since RCCL needs one GPU per rank); each runs the C++
+sharded step (hdd_block_assemble_sharded: pack -> exchange straight into the ghost columns -> interior /
+boundary tiles); ghost coefficients start as NaN and arrive only through the exchange; the concatenated rows
+equal the oracle's global block-SWIPDG matrix.
 """
 import os
 import socket
@@ -36,55 +37,36 @@ def _setup_paths():
 GRID = dict(nx=24, ny=8, lower=(0.0, 0.0), upper=(4.0, 1.0))
 
 
-def _cpu_worker(rank, world, port, outdir):
+def _transport_worker(rank, world, port, outdir):
+    """the gloo host transport with repeated peers: messages to one peer arrive in posting order"""
     _setup_paths()
-    import torch
     import torch.distributed as dist
-
-    import hdd_amd as H
-    from hdd_amd.halo import HaloExchange, strip_owner
+    from hdd_amd.halo import gloo_host_comm
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-
-    class HostHalo(HaloExchange):   # test plumbing: CPU pack/unpack
-        def pack(self, p):
-            rows = torch.cat([a.view(-1, self.ld) for a in self.arrays])
-            p["sbuf"].copy_(rows[:, p["idx"].long()])
-
-        def unpack(self, p):
-            r0 = 0
-            for a, nr in zip(self.arrays, self.rows):
-                a.view(nr, self.ld)[:, p["off"]:p["off"] + p["n_recv"]] = p["rbuf"][r0:r0 + nr]
-                r0 += nr
-
-    g = H.Grid.structured(H.SIMPLEX, GRID["nx"], GRID["ny"], GRID["lower"], GRID["upper"], px=world * 2, py=1)
-    owner = strip_owner(g.n_sub, world)
-    s0 = int(np.where(owner == rank)[0][0])
-    s1 = int(np.where(owner == rank)[0][-1]) + 1
-    loc = g.local(s0, s1)
-    truth_c = loc.coords.copy()
-    truth_k = loc.global_id.astype(np.float64) * 0.5 + 1.0
-    coords = torch.from_numpy(truth_c.copy())
-    kk = torch.from_numpy(truth_k.copy())
-    for a in (coords, kk.view(1, -1)):
-        a[:, :loc.own_begin] = 0
-        a[:, loc.own_end:] = 0
-    halo = HostHalo(None, loc, [(coords, coords.shape[0]), (kk.view(1, -1), 1)], owner, rank)
-    halo.exchange()
-    ok = np.array_equal(coords.numpy(), truth_c) and np.array_equal(kk.numpy(), truth_k)
-    np.save(os.path.join(outdir, "ok_%d.npy" % rank), np.array([ok, loc.n_ghost > 0]))
+    comm = gloo_host_comm(0)
+    cb = comm._keep   # the ctypes callback the C++ step calls; drive the Python side directly
+    peer = 1 - rank
+    sends = [np.arange(n, dtype=np.float64) + 100 * rank + 10 * k for k, n in enumerate((3, 0, 5))]
+    recvs = [np.empty(n) for n in (3, 0, 5)]
+    import ctypes as C
+    sp = (C.c_void_p * 3)(*[s_.ctypes.data if s_.size else None for s_ in sends])
+    rp = (C.c_void_p * 3)(*[r_.ctypes.data if r_.size else None for r_ in recvs])
+    cnt = (C.c_int64 * 3)(3, 0, 5)
+    rc = cb(None, 3, (C.c_int32 * 3)(peer, peer, peer), sp, cnt, rp, cnt)
+    ok = rc == 0 and all(np.array_equal(r_, np.arange(len(r_)) + 100 * peer + 10 * k) for k, r_ in enumerate(recvs))
+    np.save(os.path.join(outdir, "ok_%d.npy" % rank), np.array([ok]))
     dist.destroy_process_group()
 
 
-def test_gloo_halo_exchange_cpu():
+def test_gloo_host_transport_repeated_peers_cpu():
     import torch.multiprocessing as mp
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_cpu_worker, args=(2, _free_port(), d), nprocs=2, join=True)
+        mp.spawn(_transport_worker, args=(2, _free_port(), d), nprocs=2, join=True)
         for r in range(2):
-            ok, has_ghosts = np.load(os.path.join(d, "ok_%d.npy" % r))
-            assert ok and has_ghosts
+            assert np.load(os.path.join(d, "ok_%d.npy" % r))[0]
 
 
 def _shard_worker(rank, world, port, outdir, case):
@@ -203,7 +185,7 @@ def _gpu_worker(rank, world, port, outdir):
 
     import hdd_amd as H
     import oracle as O
-    from hdd_amd.halo import HaloExchange, strip_owner
+    from hdd_amd.halo import gloo_host_comm
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -211,29 +193,21 @@ def _gpu_worker(rank, world, port, outdir):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     perm = O.spe10_synthetic_permeability()
     g = H.Grid.structured(H.SIMPLEX, GRID["nx"], GRID["ny"], GRID["lower"], GRID["upper"], px=world * 2, py=1)
-    owner = strip_owner(g.n_sub, world)
-    s0 = int(np.where(owner == rank)[0][0])
-    s1 = int(np.where(owner == rank)[0][-1]) + 1
-    loc = g.local(s0, s1)
-    kcell = torch.from_numpy(loc.checkerboard(GRID["lower"], GRID["upper"], 100, 20, perm)).cuda()
-    kcell[:loc.own_begin] = 0
-    kcell[loc.own_end:] = 0
     ctx = H.Context(0)
-    dm = H.DeviceMesh(loc, 0, zero_ghosts=True)
-    dp = H.DevicePattern(loc, 0)
-    halo = HaloExchange(ctx, loc, [(dm.coords, dm.coords.shape[0]), (kcell.view(1, -1), 1)], owner, rank,
-                        host_staging=True)
-    # the bench's overlapped step: interior tiles before the halo lands, halo-dependent tiles after
-    t_in, t_bd = H.halo_tiles(loc)
-    kap, ten = [H.scalar_fn(H.FN_CONST, 1.0)], H.tensor_fn(H.TENSOR_ISO_PER_ELEM, per_elem=kcell)
-    val = torch.full((dp.nnz,), float("nan"), dtype=torch.float64, device="cuda")
-    halo.start()
-    H.assemble_tiles(ctx, dm, dp, kap, ten, torch.from_numpy(t_in).cuda(), [val])
-    halo.finish()
-    H.assemble_tiles(ctx, dm, dp, kap, ten, torch.from_numpy(t_bd).cuda(), [val])
+    sh = H.Shard(ctx, g, world, rank)
+    kcell = sh.checkerboard(GRID["lower"], GRID["upper"], 100, 20, perm)
+    kcell[:sh.own_begin] = np.nan          # ghost coefficients arrive only through the exchange
+    kcell[sh.own_end:] = np.nan
+    kdev = torch.from_numpy(kcell).cuda()
+    _, _, _, pat = sh.pattern(ctx, 0)
+    comm = gloo_host_comm(0)
+    kap, ten = [H.scalar_fn(H.FN_CONST, 1.0)], H.tensor_fn(H.TENSOR_ISO_PER_ELEM, per_elem=kdev)
+    val = torch.full((sh.info.nnz,), float("nan"), dtype=torch.float64, device="cuda")
+    H.assemble_sharded(ctx, sh, comm, kap, ten, pat, [val])   # overlapped: interior tiles, halo, boundary tiles
     torch.cuda.synchronize()
     np.save(os.path.join(outdir, "val_%d.npy" % rank), val.cpu().numpy())
-    np.save(os.path.join(outdir, "rng_%d.npy" % rank), np.array(g.subdomain_range(s0, s1)))
+    np.save(os.path.join(outdir, "rng_%d.npy" % rank), np.array(g.subdomain_range(sh.info.s_begin, sh.info.s_end)))
+    np.save(os.path.join(outdir, "ghost_%d.npy" % rank), kdev.cpu().numpy())
     dist.destroy_process_group()
 
 
@@ -249,6 +223,8 @@ def test_two_ranks_one_gpu_match_global_oracle():
         mp.spawn(_gpu_worker, args=(2, _free_port(), d), nprocs=2, join=True)
         vals = [np.load(os.path.join(d, "val_%d.npy" % r)) for r in range(2)]
         rngs = [np.load(os.path.join(d, "rng_%d.npy" % r)) for r in range(2)]
+        ghosts = [np.load(os.path.join(d, "ghost_%d.npy" % r)) for r in range(2)]
+    assert all(np.isfinite(gh).all() for gh in ghosts)   # every ghost column was received
     g = H.Grid.structured(H.SIMPLEX, GRID["nx"], GRID["ny"], GRID["lower"], GRID["upper"], px=4, py=1)
     pc, pev, psd = g.connectivity()
     ot, oc, oev = O.kuhn_grid(GRID["nx"], GRID["ny"], GRID["lower"], GRID["upper"])

@@ -13,11 +13,15 @@ H = pytest.importorskip("hdd_amd")
 pytestmark = pytest.mark.gpu
 
 RTOL = 1e-12
+FLOOR = 1e-10   # rows of a vanishing coefficient near a support edge: see cases.compare_rows
 
 
 def _boxes(layer=(0.1, 0.1)):
-    """channel-like boxes on the SPE10 domain: two overlapping, one thin, one touching the boundary"""
-    b = [(0.5, 0.2, 1.6, 0.35, 0.7), (1.2, 0.25, 2.0, 0.6, 0.4), (2.5, 0.5, 4.0, 0.56, 1.0),
+    """channel-like boxes on the SPE10 domain: two overlapping, one thin, one touching the boundary.
+    A box narrower than two layers has overlapping transitions, and FlatTop is then discontinuous at l + d
+    (the left transition ends at 1, the right one is already running); a quadrature point exactly there takes
+    either side by rounding -- in the reference as here -- so those lines are kept off the meshes' lines."""
+    b = [(0.5, 0.21, 1.6, 0.36, 0.7), (1.2, 0.25, 2.0, 0.6, 0.4), (2.5, 0.51, 4.0, 0.57, 1.0),
          (4.3, 0.0, 5.0, 0.3, 0.25)]
     return np.array([(lx, ly, ux, uy, layer[0], layer[1], v) for (lx, ly, ux, uy, v) in b])
 
@@ -47,7 +51,7 @@ def test_flattop_channel_components(ctx, et, vx):
     for (c, b), v in zip([(1.0, 1.0), (0.0, 1.0)], vals):
         rp, col, ref = O.assemble(og, O.flattop(boxes, c, b), A, O.params())
         assert np.array_equal(dp.host[1], col)
-        worst, ok = compare_rows(rp, v.cpu().numpy(), ref, RTOL)
+        worst, ok = compare_rows(rp, v.cpu().numpy(), ref, RTOL, FLOOR)
         assert ok, (c, b, worst)
     # the channel is really there: the component is nonzero on a good part of the rows, zero elsewhere
     v1 = vals[1].cpu().numpy()
@@ -67,7 +71,7 @@ def test_flattop_layers_and_order(ctx):
         (v,) = H.assemble(ctx, dm, dp, [H.flattop_fn(boxes, 1.0, 0.9, order=order)], H.tensor_fn())
         torch.cuda.synchronize()
         rp, col, ref = O.assemble(og, O.flattop(boxes, 1.0, 0.9, order=order), O.tensor(), O.params())
-        worst, ok = compare_rows(rp, v.cpu().numpy(), ref, RTOL)
+        worst, ok = compare_rows(rp, v.cpu().numpy(), ref, RTOL, FLOOR)
         assert ok, (order, worst)
 
 
@@ -94,7 +98,7 @@ def test_flattop_rhs_and_products(ctx, et):
         val = H.product(ctx, dm, kind, dp, kappa=kap, tensor=H.tensor_fn(), prm=H.params())
         torch.cuda.synchronize()
         rp, col, oval = O.product(og, kind, kappa=okap, A=O.tensor(), prm=O.params())
-        worst, ok = compare_rows(rp, val.cpu().numpy(), oval, RTOL)
+        worst, ok = compare_rows(rp, val.cpu().numpy(), oval, RTOL, FLOOR)
         assert ok, (kind, worst)
 
 
