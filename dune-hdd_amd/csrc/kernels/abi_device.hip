@@ -233,7 +233,8 @@ static int assemble_hex(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_fn* ka
 
 static int assemble_impl(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_fn* kappa, int32_t n_comp,
                          const hdd_tensor_fn* tensor, const hdd_swipdg_params* p, const hdd_csr* pattern,
-                         double* const* d_vals, const int32_t* d_tiles, int64_t n_tiles, void* stream)
+                         double* const* d_vals, const int32_t* d_tiles, int64_t n_tiles, void* stream,
+                         bool list_elements = false)
 {
   using namespace hdd::dev;
   if (!ctx || !m || !kappa || !tensor || !p || !pattern || !d_vals)
@@ -249,7 +250,7 @@ static int assemble_impl(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_fn* k
   if (m->n_local >= int64_t(INT32_MAX))
     return set_error(HDD_ERR_RANGE, "hdd_swipdg_assemble: n_local must fit int32 neighbour ids");
   if (m->elem_type == HDD_HEX) {
-    if (d_tiles) return set_error(HDD_ERR_UNSUPPORTED, "hdd_swipdg_assemble_tiles: no tile lists for HDD_HEX");
+    if (d_tiles) return set_error(HDD_ERR_UNSUPPORTED, "hdd_swipdg_assemble_tiles: no tile / element lists for HDD_HEX");
     return assemble_hex(ctx, m, kappa, n_comp, tensor, p, pattern, d_vals, stream);
   }
   if (m->degree > 1)
@@ -284,6 +285,7 @@ static int assemble_impl(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_fn* k
   a.beta = p->beta;
   a.tile_list = d_tiles;
   a.n_tile_list = n_tiles;
+  a.list_elements = list_elements ? 1 : 0;
   if (!m->elem_vertices != !m->vertex_coords)
     return set_error(HDD_ERR_INVALID, "hdd_swipdg_assemble: mesh elem_vertices / vertex_coords: both or neither");
   // vertex-indexed geometry (bit 16384 of HDD_DEBUG_FLAGS: A/B against the element-major coords)
@@ -342,6 +344,16 @@ extern "C" int hdd_swipdg_assemble_tiles(hdd_ctx* ctx, const hdd_mesh* m, const 
   if (!d_tiles && n_tiles) return set_error(HDD_ERR_INVALID, "hdd_swipdg_assemble_tiles: null tile list");
   if (n_tiles == 0) return HDD_OK;
   return assemble_impl(ctx, m, kappa, n_comp, tensor, p, pattern, d_vals, d_tiles, n_tiles, stream);
+}
+
+extern "C" int hdd_swipdg_assemble_elements(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_fn* kappa,
+                                            int32_t n_comp, const hdd_tensor_fn* tensor, const hdd_swipdg_params* p,
+                                            const hdd_csr* pattern, double* const* d_vals, const int32_t* d_elems,
+                                            int64_t n_elems, void* stream)
+{
+  if (!d_elems && n_elems) return set_error(HDD_ERR_INVALID, "hdd_swipdg_assemble_elements: null element list");
+  if (n_elems == 0) return HDD_OK;
+  return assemble_impl(ctx, m, kappa, n_comp, tensor, p, pattern, d_vals, d_elems, n_elems, stream, true);
 }
 
 // ------------------------------------------------------------------------------------------------

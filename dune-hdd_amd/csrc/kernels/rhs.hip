@@ -238,7 +238,9 @@ __device__ __forceinline__ void rhs2d_shape(double x, double y, double* v, doubl
 // geometry (vertex ids + 16-byte vertex rows) instead of the element-major coordinates -- neutral here (same
 // box 0.1345 ms both), kept so that one mesh serves every kernel.  (Staging the chunk's values in LDS for
 // 16-byte stores was slower: 0.102 -> 0.135 ms.)
-template <bool TRI, bool VX>
+// NQ > 0: the force's volume rule has NQ points (unrolled: the points' trig evaluations are independent and
+// interleave); FK: the force kind at compile time (-1: any, by a run-time switch)
+template <bool TRI, bool VX, int NQ = 0, int FK = -1>
 __global__ __launch_bounds__(256) void rhs2d_kernel(RhsArgs a)
 {
   constexpr int NB = TRI ? 3 : 4, NF = TRI ? 3 : 4;
@@ -264,15 +266,24 @@ __global__ __launch_bounds__(256) void rhs2d_kernel(RhsArgs a)
 #pragma unroll
     for (int i = 0; i < NB; ++i) acc[i] = 0.0;
     double v[NB], gx[NB], gy[NB], xq[2];
-    if (a.has_force) {
-      for (int q = 0; q < a.nqv; ++q) {
-        const double xh = a.qv[q][0], yh = a.qv[q][1];
-        xq[0] = x0 + j00 * xh + j01 * yh;
-        xq[1] = y0 + j10 * xh + j11 * yh;
-        rhs2d_shape<TRI>(xh, yh, v, gx, gy);
-        const double fv = a.qv[q][3] * adet * rhs_fn(a.force, e, xq, 2);
+    auto vol_point = [&](int q) {
+      const double xh = a.qv[q][0], yh = a.qv[q][1];
+      xq[0] = x0 + j00 * xh + j01 * yh;
+      xq[1] = y0 + j10 * xh + j11 * yh;
+      rhs2d_shape<TRI>(xh, yh, v, gx, gy);
+      double f;
+      if constexpr (FK == HDD_FN_COS_PRODUCT) f = a.force.c * cos_phase(a.force.kx * xq[0]) * cos_phase(a.force.ky * xq[1]);
+      else f = rhs_fn(a.force, e, xq, 2);
+      const double fv = a.qv[q][3] * adet * f;
 #pragma unroll
-        for (int i = 0; i < NB; ++i) acc[i] += fv * v[i];
+      for (int i = 0; i < NB; ++i) acc[i] += fv * v[i];
+    };
+    if (a.has_force) {
+      if constexpr (NQ > 0) {
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) vol_point(q);
+      } else {
+        for (int q = 0; q < a.nqv; ++q) vol_point(q);
       }
     }
     if (a.has_dirichlet || a.has_neumann) {
@@ -607,6 +618,14 @@ hipError_t launch_rhs(const RhsArgs& a, hipStream_t s)
   if (a.elem_type != HDD_HEX && n_own > 0) {
     const int64_t blocks = std::min<int64_t>((n_own + 255) / 256, int64_t(a.n_cu) * 8);
     const bool tri = a.elem_type == HDD_SIMPLEX;
+    // the ESV2007-type force (cos products) on the rules of order 4 (Dunavant 6 / Gauss 3 x 3): unrolled
+    if (a.has_force && a.force.kind == HDD_FN_COS_PRODUCT && a.nqv == (tri ? 6 : 9)) {
+      if (tri && a.ev) hipLaunchKernelGGL((rhs2d_kernel<true, true, 6, HDD_FN_COS_PRODUCT>), dim3(unsigned(blocks)), dim3(256), 0, s, a);
+      else if (tri) hipLaunchKernelGGL((rhs2d_kernel<true, false, 6, HDD_FN_COS_PRODUCT>), dim3(unsigned(blocks)), dim3(256), 0, s, a);
+      else if (a.ev) hipLaunchKernelGGL((rhs2d_kernel<false, true, 9, HDD_FN_COS_PRODUCT>), dim3(unsigned(blocks)), dim3(256), 0, s, a);
+      else hipLaunchKernelGGL((rhs2d_kernel<false, false, 9, HDD_FN_COS_PRODUCT>), dim3(unsigned(blocks)), dim3(256), 0, s, a);
+      return hipGetLastError();
+    }
     if (a.ev) {
       if (tri) hipLaunchKernelGGL((rhs2d_kernel<true, true>), dim3(unsigned(blocks)), dim3(256), 0, s, a);
       else hipLaunchKernelGGL((rhs2d_kernel<false, true>), dim3(unsigned(blocks)), dim3(256), 0, s, a);

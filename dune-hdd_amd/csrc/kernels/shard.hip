@@ -397,7 +397,8 @@ struct hdd_shard {
   // tiles
   int32_t* d_tiles_in = nullptr;
   int32_t* d_tiles_bd = nullptr;
-  int64_t n_tiles = 0, n_in = 0, n_bd = 0;
+  int32_t* d_fix = nullptr;            // owned elements (relative to own_begin) with a ghost face neighbour
+  int64_t n_tiles = 0, n_in = 0, n_bd = 0, n_fix = 0;
   int64_t halo_faces = 0;
   // host copies of the plan (hdd_shard_halo_lists / hdd_shard_tile_lists)
   std::vector<int32_t> send_idx, tiles_in, tiles_bd;
@@ -411,7 +412,8 @@ extern "C" void hdd_shard_destroy(hdd_shard* sh)
   for (void* p : {static_cast<void*>(sh->d_coords), static_cast<void*>(sh->d_nbrs), static_cast<void*>(sh->d_finfo),
                   static_cast<void*>(sh->d_gid), static_cast<void*>(sh->d_send_idx), static_cast<void*>(sh->d_sbuf),
                   static_cast<void*>(sh->d_rbuf), static_cast<void*>(sh->d_tiles_in),
-                  static_cast<void*>(sh->d_tiles_bd), static_cast<void*>(sh->d_ev), static_cast<void*>(sh->d_vxy)})
+                  static_cast<void*>(sh->d_tiles_bd), static_cast<void*>(sh->d_ev), static_cast<void*>(sh->d_vxy),
+                  static_cast<void*>(sh->d_fix)})
     if (p) (void)hipFree(p);
   if (sh->local) hdd_local_destroy(sh->local);
   delete sh;
@@ -511,19 +513,24 @@ extern "C" int hdd_shard_create(hdd_ctx* ctx, const hdd_grid* g, int32_t nranks,
   // interior / halo-boundary tiles (64 owned elements; a boundary tile has an element with a ghost face)
   const int64_t n_own = oe - ob;
   sh->n_tiles = (n_own + 63) / 64;
-  std::vector<int32_t> tin, tbd;
+  std::vector<int32_t> tin, tbd, fix;
   for (int64_t t = 0; t < sh->n_tiles; ++t) {
     bool ghost = false;
-    for (int64_t e = ob + 64 * t; e < std::min(oe, ob + 64 * t + 64); ++e)
+    for (int64_t e = ob + 64 * t; e < std::min(oe, ob + 64 * t + 64); ++e) {
+      bool eg = false;
       for (int f = 0; f < gi.nfaces; ++f) {
         const int32_t n = nbrs[size_t(f) * nl + e];
         if (n >= 0 && (n < ob || n >= oe)) {
-          ghost = true;
+          eg = true;
           ++sh->halo_faces;
         }
       }
+      if (eg) fix.push_back(int32_t(e - ob));
+      ghost |= eg;
+    }
     (ghost ? tbd : tin).push_back(int32_t(t));
   }
+  sh->n_fix = int64_t(fix.size());
   sh->n_in = int64_t(tin.size());
   sh->n_bd = int64_t(tbd.size());
   sh->send_idx = send_idx;
@@ -547,6 +554,7 @@ extern "C" int hdd_shard_create(hdd_ctx* ctx, const hdd_grid* g, int32_t nranks,
   if (e == hipSuccess) e = upload(&sh->d_send_idx, send_idx);
   if (e == hipSuccess) e = upload(&sh->d_tiles_in, tin);
   if (e == hipSuccess) e = upload(&sh->d_tiles_bd, tbd);
+  if (e == hipSuccess) e = upload(&sh->d_fix, fix);
   if (e == hipSuccess && sh->send_prefix[np])
     e = hipMalloc(&sh->d_sbuf, size_t(sh->max_rows) * sh->send_prefix[np] * sizeof(double));
   if (e == hipSuccess && sh->recv_prefix[np])
@@ -579,6 +587,7 @@ extern "C" int hdd_shard_get_info(const hdd_shard* sh, hdd_shard_info* o)
   o->halo_send = sh->send_prefix.back();
   o->halo_recv = sh->recv_prefix.back();
   o->halo_faces = sh->halo_faces;
+  o->halo_elements = sh->n_fix;
   return HDD_OK;
 }
 
@@ -753,12 +762,17 @@ extern "C" int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm*
     }
   }
   if (rc) return rc;
-  // 3. interior tiles overlap the transfer (the kernels that take tile lists: P1 / Q1 persistent policies)
-  bool overlap = !(flags & HDD_SHARD_NO_OVERLAP) && sh->n_in > 0 && sh->gi.elem_type != HDD_HEX;
+  // 3. the assembly overlaps the transfer.  Default: EVERY tile (one full-size launch at full rate; the row
+  // blocks of the ghost-adjacent elements read ghost columns the receives are still writing and are recomputed
+  // in 5).  HDD_SHARD_SPLIT_TILES: the interior tiles only (the kernels that take lists: P1 / Q1 persistent
+  // policies) -- a second launch of whole boundary tiles later, which on thin strips is a large fraction.
+  const bool split = (flags & HDD_SHARD_SPLIT_TILES) != 0;
+  bool overlap = !(flags & HDD_SHARD_NO_OVERLAP) && sh->gi.elem_type != HDD_HEX && (split ? sh->n_in > 0 : true);
   if (overlap) {
-    rc = hdd_swipdg_assemble_tiles(ctx, &m, kappa, n_comp, tensor, params, pattern, d_vals, sh->d_tiles_in, sh->n_in,
-                                   stream);
-    if (rc == HDD_ERR_UNSUPPORTED) overlap = false;   // no tile-list kernel: assemble everything after the halo
+    rc = split ? hdd_swipdg_assemble_tiles(ctx, &m, kappa, n_comp, tensor, params, pattern, d_vals, sh->d_tiles_in,
+                                           sh->n_in, stream)
+               : hdd_swipdg_assemble(ctx, &m, kappa, n_comp, tensor, params, pattern, d_vals, stream);
+    if (rc == HDD_ERR_UNSUPPORTED && split) overlap = false;   // no tile-list kernel: everything after the halo
     else if (rc) {
       if (transfer) (void)hdd_comm_wait(comm, stream);
       return rc;
@@ -776,9 +790,14 @@ extern "C" int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm*
     e = launch_halo(false, h, s);
     if (e != hipSuccess) return hip_fail(e, "hdd_block_assemble_sharded: unpack");
   }
-  // 5. the tiles that read a ghost (or everything without overlap)
-  if (overlap)
+  // 5. the rows that read a ghost (or everything without overlap)
+  if (overlap && split)
     return hdd_swipdg_assemble_tiles(ctx, &m, kappa, n_comp, tensor, params, pattern, d_vals, sh->d_tiles_bd, sh->n_bd,
                                      stream);
+  if (overlap) {
+    rc = hdd_swipdg_assemble_elements(ctx, &m, kappa, n_comp, tensor, params, pattern, d_vals, sh->d_fix, sh->n_fix,
+                                      stream);
+    if (rc != HDD_ERR_UNSUPPORTED) return rc;   // (no list kernel for these rules: the whole range again)
+  }
   return hdd_swipdg_assemble(ctx, &m, kappa, n_comp, tensor, params, pattern, d_vals, stream);
 }

@@ -925,7 +925,6 @@ struct GenericPolicy {
   static constexpr int WGCU = NB == 4 ? 4 : 8;
   static constexpr int MINW = NB == 4 ? 1 : 2;
   static constexpr bool PAD = NB == 4;   // rotated LDS image for uniform tiles (see the persistent kernel)
-  static constexpr bool DEEP_OK = NB == 4;   // the DEEP pipeline variant is instantiated (A/B: debug bit 2048)
   using Own = GOwn<E>;
   using Gat = GGat<E>;
 
@@ -1298,7 +1297,6 @@ struct P1PwcPolicy {
   // (same box, profiles/r02/s2/ab_wgcu_vx*)
   static constexpr int WGCU = VX ? 4 : 8, MINW = 1;
   static constexpr bool PAD = false;          // store-bound: its 4-way write conflicts stay hidden
-  static constexpr bool DEEP_OK = false;
   using Own = P1Own;
   using Gat = P1Gat;
   __device__ static void load_own(const AssembleArgs& a, int64_t e, Own& o) { p1_load_own<TK, KK, VX>(a, e, o); }
@@ -1331,7 +1329,6 @@ struct P1SmoothPolicy {
   // quadrature policy at 8; profiles/r01/s2/ab_p1s.log)
   static constexpr int WGCU = 8, MINW = 2;
   static constexpr bool PAD = false;
-  static constexpr bool DEEP_OK = false;
   using Own = P1Own;
   using Gat = P1Gat;
   __device__ static void load_own(const AssembleArgs& a, int64_t e, Own& o) { p1_load_own<TK, HDD_FN_CONST, VX>(a, e, o); }
@@ -1493,23 +1490,30 @@ struct P1SmoothFusedPolicy : P1SmoothPolicy<TK, VX> {
   using Own = typename Base::Own;
   using Gat = typename Base::Gat;
   static constexpr bool FUSED = true;
+  // one wave per SIMD with the whole register file: at two (<= 256 registers) the shared sines, the tile's
+  // records and the next tile's in-flight data spill (160-400 B of scratch per lane)
+  static constexpr int WGCU = 4, MINW = 1;
   struct Shared {
-    double sv, wv;        // sum_q w_q sin(phase(x_q)), sum_q w_q (Dunavant 6)
+    double sv;            // sum_q w_q sin(phase(x_q)) (Dunavant 6)
     double sf[3][3];      // sin at the Gauss 3 points of every face
   };
+  __device__ static constexpr double wv()   // sum_q w_q = 1/2, the reference triangle's area
+  {
+    double w = 0.0;
+    for (int q = 0; q < 6; ++q) w += VolRule<Simplex, 6>::w(q);
+    return w;
+  }
   __device__ static void prepare(const AssembleArgs& a, const Own& o, Shared& sh)
   {
     using E = Simplex;
     const KappaArg& K = a.kappa[0];   // the phase (kx, ky) every fused component shares
     const double j00 = o.X[1] - o.X[0], j01 = o.X[2] - o.X[0], j10 = o.Y[1] - o.Y[0], j11 = o.Y[2] - o.Y[0];
     sh.sv = 0.0;
-    sh.wv = 0.0;
 #pragma unroll
     for (int q = 0; q < 6; ++q) {
       const double xh = VolRule<Simplex, 6>::x(q), yh = VolRule<Simplex, 6>::y(q);
       const double x = o.X[0] + j00 * xh + j01 * yh, y = o.Y[0] + j10 * xh + j11 * yh;
       sh.sv += VolRule<Simplex, 6>::w(q) * sin_phase(K.kx * x + K.ky * y);
-      sh.wv += VolRule<Simplex, 6>::w(q);
     }
 #pragma unroll
     for (int f = 0; f < 3; ++f) {
@@ -1526,7 +1530,7 @@ struct P1SmoothFusedPolicy : P1SmoothPolicy<TK, VX> {
                                         const Shared& sh, double* img)
   {
     const KappaArg& K = a.kappa[c];
-    Base::emit(a, e, o, gt, img, K.c * sh.wv + K.b * sh.sv,
+    Base::emit(a, e, o, gt, img, K.c * wv() + K.b * sh.sv,
                [&](int f, double, double, int q) { return K.c + K.b * sh.sf[f][q]; });
   }
 };
@@ -1549,7 +1553,6 @@ struct VolProductPolicy {
   static constexpr int RB = NB * NB;
   static constexpr int WGCU = 4, MINW = 1;
   static constexpr bool PAD = false;
-  static constexpr bool DEEP_OK = false;
   struct Own {
     double X[NV], Y[NV];
     int32_t nbr[NF];
@@ -1687,11 +1690,7 @@ __device__ __forceinline__ int tile_offset(int c, bool active)
 // tile's CSR range with one ds_read_b128.  Other tiles use the contiguous image; for P::PAD policies their
 // tail lanes dump into the image's last row block (free: a non-uniform tile with < 64 elements holds at
 // most 63 RB - NB^2 values).
-//
-// DEEP pipeline (one more tile of look-ahead): [own data t+2][gathers t+1][compute t -> LDS][stores t], so the
-// neighbour gathers of a tile are issued a whole compute phase before they are needed (the default issues
-// them right after the previous compute, and with one wave per SIMD -- Q1 tiles -- their L2 / MALL latency
-// is exposed at the next compute).  Costs the registers of one more tile of own data and gathers in flight.
+
 // FUSED policies emit several components per tile from one prepare() (P1SmoothFusedPolicy): the driver
 // builds and streams one LDS image per component (a.n_comp of them, into a.vals[c])
 template <class P, class = void>
@@ -1703,7 +1702,7 @@ struct fused_of<P, std::void_t<decltype(P::FUSED)>> : std::bool_constant<P::FUSE
   using Shared = typename P::Shared;
 };
 
-template <class P, bool TL, bool DEEP = false>   // TL: tiles come from a.tile_list, else 0..n_tiles-1
+template <class P, bool TL>   // TL: tiles come from a.tile_list, else 0..n_tiles-1
 __global__ void __launch_bounds__(64, P::MINW)
 swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
 {
@@ -1762,19 +1761,11 @@ swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
   typename P::Own own;
   typename P::Gat gat;
   P::load_own(a, e, own);
-  // DEEP: the next tile's own data too (its gathers are issued in the first iteration)
-  [[maybe_unused]] int64_t tile1 = 0, e1 = 0;
-  [[maybe_unused]] typename P::Own own1;
-  if constexpr (DEEP) {
-    tile1 = uni64(tile_raw(next(t)));
-    e1 = elem_of_tile(tile1);
-    P::load_own(a, e1, own1);
-  }
   P::load_gat(a, e, own, gat);
   P::load_gat2(a, gat);
   int64_t base_r, tile_end_r;
   bounds_raw(tile, base_r, tile_end_r);
-  int64_t tile_n_r = tile_raw(DEEP ? next(next(t)) : next(t));
+  int64_t tile_n_r = tile_raw(next(t));
   // Drain the prologue's loads before entering the loop.  The compiler's wait counts at the loop head are
   // the minimum over the entry paths: entered straight from the prologue, the first tile's vertex rows
   // are followed by only ~7 memory operations, so the first compute of EVERY iteration waited with
@@ -1786,19 +1777,15 @@ swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
   for (;;) {
     const bool has_next = t + t_step < t_end;
     const int64_t tn = has_next ? t + t_step : t;
-    // own data of the tile one (DEEP: two) ahead; its id was loaded one iteration ago
+    // own data of the next tile; its id was loaded one iteration ago
     const int64_t tile_n = uni64(tile_n_r);
     const int64_t en = elem_of_tile(tile_n);
     typename P::Own own_n;
     P::load_own(a, en, own_n);
     int64_t base_n_r, tile_end_n_r;
-    bounds_raw(DEEP ? tile1 : tile_n, base_n_r, tile_end_n_r);   // CSR bounds of tile t+1
-    const int64_t tile_nn_r = tile_raw(DEEP ? next(next(tn)) : next(tn));
+    bounds_raw(tile_n, base_n_r, tile_end_n_r);   // CSR bounds of tile t+1
+    const int64_t tile_nn_r = tile_raw(next(tn));
     const int64_t base = uni64(base_r), tile_end = uni64(tile_end_r);   // loaded one iteration ago
-    [[maybe_unused]] typename P::Gat gat1;
-    if constexpr (DEEP) {   // gathers of t+1 (its own data arrived during the previous iteration)
-      if (!HDD_ABL(a, 4)) P::load_gat(a, e1, own1, gat1);
-    }
 
     const int64_t t0 = a.own_begin + tile * 64;
     const bool active = t0 + lane < a.own_end;
@@ -1883,9 +1870,7 @@ swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
     };
     if (ksplit > 0) stores(true);
     typename P::Gat gat_n;
-    if constexpr (!DEEP) {
-      if (!HDD_ABL(a, 4)) P::load_gat(a, en, own_n, gat_n);
-    }
+    if (!HDD_ABL(a, 4)) P::load_gat(a, en, own_n, gat_n);
     stores(false);
     if constexpr (FUSED) {   // the other components: same image slots, their own value arrays
       for (int c = 1; c < a.n_comp; ++c) {
@@ -1903,25 +1888,57 @@ swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
     // second gather stage of tile t+1 (vertex-indexed geometry: the neighbours' off-face vertices by the
     // ids the first stage brought): its wait covers the first stage only, which was issued before the
     // stores of tile t (vmcnt is in order), so it never waits for those stores
-    if (!HDD_ABL(a, 4)) P::load_gat2(a, DEEP ? gat1 : gat_n);   // (ablation 4: no stage-1 ids to follow)
+    if (!HDD_ABL(a, 4)) P::load_gat2(a, gat_n);   // (ablation 4: no stage-1 ids to follow)
     if (!has_next) break;
     t = tn;
     tile_n_r = tile_nn_r;
     base_r = base_n_r;
     tile_end_r = tile_end_n_r;
-    if constexpr (DEEP) {
-      tile = tile1;
-      e = e1;
-      own = own1;
-      gat = gat1;
-      tile1 = tile_n;
-      e1 = en;
-      own1 = own_n;
-    } else {
-      tile = tile_n;
-      e = en;
-      own = own_n;
-      gat = gat_n;
+    tile = tile_n;
+    e = en;
+    own = own_n;
+    gat = gat_n;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Element-list pass (a.list_elements): one lane per listed owned element -- the fixup of a sharded step, which
+// assembles every tile while the halo is in flight and then recomputes only the elements that read a ghost
+// (a few thousand: one lane each, its row block built in the lane's own LDS slot and written by that lane).
+// ------------------------------------------------------------------------------------------------
+template <class P>
+__global__ void __launch_bounds__(64) swipdg_elements_kernel(const AssembleArgs a, int64_t n)
+{
+  constexpr int RB = P::RB;
+  constexpr bool FUSED = fused_of<P>::value;
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  const int lane = threadIdx.x;
+  double* img = lds + lane * RB;
+  for (int64_t i0 = int64_t(blockIdx.x) * 64; i0 < n; i0 += int64_t(gridDim.x) * 64) {
+    const int64_t i = i0 + lane;
+    const bool act = i < n;
+    const int64_t e = a.own_begin + int64_t(a.tile_list[act ? i : i0]);
+    typename P::Own own;
+    typename P::Gat gat;
+    P::load_own(a, e, own);
+    P::load_gat(a, e, own, gat);
+    P::load_gat2(a, gat);
+    const int64_t base = a.elem_ptr[e - a.own_begin];
+    const int len = P::NB * P::NB * (P::n_interior(own) + 1);
+    [[maybe_unused]] typename fused_of<P>::Shared shv;
+    if constexpr (FUSED) P::prepare(a, own, shv);
+    const int ncomp = FUSED ? a.n_comp : 1;
+    for (int c = 0; c < ncomp; ++c) {
+      if constexpr (FUSED) {
+        P::emit_component(a, c, e, own, gat, shv, img);
+      } else if constexpr (P::PAD) {
+        P::compute(a, e, own, gat, RotImg<RB>{img, 0});
+      } else {
+        P::compute(a, e, own, gat, img);
+      }
+      double* out = a.vals[c];
+      if (act)
+        for (int k = 0; k < len; ++k) __builtin_nontemporal_store(img[k], out + base + k);
     }
   }
 }
@@ -1964,6 +1981,22 @@ static hipError_t launch_persistent(const AssembleArgs& a, hipStream_t s)
   wgcu = std::max(1, std::min<int>(wgcu, int((160 * 1024) / lds)));   // resident by LDS (Q1 tiles: 3 per CU)
   const int64_t G = std::min<int64_t>(tiles, int64_t(cus) * wgcu);
   const int n_launch = fused_of<P>::value ? 1 : a.n_comp;   // a FUSED policy emits every component per tile
+  if (a.list_elements) {   // element-list fixup pass: one lane per element
+    const size_t lds_e = size_t(64) * P::RB * sizeof(double);
+    const int64_t ge = std::min<int64_t>((a.n_tile_list + 63) / 64, int64_t(cus) * 4);
+    for (int c = 0; c < n_launch; ++c) {
+      AssembleArgs ac = a;
+      if (!fused_of<P>::value) {
+        ac.n_comp = 1;
+        ac.kappa[0] = a.kappa[c];
+        ac.vals[0] = a.vals[c];
+      }
+      hipLaunchKernelGGL((swipdg_elements_kernel<P>), dim3(unsigned(ge)), dim3(64), lds_e, s, ac, a.n_tile_list);
+      const hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+  }
   for (int c = 0; c < n_launch; ++c) {
     AssembleArgs ac = a;
     if (!fused_of<P>::value) {
@@ -1971,14 +2004,10 @@ static hipError_t launch_persistent(const AssembleArgs& a, hipStream_t s)
       ac.kappa[0] = a.kappa[c];
       ac.vals[0] = a.vals[c];
     }
-    const bool deep = P::DEEP_OK && (a.debug_flags & 2048);
-    if (a.tile_list) {
-      if (deep) hipLaunchKernelGGL((swipdg_persistent_kernel<P, true, P::DEEP_OK>), dim3(unsigned(G)), dim3(64), lds, s, ac, tiles);
-      else hipLaunchKernelGGL((swipdg_persistent_kernel<P, true>), dim3(unsigned(G)), dim3(64), lds, s, ac, tiles);
-    } else {
-      if (deep) hipLaunchKernelGGL((swipdg_persistent_kernel<P, false, P::DEEP_OK>), dim3(unsigned(G)), dim3(64), lds, s, ac, tiles);
-      else hipLaunchKernelGGL((swipdg_persistent_kernel<P, false>), dim3(unsigned(G)), dim3(64), lds, s, ac, tiles);
-    }
+    if (a.tile_list)
+      hipLaunchKernelGGL((swipdg_persistent_kernel<P, true>), dim3(unsigned(G)), dim3(64), lds, s, ac, tiles);
+    else
+      hipLaunchKernelGGL((swipdg_persistent_kernel<P, false>), dim3(unsigned(G)), dim3(64), lds, s, ac, tiles);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }

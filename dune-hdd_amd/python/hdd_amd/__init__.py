@@ -99,7 +99,7 @@ class ShardInfo(C.Structure):
                 ("rank", C.c_int32), ("nranks", C.c_int32), ("s_begin", C.c_int32), ("s_end", C.c_int32),
                 ("n_peers", C.c_int32), ("nb", C.c_int32), ("n_tiles", C.c_int64), ("n_tiles_interior", C.c_int64),
                 ("n_tiles_boundary", C.c_int64), ("halo_send", C.c_int64), ("halo_recv", C.c_int64),
-                ("halo_faces", C.c_int64)]
+                ("halo_faces", C.c_int64), ("halo_elements", C.c_int64)]
 
 
 # int (*)(void* user, int32 n_peers, const int32* peers, const double* const* send, const int64* send_count,
@@ -107,7 +107,7 @@ class ShardInfo(C.Structure):
 HOST_EXCHANGE_FN = C.CFUNCTYPE(C.c_int32, C.c_void_p, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_void_p),
                                C.POINTER(C.c_int64), C.POINTER(C.c_void_p), C.POINTER(C.c_int64))
 RCCL_ID_BYTES = 128
-SHARD_NO_OVERLAP, SHARD_HALO_GEOMETRY, SHARD_NO_HALO, SHARD_NO_TRANSFER = 1, 2, 4, 8
+SHARD_NO_OVERLAP, SHARD_HALO_GEOMETRY, SHARD_NO_HALO, SHARD_NO_TRANSFER, SHARD_SPLIT_TILES = 1, 2, 4, 8, 16
 
 
 _LIB = None
@@ -160,6 +160,9 @@ def lib():
                                        C.POINTER(Params), C.POINTER(CsrT), _VP, _VP]),
         "hdd_swipdg_assemble_tiles": (_I32, [_VP, C.POINTER(MeshT), C.POINTER(ScalarFn), _I32, C.POINTER(TensorFn),
                                              C.POINTER(Params), C.POINTER(CsrT), _VP, _VP, _I64, _VP]),
+        "hdd_swipdg_assemble_elements": (_I32, [_VP, C.POINTER(MeshT), C.POINTER(ScalarFn), _I32,
+                                                C.POINTER(TensorFn), C.POINTER(Params), C.POINTER(CsrT), _VP, _VP,
+                                                _I64, _VP]),
         "hdd_affine_lincomb": (_I32, [_VP, _I64, _VP, _I32, _VP, _I32, _VP, _I64, _VP]),
         "hdd_product_assemble": (_I32, [_VP, C.POINTER(MeshT), _I32, _VP, _VP, C.POINTER(Params), C.POINTER(CsrT),
                                         _VP, _VP]),
@@ -603,8 +606,9 @@ def assemble(ctx, dmesh, dpattern, kappas, tensor, prm=None, vals=None, stream=N
     return vals
 
 
-def assemble_tiles(ctx, dmesh, dpattern, kappas, tensor, tiles, vals, prm=None, stream=None):
-    """hdd_swipdg_assemble_tiles: assemble only the 64-element tiles listed in `tiles` (device int32)."""
+def assemble_tiles(ctx, dmesh, dpattern, kappas, tensor, tiles, vals, prm=None, stream=None, elements=False):
+    """hdd_swipdg_assemble_tiles: assemble only the 64-element tiles listed in `tiles` (device int32);
+    elements=True: hdd_swipdg_assemble_elements, `tiles` lists single owned elements."""
     torch = _torch()
     kappas = list(kappas)
     n = len(kappas)
@@ -612,9 +616,9 @@ def assemble_tiles(ctx, dmesh, dpattern, kappas, tensor, tiles, vals, prm=None, 
     ptrs = (C.c_void_p * n)(*[v.data_ptr() for v in vals])
     prm = prm or params_for(dmesh.local.degree, dmesh.local.dim)
     s = stream if stream is not None else torch.cuda.current_stream(dmesh.coords.device).cuda_stream
-    _check(lib().hdd_swipdg_assemble_tiles(ctx.h, C.byref(dmesh.t), arr, n, C.byref(tensor), C.byref(prm),
-                                           C.byref(dpattern.t), ptrs, tiles.data_ptr(), tiles.numel(),
-                                           C.c_void_p(s)), "hdd_swipdg_assemble_tiles")
+    name = "hdd_swipdg_assemble_elements" if elements else "hdd_swipdg_assemble_tiles"
+    _check(getattr(lib(), name)(ctx.h, C.byref(dmesh.t), arr, n, C.byref(tensor), C.byref(prm),
+                                C.byref(dpattern.t), ptrs, tiles.data_ptr(), tiles.numel(), C.c_void_p(s)), name)
     return vals
 
 
@@ -628,6 +632,14 @@ def halo_tiles(local):
     padded[:local.n_own] = ghost
     bt = padded.reshape(n_tiles, 64).any(axis=1)
     return np.nonzero(~bt)[0].astype(np.int32), np.nonzero(bt)[0].astype(np.int32)
+
+
+def halo_elements(local):
+    """owned elements (relative to own_begin) with a face neighbour in the ghost region: the fixup list of the
+    sharded step (hdd_swipdg_assemble_elements)"""
+    nb = local.neighbors[:, local.own_begin:local.own_end]
+    ghost = ((nb >= 0) & ((nb < local.own_begin) | (nb >= local.own_end))).any(axis=0)
+    return np.nonzero(ghost)[0].astype(np.int32)
 
 
 def product(ctx, dmesh, kind, dpattern, kappa=None, tensor=None, prm=None, out=None, stream=None):

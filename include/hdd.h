@@ -36,8 +36,9 @@
 extern "C" {
 #endif
 
-#define HDD_ABI_VERSION 4   /* 3: hdd_mesh vertex-indexed geometry, hdd_local_vertices;
-                               4: HDD_FN_FLATTOP (hdd_scalar_fn.table / n_table), hdd_indicator_sum */
+#define HDD_ABI_VERSION 5   /* 3: hdd_mesh vertex-indexed geometry, hdd_local_vertices;
+                               4: HDD_FN_FLATTOP (hdd_scalar_fn.table / n_table), hdd_indicator_sum;
+                               5: hdd_shard_info.halo_elements, hdd_swipdg_assemble_elements */
 #define HDD_MAX_COMP 8
 
 typedef enum {
@@ -278,6 +279,15 @@ int hdd_swipdg_assemble_tiles(hdd_ctx* ctx, const hdd_mesh* mesh, const hdd_scal
                               const hdd_tensor_fn* tensor, const hdd_swipdg_params* params, const hdd_csr* pattern,
                               double* const* d_vals, const int32_t* d_tiles, int64_t n_tiles, void* stream);
 
+/* Same, restricted to the single owned elements own_begin + d_elems[0..n_elems) (one lane each, any order,
+ * no duplicates): the fixup pass of a sharded step, which assembles every tile while the halo is in flight
+ * (ghost rows stale) and then recomputes only the row blocks of elements with a ghost face neighbour.
+ * Same kernel coverage as hdd_swipdg_assemble_tiles. */
+int hdd_swipdg_assemble_elements(hdd_ctx* ctx, const hdd_mesh* mesh, const hdd_scalar_fn* kappa, int32_t n_comp,
+                                 const hdd_tensor_fn* tensor, const hdd_swipdg_params* params,
+                                 const hdd_csr* pattern, double* const* d_vals, const int32_t* d_elems,
+                                 int64_t n_elems, void* stream);
+
 /* SWIPDG right-hand side -- replaces the functionals of SWIPDG::init() (swipdg.hh:251-347):
  *   L2Volume(force) + DirichletBoundarySWIPDG(kappa, tensor, dirichlet) on Dirichlet faces
  *   + L2Face(neumann) on Neumann faces, each of force / dirichlet / neumann nullable (absent = zero).
@@ -387,6 +397,7 @@ typedef struct {
   int64_t n_tiles, n_tiles_interior, n_tiles_boundary;   /* 64-element tiles of the owned elements */
   int64_t halo_send, halo_recv;     /* elements sent / ghost elements received per exchange */
   int64_t halo_faces;               /* faces between an owned and a ghost element */
+  int64_t halo_elements;            /* owned elements with a ghost face neighbour (the fixup pass) */
 } hdd_shard_info;
 
 /* Rank `rank` of `nranks` owns the subdomains s with owner[s] == rank, which must form one contiguous
@@ -420,18 +431,23 @@ int hdd_shard_pattern_fill(hdd_ctx* ctx, const hdd_shard* sh, int64_t* d_row_ptr
                            int64_t* d_elem_ptr, void* stream);
 
 enum {
-  HDD_SHARD_NO_OVERLAP = 1,     /* exchange, then assemble every tile (default: interior tiles overlap the halo) */
+  HDD_SHARD_NO_OVERLAP = 1,     /* exchange, then assemble every tile (default: the assembly overlaps the halo) */
   HDD_SHARD_HALO_GEOMETRY = 2,  /* also send the ghost vertex coordinates (default: geometry is rank-local) */
   HDD_SHARD_NO_HALO = 4,        /* ghost columns already valid (static coefficients): no exchange at all */
-  HDD_SHARD_NO_TRANSFER = 8     /* timing studies only: pack and split tile launches as in an exchange, a
+  HDD_SHARD_NO_TRANSFER = 8,    /* timing studies only: pack and split tile launches as in an exchange, a
                                    loopback copy + unpack kernel instead of the transfer (comm may be NULL; the
                                    ghost columns receive the rank's own send buffers, i.e. wrong values) -- an
                                    upper bound of the GPU-side cost of the sharded step */
+  HDD_SHARD_SPLIT_TILES = 16    /* overlap by tiles (round 2): interior tiles during the exchange, the tiles with a
+                                   ghost-adjacent element after it (default: every tile during the exchange, then
+                                   the ghost-adjacent ELEMENTS again, hdd_swipdg_assemble_elements) */
 };
 /* One sharded assembly step -- the LHS of BlockSWIPDG::init() for the owned subdomains: pack the halo
  * records (per-element tensor / kappa rows, [+ coordinates]) of the elements the peers need -> post the
  * exchange, one message per (peer, halo row), received straight into the ghost columns (the ghosts of one
- * owner are contiguous, recv_col0) -> interior tiles -> wait -> halo-boundary tiles.  The per-element arrays
+ * owner are contiguous, recv_col0) -> every tile (the row blocks of ghost-adjacent elements read stale ghost
+ * columns and are discarded) -> wait -> the ghost-adjacent elements again (hdd_shard_info.halo_elements of
+ * them, one lane each, overwriting their row blocks).  The per-element arrays
  * of `kappa` / `tensor` must span n_local columns: their owned columns are read and their GHOST COLUMNS ARE
  * WRITTEN by the receives.  comm may be NULL when the shard has no peers. */
 int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm* comm, const hdd_scalar_fn* kappa,

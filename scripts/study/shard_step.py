@@ -5,10 +5,11 @@ the assembly), for rank r of an N-rank decomposition of
       scaling: N = 8 gives each rank 440 x 1200 elements),
 timed as
   (a) NO_HALO       -- the whole owned range in one launch (ghost columns valid): the kernel alone,
-  (b) step          -- pack, loopback copy instead of the transfer (HDD_SHARD_NO_TRANSFER), interior tiles,
-                       unpack, halo-boundary tiles: every launch of the real step, RCCL excluded,
-  (c) serial step   -- the same without the overlap split (one launch of all tiles after the unpack),
-  (d) step, graph   -- (b) captured once into a hipGraph (torch.cuda.CUDAGraph) and replayed.
+  (b) step          -- pack, loopback copy instead of the transfer (HDD_SHARD_NO_TRANSFER), every tile, unpack,
+                       the ghost-adjacent elements again: every launch of the real step, RCCL excluded,
+  (c) serial step   -- the same without the overlap (one launch of all tiles after the unpack),
+  (d) step, graph   -- (b) captured once into a hipGraph (torch.cuda.CUDAGraph) and replayed,
+  (e) split tiles   -- round 2's overlap (HDD_SHARD_SPLIT_TILES): interior tiles, unpack, boundary tiles.
 usage: python scripts/study/shard_step.py [c2|c4] [N ...]"""
 import os, sys
 import numpy as np
@@ -59,6 +60,7 @@ def main():
                 "a NO_HALO (one launch)": H.SHARD_NO_HALO,
                 "b step, no transfer": H.SHARD_NO_TRANSFER,
                 "c serial step, no transfer": H.SHARD_NO_TRANSFER | H.SHARD_NO_OVERLAP,
+                "e split tiles, no transfer": H.SHARD_NO_TRANSFER | H.SHARD_SPLIT_TILES,
             }
             res = {name: timeit(lambda f=f: H.assemble_sharded(ctx, sh, None, kap, ten, pat, vals, flags=f))
                    for name, f in runs.items()}
@@ -78,9 +80,10 @@ def main():
             except Exception as e:   # report, keep the other numbers
                 print("  graph capture failed: %s" % e)
             i = sh.info
-            print("%s N=%d rank %d: %d owned, %d ghosts, tiles %d interior + %d boundary, halo %d/%d elements"
-                  % (workload, n, rank, sh.n_own, i.n_ghost, i.n_tiles_interior, i.n_tiles_boundary, i.halo_send,
-                     i.halo_recv))
+            print("%s N=%d rank %d: %d owned, %d ghosts, tiles %d interior + %d boundary, %d ghost-adjacent "
+                  "elements, halo %d/%d elements"
+                  % (workload, n, rank, sh.n_own, i.n_ghost, i.n_tiles_interior, i.n_tiles_boundary, i.halo_elements,
+                     i.halo_send, i.halo_recv))
             base = res["a NO_HALO (one launch)"][0]
             for name, (med, mn) in res.items():
                 print("  %-32s median %.4f ms  min %.4f ms  (%+.1f %%)" % (name, med, mn, 100 * (med / base - 1)),

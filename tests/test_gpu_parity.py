@@ -219,23 +219,32 @@ def test_q1_ragged_tiles_and_tile_lists(ctx, tk, bnd):
     assert np.array_equal(lv, lt)
 
 
+@pytest.mark.parametrize("mode", ["tiles", "elements"])
 @pytest.mark.parametrize("et,smooth", [(H.SIMPLEX, False), (H.SIMPLEX, True), (H.CUBE, False), (H.CUBE, True)])
-def test_tile_split_overlap(ctx, et, smooth):
-    """hdd_swipdg_assemble_tiles: interior tiles assembled while the ghost records are garbage (NaN), then
-    the halo-boundary tiles after the ghosts are restored, reproduce the one-shot assembly bit for bit."""
+def test_tile_split_overlap(ctx, et, smooth, mode):
+    """The two overlap schemes of the sharded step reproduce the one-shot assembly bit for bit:
+    tiles     -- hdd_swipdg_assemble_tiles: interior tiles assembled while the ghost records are garbage (NaN),
+                 the halo-boundary tiles after the ghosts are restored;
+    elements  -- every tile assembled on the garbage ghosts (hdd_swipdg_assemble), then the ghost-adjacent
+                 elements again (hdd_swipdg_assemble_elements, listed in shuffled order).
+    Two components for the smooth case: the fused two-component P1 policy takes the element list too."""
     torch = _torch()
     grid = H.Grid.structured(et, 1024, 4, (0, 0), (4, 1), px=4, py=1)
     local = grid.local(1, 3)
     dm = H.DeviceMesh(local)
     dp = H.DevicePattern(local)
     kcell = torch.from_numpy(local.checkerboard((0, 0), (4, 1), 100, 20, O.spe10_synthetic_permeability())).cuda()
-    kap = [H.scalar_fn(H.FN_SINUSOID if smooth else H.FN_CONST, 1.0, b=0.5, kx=3.0, ky=2.0, order=3)
-           if smooth else H.scalar_fn(H.FN_CONST, 1.0)]
+    kap = ([H.scalar_fn(H.FN_SINUSOID, 1.0, b=0.5, kx=3.0, ky=2.0, order=3),
+            H.scalar_fn(H.FN_SINUSOID, 0.0, b=1.0, kx=3.0, ky=2.0, order=3)]
+           if smooth else [H.scalar_fn(H.FN_CONST, 1.0)])
     ten = H.tensor_fn(H.TENSOR_ISO_PER_ELEM, per_elem=kcell)
-    (ref,) = H.assemble(ctx, dm, dp, kap, ten)
+    refs = H.assemble(ctx, dm, dp, kap, ten)
     t_in, t_bd = H.halo_tiles(local)
+    fix = H.halo_elements(local)
     assert len(t_in) and len(t_bd)
-    val = torch.full_like(ref, float("nan"))
+    assert 0 < len(fix) < 64 * len(t_bd)
+    fix = np.random.default_rng(3).permutation(fix).astype(np.int32)
+    vals = [torch.full_like(r, float("nan")) for r in refs]
     saved = dm.coords.clone()
     ghosts = torch.ones(local.n_local, dtype=torch.bool, device="cuda")
     ghosts[local.own_begin:local.own_end] = False
@@ -249,12 +258,21 @@ def test_tile_split_overlap(ctx, et, smooth):
     assert bool(ghost_only.any())
     saved_v = dm.vertex_coords.clone()
     dm.vertex_coords[ghost_only] = float("nan")
-    H.assemble_tiles(ctx, dm, dp, kap, ten, torch.from_numpy(t_in).cuda(), [val])
+    if mode == "tiles":
+        H.assemble_tiles(ctx, dm, dp, kap, ten, torch.from_numpy(t_in).cuda(), vals)
+    else:
+        H.assemble(ctx, dm, dp, kap, ten, vals=vals)
+        torch.cuda.synchronize()
+        assert not all(torch.equal(v, r) for v, r in zip(vals, refs))   # the garbage ghosts reached some rows
     dm.coords.copy_(saved)
     dm.vertex_coords.copy_(saved_v)
-    H.assemble_tiles(ctx, dm, dp, kap, ten, torch.from_numpy(t_bd).cuda(), [val])
+    if mode == "tiles":
+        H.assemble_tiles(ctx, dm, dp, kap, ten, torch.from_numpy(t_bd).cuda(), vals)
+    else:
+        H.assemble_tiles(ctx, dm, dp, kap, ten, torch.from_numpy(fix).cuda(), vals, elements=True)
     torch.cuda.synchronize()
-    assert torch.equal(val, ref)
+    for v, r in zip(vals, refs):
+        assert torch.equal(v, r)
 
 
 def test_golden_fixtures(ctx):

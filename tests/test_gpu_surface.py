@@ -214,7 +214,7 @@ def test_cpp_spe10_flattop_channel(surface_run):
     for name, (cc, bb) in [("spe10ft_affine", (1.0, 0.9)), ("spe10ftp_affine", (1.0, 1.0)), ("spe10ftp_comp0", (0.0, 1.0))]:
         rp, col, ref = O.assemble(og, O.flattop(boxes, cc, bb), A, O.params())
         assert compare_rows(rp, _ld(d, name), ref, 1e-12, floor_frac=1e-10)[1], name
-    assert np.count_nonzero(_ld(d, "spe10ftp_comp0")) > 0.2 * _ld(d, "spe10ftp_comp0").size   # the channel is there
+    assert np.count_nonzero(_ld(d, "spe10ftp_comp0")) > 0.05 * _ld(d, "spe10ftp_comp0").size   # the channel is there
 
 
 @pytest.mark.gpu

@@ -63,6 +63,7 @@ CASES = {
                                H.SHARD_NO_OVERLAP | H.SHARD_HALO_GEOMETRY, False),
     "p1_sym_two_comp": (H.SIMPLEX, 36, 12, 4, 2, H.TENSOR_SYM_PER_ELEM, 0, True),
     "q1_iso_overlap_2x2": (H.CUBE, 44, 15, 4, 2, H.TENSOR_ISO_PER_ELEM, 0, True),
+    "q1_iso_split_tiles": (H.CUBE, 44, 15, 4, 2, H.TENSOR_ISO_PER_ELEM, H.SHARD_SPLIT_TILES, True),
 }
 
 
