@@ -30,6 +30,10 @@ struct hdd_ctx {
   double* q3g_tab = nullptr;   // p=3 reference matrices [Q3G_K][4096], uploaded on first use
   void* scan_ws = nullptr;     // device-pattern row-length scan scratch (kept: no allocation per build)
   size_t scan_ws_bytes = 0;
+  void* ops_d = nullptr;       // batched block operators: device descriptor table,
+  void* ops_h = nullptr;       //   its pinned host staging copy (reused once the last upload has completed)
+  size_t ops_bytes = 0;
+  hipEvent_t ops_evt = nullptr;
 };
 
 int hdd::ctx_device(const hdd_ctx* ctx) { return ctx ? ctx->device : 0; }
@@ -84,6 +88,9 @@ extern "C" void hdd_ctx_destroy(hdd_ctx* ctx)
   if (ctx && ctx->ws) (void)hipFree(ctx->ws);
   if (ctx && ctx->q3g_tab) (void)hipFree(ctx->q3g_tab);
   if (ctx && ctx->scan_ws) (void)hipFree(ctx->scan_ws);
+  if (ctx && ctx->ops_d) (void)hipFree(ctx->ops_d);
+  if (ctx && ctx->ops_h) (void)hipHostFree(ctx->ops_h);
+  if (ctx && ctx->ops_evt) (void)hipEventDestroy(ctx->ops_evt);
   delete ctx;
 }
 
@@ -966,7 +973,215 @@ int subcsr_check(const hdd_csr* p, int64_t r0, int64_t r1, int64_t c0, int64_t c
 }
 
 unsigned rows_grid(int64_t n, int n_cu) { return unsigned(std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, int64_t(n_cu) * 16))); }
+
+// ---- batched: n_ops sub-blocks of one pattern in four launches.  The concatenated row-pointer array holds
+// a leading slot per operator (count 0) before its row counts, so ONE inclusive scan over all operators leaves
+// at operator k's leading slot the number of entries of the operators before it (base) and at its slot j the
+// global start of its row j.  Operator k's entries start at noff = the prefix of the EVEN-rounded counts
+// (16-byte aligned value arrays: hdd_affine_lincomb takes every operator as it is).
+struct OpDesc {
+  int64_t r0, c0, c1;   // rows [r0, r0 + rows), columns [c0, c1) of the pattern
+  int64_t roff, rows;   // slots [roff, roff + rows + 1) of the concatenated row-pointer array
+  int64_t base;         // entries of the operators before k (the scan's value at the leading slot)
+  int64_t noff;         // where operator k's entries start in the concatenated outputs (even)
+};
+
+__device__ __forceinline__ int op_of_slot(const OpDesc* d, int n_ops, int64_t x)
+{
+  int lo = 0, hi = n_ops - 1;   // last k with roff_k <= x
+  while (lo < hi) {
+    const int m = (lo + hi + 1) >> 1;
+    if (d[m].roff <= x) lo = m;
+    else hi = m - 1;
+  }
+  return lo;
+}
+
+__global__ void __launch_bounds__(256) ops_count_kernel(const int64_t* __restrict__ rp, const int32_t* __restrict__ col,
+                                                        const OpDesc* __restrict__ d, int n_ops, int64_t n_slots,
+                                                        int64_t* __restrict__ out)
+{
+  for (int64_t x = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; x < n_slots; x += int64_t(gridDim.x) * blockDim.x) {
+    const OpDesc o = d[op_of_slot(d, n_ops, x)];
+    const int64_t j = x - o.roff;
+    int64_t c = 0;
+    if (j > 0) {
+      const int64_t a = rp[o.r0 + j - 1], b = rp[o.r0 + j];
+      const int64_t lo = lower_bound_col(col, a, b, o.c0);
+      c = lower_bound_col(col, lo, b, o.c1) - lo;
+    }
+    out[x] = c;
+  }
+}
+
+__global__ void ops_base_kernel(const int64_t* __restrict__ scanned, OpDesc* d, int n_ops, int64_t* __restrict__ totals)
+{
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  int64_t noff = 0;   // a serial pass over the operators (thousands at most)
+  for (int k = 0; k < n_ops; ++k) {
+    const int64_t b = scanned[d[k].roff];
+    const int64_t n = scanned[d[k].roff + d[k].rows] - b;
+    d[k].base = b;
+    d[k].noff = noff;
+    if (totals) totals[k] = noff;
+    noff += n + (n & 1);
+  }
+  if (totals) totals[n_ops] = noff;
+}
+
+// columns (local) / sources at the global positions, then the row pointer made operator-relative in place
+// (each slot reads only itself: its count is recomputed, the base comes from the descriptor)
+__global__ void __launch_bounds__(256) ops_fill_kernel(const int64_t* __restrict__ rp, const int32_t* __restrict__ col,
+                                                       const OpDesc* __restrict__ d, int n_ops, int64_t n_slots,
+                                                       int64_t* __restrict__ out_rp, int32_t* __restrict__ out_col,
+                                                       int64_t* __restrict__ out_src)
+{
+  for (int64_t x = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; x < n_slots; x += int64_t(gridDim.x) * blockDim.x) {
+    const OpDesc o = d[op_of_slot(d, n_ops, x)];
+    const int64_t j = x - o.roff;
+    const int64_t end = out_rp[x] - o.base;   // operator-relative end of row j - 1
+    if (j > 0 && (out_col || out_src)) {
+      const int64_t a = rp[o.r0 + j - 1], b = rp[o.r0 + j];
+      const int64_t lo = lower_bound_col(col, a, b, o.c0);
+      const int64_t len = lower_bound_col(col, lo, b, o.c1) - lo;
+      for (int64_t i = 0; i < len; ++i) {
+        const int64_t g = o.noff + end - len + i;
+        if (out_col) out_col[g] = int32_t(int64_t(col[lo + i]) - o.c0);
+        if (out_src) out_src[g] = lo + i;
+      }
+    }
+    out_rp[x] = end;
+  }
+}
+
+// values: thread per row slot; operator k's entries at noff_k + its (relative) row pointer
+__global__ void __launch_bounds__(256) ops_values_kernel(const int64_t* __restrict__ rp, const int32_t* __restrict__ col,
+                                                         const OpDesc* __restrict__ d, int n_ops, int64_t n_slots,
+                                                         const int64_t* __restrict__ out_rp, ValPtrs v, int nc)
+{
+  for (int64_t x = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; x < n_slots; x += int64_t(gridDim.x) * blockDim.x) {
+    const OpDesc o = d[op_of_slot(d, n_ops, x)];
+    const int64_t j = x - o.roff;
+    if (j == 0) continue;
+    const int64_t k0 = o.noff + out_rp[x - 1], len = out_rp[x] - out_rp[x - 1];
+    if (len == 0) continue;
+    const int64_t lo = lower_bound_col(col, rp[o.r0 + j - 1], rp[o.r0 + j], o.c0);
+    for (int c = 0; c < nc; ++c)
+      for (int64_t i = 0; i < len; ++i) v.out[c][k0 + i] = v.in[c][lo + i];
+  }
+}
 }  // namespace
+
+// descriptor table of a batched call -> ctx->ops_d (stream-ordered upload through the pinned staging copy,
+// reused only after the previous upload completed); noff from the host array when given
+static int ops_upload(hdd_ctx* ctx, const hdd_csr* p, int32_t n_ops, const hdd_block_range* ops,
+                      const int64_t* nnz_off, hipStream_t s, int64_t* n_slots, const char* who)
+{
+  if (n_ops < 1 || !ops) return set_error(HDD_ERR_INVALID, std::string(who) + ": need n_ops >= 1 ranges");
+  const size_t bytes = size_t(n_ops) * sizeof(OpDesc);
+  hipError_t e = hipSuccess;
+  if (!ctx->ops_evt && (e = hipEventCreateWithFlags(&ctx->ops_evt, hipEventDisableTiming)) != hipSuccess)
+    return hip_fail(e, who);
+  if ((e = hipEventSynchronize(ctx->ops_evt)) != hipSuccess) return hip_fail(e, who);
+  if (bytes > ctx->ops_bytes) {
+    if (ctx->ops_d) (void)hipFree(ctx->ops_d);
+    if (ctx->ops_h) (void)hipHostFree(ctx->ops_h);
+    ctx->ops_d = ctx->ops_h = nullptr;
+    ctx->ops_bytes = 0;
+    if ((e = hipMalloc(&ctx->ops_d, bytes)) != hipSuccess) return hip_fail(e, who);
+    if ((e = hipHostMalloc(&ctx->ops_h, bytes, hipHostMallocDefault)) != hipSuccess) return hip_fail(e, who);
+    ctx->ops_bytes = bytes;
+  }
+  auto* h = static_cast<OpDesc*>(ctx->ops_h);
+  int64_t slots = 0;
+  for (int32_t k = 0; k < n_ops; ++k) {
+    const hdd_block_range& r = ops[k];
+    if (int rc = subcsr_check(p, r.row_begin, r.row_end, r.col_begin, r.col_end, who)) return rc;
+    if (nnz_off && (nnz_off[k] & 1))
+      return set_error(HDD_ERR_INVALID, std::string(who) + ": nnz_off must be even (16-byte aligned operators)");
+    h[k] = OpDesc{r.row_begin, r.col_begin, r.col_end, slots, r.row_end - r.row_begin, 0, nnz_off ? nnz_off[k] : 0};
+    slots += r.row_end - r.row_begin + 1;
+  }
+  if (slots >= int64_t(INT32_MAX))
+    return set_error(HDD_ERR_RANGE, std::string(who) + ": sum of (rows + 1) over the operators must fit int32");
+  if ((e = hipMemcpyAsync(ctx->ops_d, ctx->ops_h, bytes, hipMemcpyHostToDevice, s)) != hipSuccess) return hip_fail(e, who);
+  if ((e = hipEventRecord(ctx->ops_evt, s)) != hipSuccess) return hip_fail(e, who);
+  *n_slots = slots;
+  return HDD_OK;
+}
+
+extern "C" int hdd_block_operators_map_device(hdd_ctx* ctx, const hdd_csr* pattern, int32_t n_ops,
+                                              const hdd_block_range* ops, int64_t* d_out_row_ptr, int32_t* d_out_col,
+                                              int64_t* d_out_src, int64_t* nnz_off, void* stream)
+{
+  static const char* who = "hdd_block_operators_map_device";
+  if (!ctx || !d_out_row_ptr) return set_error(HDD_ERR_INVALID, std::string(who) + ": null argument");
+  hipError_t e = hipSetDevice(ctx->device);
+  if (e != hipSuccess) return hip_fail(e, who);
+  const hipStream_t s = static_cast<hipStream_t>(stream);
+  int64_t n = 0;
+  if (int rc = ops_upload(ctx, pattern, n_ops, ops, nullptr, s, &n, who)) return rc;
+  auto* d = static_cast<OpDesc*>(ctx->ops_d);
+  const unsigned grid = rows_grid(n, ctx->n_cu);
+  hipLaunchKernelGGL(ops_count_kernel, dim3(grid), dim3(256), 0, s, pattern->row_ptr, pattern->col, d, int(n_ops), n,
+                     d_out_row_ptr);
+  if ((e = hipGetLastError()) != hipSuccess) return hip_fail(e, who);
+  size_t tmp = 0;
+  if ((e = hipcub::DeviceScan::InclusiveSum(nullptr, tmp, d_out_row_ptr, d_out_row_ptr, n, s)) != hipSuccess)
+    return hip_fail(e, who);
+  // scan scratch + (n_ops + 1) totals, kept in the context
+  const size_t need = tmp + size_t(n_ops + 1) * sizeof(int64_t) + 256;
+  if (need > ctx->scan_ws_bytes) {
+    (void)hipStreamSynchronize(s);
+    if (ctx->scan_ws) (void)hipFree(ctx->scan_ws);
+    ctx->scan_ws = nullptr;
+    ctx->scan_ws_bytes = 0;
+    if ((e = hipMalloc(&ctx->scan_ws, need)) != hipSuccess) return hip_fail(e, who);
+    ctx->scan_ws_bytes = need;
+  }
+  if ((e = hipcub::DeviceScan::InclusiveSum(ctx->scan_ws, tmp, d_out_row_ptr, d_out_row_ptr, n, s)) != hipSuccess)
+    return hip_fail(e, who);
+  auto* totals = reinterpret_cast<int64_t*>(static_cast<char*>(ctx->scan_ws) + ((tmp + 255) & ~size_t(255)));
+  hipLaunchKernelGGL(ops_base_kernel, dim3(1), dim3(64), 0, s, d_out_row_ptr, d, int(n_ops),
+                     nnz_off ? totals : nullptr);
+  if ((e = hipGetLastError()) != hipSuccess) return hip_fail(e, who);
+  hipLaunchKernelGGL(ops_fill_kernel, dim3(grid), dim3(256), 0, s, pattern->row_ptr, pattern->col, d, int(n_ops), n,
+                     d_out_row_ptr, d_out_col, d_out_src);
+  if ((e = hipGetLastError()) != hipSuccess) return hip_fail(e, who);
+  if (nnz_off) {
+    e = hipMemcpyAsync(nnz_off, totals, size_t(n_ops + 1) * sizeof(int64_t), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return hip_fail(e, who);
+  }
+  return HDD_OK;
+}
+
+extern "C" int hdd_block_operators_values_device(hdd_ctx* ctx, const hdd_csr* pattern, int32_t n_ops,
+                                                 const hdd_block_range* ops, const int64_t* nnz_off,
+                                                 const int64_t* d_out_row_ptr, const double* const* d_vals,
+                                                 int32_t n_comp, double* const* d_out, void* stream)
+{
+  static const char* who = "hdd_block_operators_values_device";
+  if (!ctx || !nnz_off || !d_out_row_ptr || !d_vals || !d_out || n_comp < 0 || n_comp > HDD_MAX_COMP)
+    return set_error(HDD_ERR_INVALID, std::string(who) + ": invalid argument");
+  ValPtrs v{};
+  for (int c = 0; c < n_comp; ++c) {
+    if (!d_vals[c] || !d_out[c]) return set_error(HDD_ERR_INVALID, std::string(who) + ": null value array");
+    v.in[c] = d_vals[c];
+    v.out[c] = d_out[c];
+  }
+  hipError_t e = hipSetDevice(ctx->device);
+  if (e != hipSuccess) return hip_fail(e, who);
+  const hipStream_t s = static_cast<hipStream_t>(stream);
+  int64_t n = 0;
+  if (int rc = ops_upload(ctx, pattern, n_ops, ops, nnz_off, s, &n, who)) return rc;
+  if (n_comp == 0) return HDD_OK;
+  hipLaunchKernelGGL(ops_values_kernel, dim3(rows_grid(n, ctx->n_cu)), dim3(256), 0, s, pattern->row_ptr, pattern->col,
+                     static_cast<const OpDesc*>(ctx->ops_d), int(n_ops), n, d_out_row_ptr, v, int(n_comp));
+  e = hipGetLastError();
+  return e == hipSuccess ? HDD_OK : hip_fail(e, who);
+}
+
 
 extern "C" int hdd_block_operator_map_device(hdd_ctx* ctx, const hdd_csr* pattern, int64_t row_begin, int64_t row_end,
                                              int64_t col_begin, int64_t col_end, int64_t* d_out_row_ptr,

@@ -171,6 +171,8 @@ def lib():
         "hdd_gather_values": (_I32, [_VP, _VP, _VP, _I64, _VP, _VP]),
         "hdd_block_operator_map_device": (_I32, [_VP, _VP, _I64, _I64, _I64, _I64, _VP, _VP, _VP, _VP, _VP]),
         "hdd_block_operator_values_device": (_I32, [_VP, _VP, _I64, _I64, _I64, _I64, _VP, _VP, _I32, _VP, _VP]),
+        "hdd_block_operators_map_device": (_I32, [_VP, _VP, _I32, _VP, _VP, _VP, _VP, _VP, _VP]),
+        "hdd_block_operators_values_device": (_I32, [_VP, _VP, _I32, _VP, _VP, _VP, _VP, _I32, _VP, _VP]),
         "hdd_soa_gather": (_I32, [_VP, _VP, _VP, _I32, _I64, _VP, _I64, _VP, _VP]),
         "hdd_soa_scatter": (_I32, [_VP, _VP, _VP, _I32, _I64, _I64, _I64, _VP, _VP]),
         "hdd_rccl_get_unique_id": (_I32, [_VP]),
@@ -588,6 +590,54 @@ def block_operator(ctx, grid, dpattern, vals, ss, nn, nnz=None, stream=None):
     _check(lib().hdd_block_operator_values_device(ctx.h, C.byref(dpattern.t), a * nb, b * nb, c * nb, d * nb,
                                                   orp.data_ptr(), vin, len(vals), vout, s), "block_operator")
     return orp, ocol[:nnz], [o[:nnz] for o in outs]
+
+
+def block_operators(ctx, grid, dpattern, vals, pairs, nnz=None, stream=None):
+    """Every listed (ss, nn) operator at once (hdd_block_operators_map_device + _values_device: four launches
+    for the map, one for the values, whatever the number of operators).  Returns {(ss, nn): (row_ptr, col,
+    [values per component])}, views into three concatenated device arrays.  nnz: dict (ss, nn) -> nnz (e.g.
+    block_operator_nnz) keeps the call asynchronous; None synchronises once for the counts."""
+    torch = _torch()
+    dev = dpattern.row_ptr.device
+    nb = grid.nb
+    pairs = list(pairs)
+    n_ops = len(pairs)
+    rng = (C.c_int64 * (4 * n_ops))()
+    rows = []
+    for k, (ss, nn) in enumerate(pairs):
+        a, b = grid.subdomain_range(ss, ss + 1)
+        c, d = grid.subdomain_range(nn, nn + 1)
+        rng[4 * k:4 * k + 4] = [a * nb, b * nb, c * nb, d * nb]
+        rows.append((b - a) * nb)
+    roff = np.concatenate([[0], np.cumsum(np.asarray(rows, np.int64) + 1)])
+    s = C.c_void_p(stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream)
+    orp = torch.empty(int(roff[-1]), dtype=torch.int64, device=dev)
+    noff = (C.c_int64 * (n_ops + 1))()
+    if nnz is not None:
+        noff[:] = np.concatenate([[0], np.cumsum([nnz[p] + (nnz[p] & 1) for p in pairs])]).tolist()
+    total = noff[n_ops] if nnz is not None else None
+    if total is None:   # counts from the device: the map call returns them (one synchronisation)
+        _check(lib().hdd_block_operators_map_device(ctx.h, C.byref(dpattern.t), n_ops, rng, orp.data_ptr(), None, None,
+                                                    noff, s), "block_operators")
+        total = noff[n_ops]
+    ocol = torch.empty(max(total, 1), dtype=torch.int32, device=dev)
+    _check(lib().hdd_block_operators_map_device(ctx.h, C.byref(dpattern.t), n_ops, rng, orp.data_ptr(),
+                                                ocol.data_ptr(), None, None, s), "block_operators")
+    vals = list(vals)
+    outs = [torch.empty(max(total, 1), dtype=torch.float64, device=dev) for _ in vals]
+    for i0 in range(0, len(vals), MAX_COMP):
+        vin = (C.c_void_p * MAX_COMP)(*[v.data_ptr() for v in vals[i0:i0 + MAX_COMP]])
+        vout = (C.c_void_p * MAX_COMP)(*[o.data_ptr() for o in outs[i0:i0 + MAX_COMP]])
+        _check(lib().hdd_block_operators_values_device(ctx.h, C.byref(dpattern.t), n_ops, rng, noff, orp.data_ptr(),
+                                                       vin, len(vals[i0:i0 + MAX_COMP]), vout, s), "block_operators")
+    if nnz is None:   # the operators' counts: the last entry of every row pointer (one gather, one copy)
+        last = orp[torch.from_numpy(roff[1:] - 1).to(dev)].cpu().numpy()
+        nnz = {p: int(last[k]) for k, p in enumerate(pairs)}
+    out = {}
+    for k, p in enumerate(pairs):
+        n0 = noff[k]
+        out[p] = (orp[roff[k]:roff[k + 1]], ocol[n0:n0 + nnz[p]], [o[n0:n0 + nnz[p]] for o in outs])
+    return out
 
 
 def assemble(ctx, dmesh, dpattern, kappas, tensor, prm=None, vals=None, stream=None):

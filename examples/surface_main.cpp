@@ -3,6 +3,7 @@
 // block-swipdg_main.cc:21-92, test/linearelliptic-block-swipdg.hh): construct on a (multiscale) grid,
 // init(), query the affinely decomposed system matrix, local and coupling operators, freeze a parameter.
 // Writes raw arrays to <outdir> for tests/test_gpu_surface.py to compare with the CPU oracle.
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -52,6 +53,51 @@ uint64_t checksum(const internal_array_t<T>& a, int64_t n)
 // 3200 x 640 Kuhn) and ESV2007 3d Q3 on n^3 hexahedra
 int run_big(const std::string& which, int n)
 {
+  if (which == "c4ops") {   // BASELINE's 8-GPU decomposition: every block operator, one by one and batched
+    hdd_structured_desc d{HDD_CUBE, 3520, 1200, 8, 8, HDD_BOUNDARY_ALL_DIRICHLET, 0, {0.0, 0.0}, {5.0, 1.0}};
+    hdd_grid* g = nullptr;
+    if (hdd_grid_create_structured(&d, &g) != HDD_OK) return 1;
+    std::vector<double> perm(2000);
+    for (int i = 0; i < 2000; ++i) perm[size_t(i)] = std::pow(10.0, -3.0 + 6.0 * std::fmod(0.618033988749895 * i, 1.0));
+    {
+      Discretizations::BlockSWIPDG block(g, Problems::Spe10Model1(perm, {}, {}, false));
+      block.init();
+      (void)hipDeviceSynchronize();
+      std::vector<std::pair<int, int>> pairs;
+      for (int ss = 0; ss < block.num_subdomains(); ++ss) {
+        pairs.push_back({ss, ss});
+        for (int nn : block.neighbouring_subdomains(ss)) pairs.push_back({ss, nn});
+      }
+      std::vector<Discretizations::AffinelyDecomposedMatrix> one;
+      for (int rep = 0; rep < 2; ++rep) {   // (the second pass: allocator warm)
+        one.clear();
+        const auto t0 = std::chrono::steady_clock::now();
+        for (const auto& p : pairs)
+          one.push_back(p.first == p.second ? block.get_local_operator(p.first) : block.get_coupling_operator(p.first, p.second));
+        (void)hipDeviceSynchronize();
+        std::printf("c4 ops one-by-one: %zu operators %.2f ms\n", pairs.size(),
+                    1e3 * std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
+      }
+      const auto t0 = std::chrono::steady_clock::now();
+      const auto& all = block.extract_operators();
+      (void)hipDeviceSynchronize();
+      const double ms = 1e3 * std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      int64_t nnz = 0;
+      bool same = all.size() == pairs.size();
+      for (size_t k = 0; k < pairs.size() && same; ++k) {
+        const auto& b = all.at(pairs[k]);
+        const auto& a = one[k];
+        nnz += b.pattern->nnz;
+        same = a.pattern->nnz == b.pattern->nnz &&
+               checksum(a.pattern->d_row_ptr, a.pattern->rows + 1) == checksum(b.pattern->d_row_ptr, b.pattern->rows + 1) &&
+               checksum(a.pattern->d_col, a.pattern->nnz) == checksum(b.pattern->d_col, b.pattern->nnz) &&
+               checksum(*a.affine, a.pattern->nnz) == checksum(*b.affine, b.pattern->nnz);
+      }
+      std::printf("c4 ops batched: %zu operators nnz %lld %.2f ms equal %d\n", all.size(), (long long)nnz, ms, int(same));
+    }
+    hdd_grid_destroy(g);
+    return 0;
+  }
   if (which == "c2") {
     S::Grid::Providers::Cube provider(HDD_SIMPLEX, {0.0, 0.0}, {5.0, 1.0}, {3200, 640});
     std::vector<double> perm(2000);
@@ -139,6 +185,20 @@ int main(int argc, char** argv)
     std::vector<std::vector<double>> locals;
     for (int ss = 0; ss < block.num_subdomains(); ++ss) locals.push_back(block.localize_vector(x, ss));
     std::printf("roundtrip %d\n", int(block.globalize_vectors(locals) == x));
+    // every operator at once (extract_operators): the same arrays as the one-by-one extraction above
+    {
+      const auto& all = block.extract_operators();
+      const auto& L2 = all.at({0, 0});
+      const auto& C2 = all.at({0, nbs.at(0)});
+      auto l2v = L2.affine_part();
+      auto c2v = C2.affine_part();
+      const bool same = L2.pattern->row_ptr() == L.pattern->row_ptr() && L2.pattern->col() == L.pattern->col() &&
+                        l2v == lv && C2.pattern->row_ptr() == C.pattern->row_ptr() &&
+                        C2.pattern->col() == C.pattern->col() && c2v == cv &&
+                        L2.freeze_parameter(0.5) == L.freeze_parameter(0.5) &&
+                        block.get_coupling_operator(0, nbs.at(0)).pattern == C2.pattern;
+      std::printf("batched operators %zu same %d\n", all.size(), int(same));
+    }
     try {
       block.get_coupling_operator(0, 3);   // diagonal subdomain: not a face neighbour
       std::printf("coupling(0,3) unexpectedly allowed\n");

@@ -355,6 +355,26 @@ int hdd_block_operator_values_device(hdd_ctx* ctx, const hdd_csr* pattern, int64
                                      int64_t col_begin, int64_t col_end, const int64_t* d_out_row_ptr,
                                      const double* const* d_vals, int32_t n_comp, double* const* d_out, void* stream);
 
+/* Batched: n_ops operators of one pattern in four launches (count, one scan over all, bases, fill) -- e.g.
+ * every get_local_operator / get_coupling_operator of a BlockSWIPDG at once.  Outputs are concatenated:
+ * operator k's row pointer [rows_k + 1] (operator-relative, starting at 0) is at d_out_row_ptr + row_off_k,
+ * row_off_k = sum_{j<k} (rows_j + 1); its local columns / source positions at d_out_col / d_out_src +
+ * nnz_off[k] (either may be NULL), nnz_off[k+1] = nnz_off[k] + nnz_k + (nnz_k & 1): every operator starts
+ * 16-byte aligned in the value arrays (one padding entry after an odd count, left unwritten).  nnz_off (host
+ * [n_ops + 1], nnz_off[n_ops] = the padded total) is returned when non-NULL, which synchronises `stream`; a
+ * caller that knows the counts (from the mesh: nb^2 x face pairs, + nb^2 |ss| on the diagonal) passes NULL
+ * and stays asynchronous.  sum_k (rows_k + 1) < 2^31. */
+typedef struct {
+  int64_t row_begin, row_end, col_begin, col_end;
+} hdd_block_range;
+int hdd_block_operators_map_device(hdd_ctx* ctx, const hdd_csr* pattern, int32_t n_ops, const hdd_block_range* ops,
+                                   int64_t* d_out_row_ptr, int32_t* d_out_col, int64_t* d_out_src, int64_t* nnz_off,
+                                   void* stream);
+/* the operators' values of n_comp value arrays (concatenated like the columns; nnz_off host [n_ops + 1]) */
+int hdd_block_operators_values_device(hdd_ctx* ctx, const hdd_csr* pattern, int32_t n_ops, const hdd_block_range* ops,
+                                      const int64_t* nnz_off, const int64_t* d_out_row_ptr, const double* const* d_vals,
+                                      int32_t n_comp, double* const* d_out, void* stream);
+
 /* ---------------------------------------------------------------------------------------------- */
 /* sharded BlockSWIPDG (SURVEY.md 8(b) hdd_block_assemble_sharded, 8(e)): one process (or thread) per  */
 /* GPU owns a contiguous range of subdomains and assembles their rows -- A_ss and A_ss,nn are written  */

@@ -210,19 +210,21 @@ class DeviceArray {
   DeviceArray() = default;
   explicit DeviceArray(size_t n) : n_(n) { if (n) hip_check(hipMalloc(&p_, n * sizeof(T)), "hipMalloc"); }
   DeviceArray(const std::vector<T>& h) : DeviceArray(h.size()) { upload(h); }
+  // a view of n elements inside an allocation that `owner` keeps alive (batched block operators)
+  DeviceArray(T* p, size_t n, std::shared_ptr<const void> owner) : p_(p), n_(n), owner_(std::move(owner)) {}
   DeviceArray(const DeviceArray&) = delete;
   DeviceArray& operator=(const DeviceArray&) = delete;
-  DeviceArray(DeviceArray&& o) noexcept : p_(o.p_), n_(o.n_) { o.p_ = nullptr; o.n_ = 0; }
+  DeviceArray(DeviceArray&& o) noexcept : p_(o.p_), n_(o.n_), owner_(std::move(o.owner_)) { o.p_ = nullptr; o.n_ = 0; }
   DeviceArray& operator=(DeviceArray&& o) noexcept
   {
     if (this != &o) {
-      if (p_) (void)hipFree(p_);
-      p_ = o.p_; n_ = o.n_;
+      release();
+      p_ = o.p_; n_ = o.n_; owner_ = std::move(o.owner_);
       o.p_ = nullptr; o.n_ = 0;
     }
     return *this;
   }
-  ~DeviceArray() { if (p_) (void)hipFree(p_); }
+  ~DeviceArray() { release(); }
   void upload(const std::vector<T>& h) { hip_check(hipMemcpy(p_, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice), "H2D"); }
   std::vector<T> download() const
   {
@@ -233,8 +235,14 @@ class DeviceArray {
   T* get() const { return p_; }
   size_t size() const { return n_; }
  private:
+  void release()
+  {
+    if (p_ && !owner_) (void)hipFree(p_);
+    owner_.reset();
+  }
   T* p_ = nullptr;
   size_t n_ = 0;
+  std::shared_ptr<const void> owner_;   // set for views: the allocation is the owner's
 };
 using Timer = std::chrono::steady_clock;
 inline double seconds_since(Timer::time_point t0)
@@ -1208,6 +1216,84 @@ class BlockSWIPDG : public SWIPDG {
 
   AffinelyDecomposedMatrix get_local_operator(int ss) const { return extract(ss, ss); }
 
+  // Every local and coupling operator at once (hdd_block_operators_map_device / _values_device: five
+  // launches whatever their number, asynchronous -- the counts come from the face pairs counted at
+  // construction).  Their patterns and values are views into one row-pointer, one column and one value array
+  // per component (together the size of the system matrix); afterwards get_local_operator /
+  // get_coupling_operator return these instead of extracting one by one.  The LRBMS consumer
+  // (pyMOR's BlockSWIPDG wrapper) asks for all of them.
+  const std::map<std::pair<int, int>, AffinelyDecomposedMatrix>& extract_operators() const
+  {
+    if (!operators_.empty()) return operators_;
+    const auto& M = system_matrix();
+    const int64_t nb = info_.nb;
+    std::vector<std::pair<int, int>> pairs;
+    std::vector<hdd_block_range> rng;
+    std::vector<int64_t> rows, nnz, noff{0}, roff{0};
+    for (int ss = 0; ss < num_subdomains(); ++ss) {
+      std::vector<int> nns(neighbours_[size_t(ss)].begin(), neighbours_[size_t(ss)].end());
+      nns.push_back(ss);
+      std::sort(nns.begin(), nns.end());
+      int64_t a, b;
+      internal::check(hdd_grid_subdomain_range(grid_, ss, ss + 1, &a, &b), "range");
+      for (int nn : nns) {
+        int64_t c, d;
+        internal::check(hdd_grid_subdomain_range(grid_, nn, nn + 1, &c, &d), "range");
+        const auto fp = face_pairs_.find({ss, nn});
+        const int64_t n = nb * nb * ((fp == face_pairs_.end() ? 0 : fp->second) + (ss == nn ? b - a : 0));
+        pairs.push_back({ss, nn});
+        rng.push_back(hdd_block_range{a * nb, b * nb, c * nb, d * nb});
+        rows.push_back((b - a) * nb);
+        nnz.push_back(n);
+        noff.push_back(noff.back() + n + (n & 1));
+        roff.push_back(roff.back() + (b - a) * nb + 1);
+      }
+    }
+    const int32_t n_ops = int32_t(pairs.size());
+    auto rp = std::make_shared<internal::DeviceArray<int64_t>>(size_t(roff.back()));
+    auto col = std::make_shared<internal::DeviceArray<int32_t>>(size_t(noff.back()) + 1);
+    const hdd_csr pat = pattern_->csr();
+    internal::check(hdd_block_operators_map_device(ctx_, &pat, n_ops, rng.data(), rp->get(), col->get(), nullptr,
+                                                   nullptr, nullptr), "hdd_block_operators_map_device");
+    std::vector<std::shared_ptr<internal::DeviceArray<double>>> all;   // affine first, then the components
+    std::vector<const double*> in;
+    std::vector<double*> res;
+    auto slot = [&](const internal::DeviceArray<double>& v) {
+      all.push_back(std::make_shared<internal::DeviceArray<double>>(size_t(noff.back()) + 1));
+      in.push_back(v.get());
+      res.push_back(all.back()->get());
+    };
+    if (M.affine) slot(*M.affine);
+    for (const auto& q : M.comps) slot(*q);
+    for (size_t i0 = 0; i0 < in.size(); i0 += HDD_MAX_COMP) {
+      const int32_t k = int32_t(std::min<size_t>(HDD_MAX_COMP, in.size() - i0));
+      internal::check(hdd_block_operators_values_device(ctx_, &pat, n_ops, rng.data(), noff.data(), rp->get(),
+                                                        in.data() + i0, k, res.data() + i0, nullptr),
+                      "hdd_block_operators_values_device");
+    }
+    for (int32_t k = 0; k < n_ops; ++k) {
+      auto P = std::make_shared<Pattern>();
+      P->rows = rows[size_t(k)];
+      P->cols = rng[size_t(k)].col_end - rng[size_t(k)].col_begin;
+      P->nnz = nnz[size_t(k)];
+      P->d_row_ptr = internal::DeviceArray<int64_t>(rp->get() + roff[size_t(k)], size_t(P->rows + 1), rp);
+      P->d_col = internal::DeviceArray<int32_t>(col->get() + noff[size_t(k)], size_t(P->nnz), col);
+      AffinelyDecomposedMatrix out;
+      out.pattern = P;
+      out.ctx = ctx_;
+      out.coefficients = M.coefficients;
+      auto view = [&](size_t i) {
+        return std::make_shared<internal::DeviceArray<double>>(all[i]->get() + noff[size_t(k)],
+                                                               size_t(P->nnz + (P->nnz & 1)), all[i]);
+      };
+      size_t i = 0;
+      if (M.affine) out.affine = view(i++);
+      for (; i < all.size(); ++i) out.comps.push_back(view(i));
+      operators_.emplace(pairs[size_t(k)], std::move(out));
+    }
+    return operators_;
+  }
+
   AffinelyDecomposedMatrix get_coupling_operator(int ss, int nn) const
   {
     range_check(ss);
@@ -1365,6 +1451,8 @@ class BlockSWIPDG : public SWIPDG {
   {
     range_check(ss);
     range_check(nn);
+    const auto it = operators_.find({ss, nn});
+    if (it != operators_.end()) return it->second;   // extract_operators() ran
     const auto& M = system_matrix();
     int64_t a, b, c, d;
     internal::check(hdd_grid_subdomain_range(grid_, ss, ss + 1, &a, &b), "range");
@@ -1427,6 +1515,7 @@ class BlockSWIPDG : public SWIPDG {
   int oversampling_layers_ = 0;
   std::vector<std::set<int>> neighbours_;
   std::map<std::pair<int, int>, int64_t> face_pairs_;   // (ss, nn) -> element-face pairs (operator nnz / nb^2)
+  mutable std::map<std::pair<int, int>, AffinelyDecomposedMatrix> operators_;   // extract_operators()
   mutable std::vector<std::shared_ptr<SWIPDG>> local_discretizations_;
   mutable std::map<std::pair<int, std::string>, std::shared_ptr<SWIPDG>> oversampled_;
 };

@@ -533,3 +533,31 @@ def test_penalty_exponent_beta(ctx, et, smooth):
     assert ok, worst
     _, _, (v1,) = _run_product(ctx, grid, fns, ten)   # beta = 1 differs (the exponent is really applied)
     assert not np.allclose(v1, val)
+
+
+@pytest.mark.parametrize("et", [H.SIMPLEX, H.CUBE])
+def test_element_list_bitwise(ctx, et):
+    """hdd_swipdg_assemble_elements over every owned element == hdd_swipdg_assemble, bit for bit, for every
+    tensor kind x diffusion-factor kind of the persistent policies (the sharded step's fixup relies on it;
+    -ffp-contract=on makes a formula round the same in both kernels, profiles/r03/fp_contract.log)"""
+    torch = _torch()
+    rng = np.random.default_rng(1)
+    grid = H.Grid.structured(et, 96, 40, (0, 0), (5, 1), px=4, py=2)
+    loc = grid.local(2, 6)
+    dm, dp = H.DeviceMesh(loc), H.DevicePattern(loc)
+    n = loc.n_local
+    iso = torch.from_numpy(rng.uniform(0.5, 2, n)).cuda()
+    sym = torch.from_numpy(np.stack([rng.uniform(1, 2, n), rng.uniform(-.3, .3, n), rng.uniform(1, 2, n)])).cuda()
+    kpe = torch.from_numpy(rng.uniform(0.5, 2, n)).cuda()
+    lst = torch.arange(loc.n_own, dtype=torch.int32, device="cuda")
+    sin = lambda c, b: H.scalar_fn(H.FN_SINUSOID, c, b=b, kx=3.0, ky=2.0, order=3)
+    for ten in [H.tensor_fn(H.TENSOR_ISO_PER_ELEM, per_elem=iso), H.tensor_fn(H.TENSOR_SYM_PER_ELEM, per_elem=sym),
+                H.tensor_fn()]:
+        for kap in [[H.scalar_fn(H.FN_CONST, 1.0)], [H.scalar_fn(H.FN_PER_ELEM, per_elem=kpe)], [sin(1.0, 0.5)],
+                    [sin(1.0, 0.5), sin(0.0, 1.0)]]:
+            ref = H.assemble(ctx, dm, dp, kap, ten)
+            vals = [torch.full_like(r, float("nan")) for r in ref]
+            H.assemble_tiles(ctx, dm, dp, kap, ten, lst, vals, elements=True)
+            torch.cuda.synchronize()
+            for v, r in zip(vals, ref):
+                assert torch.equal(v, r), (ten.kind, [k.kind for k in kap])
