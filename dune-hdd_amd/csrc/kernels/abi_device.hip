@@ -997,6 +997,24 @@ __device__ __forceinline__ int op_of_slot(const OpDesc* d, int n_ops, int64_t x)
   return lo;
 }
 
+// the sub-range [lo, lo + len) of sorted row [a, b) with columns in [c0, c1): most rows of a coupling operator
+// lie wholly outside (first / last column decide, two independent loads), only the rest binary-search
+__device__ __forceinline__ void row_range(const int32_t* __restrict__ col, int64_t a, int64_t b, int64_t c0,
+                                          int64_t c1, int64_t& lo, int64_t& len)
+{
+  lo = a;
+  len = 0;
+  if (a == b) return;
+  const int64_t first = col[a], last = col[b - 1];
+  if (last < c0 || first >= c1) return;
+  if (first >= c0 && last < c1) {
+    len = b - a;
+    return;
+  }
+  lo = lower_bound_col(col, a, b, c0);
+  len = lower_bound_col(col, lo, b, c1) - lo;
+}
+
 __global__ void __launch_bounds__(256) ops_count_kernel(const int64_t* __restrict__ rp, const int32_t* __restrict__ col,
                                                         const OpDesc* __restrict__ d, int n_ops, int64_t n_slots,
                                                         int64_t* __restrict__ out)
@@ -1004,70 +1022,141 @@ __global__ void __launch_bounds__(256) ops_count_kernel(const int64_t* __restric
   for (int64_t x = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; x < n_slots; x += int64_t(gridDim.x) * blockDim.x) {
     const OpDesc o = d[op_of_slot(d, n_ops, x)];
     const int64_t j = x - o.roff;
-    int64_t c = 0;
-    if (j > 0) {
-      const int64_t a = rp[o.r0 + j - 1], b = rp[o.r0 + j];
-      const int64_t lo = lower_bound_col(col, a, b, o.c0);
-      c = lower_bound_col(col, lo, b, o.c1) - lo;
-    }
+    int64_t lo = 0, c = 0;
+    if (j > 0) row_range(col, rp[o.r0 + j - 1], rp[o.r0 + j], o.c0, o.c1, lo, c);
     out[x] = c;
   }
 }
 
-__global__ void ops_base_kernel(const int64_t* __restrict__ scanned, OpDesc* d, int n_ops, int64_t* __restrict__ totals)
+// one wave: bases and even-rounded offsets of 64 operators per step (loads in parallel, a wave prefix sum)
+__global__ void __launch_bounds__(64) ops_base_kernel(const int64_t* __restrict__ scanned, OpDesc* d, int n_ops,
+                                                      int64_t* __restrict__ totals)
 {
-  if (blockIdx.x != 0 || threadIdx.x != 0) return;
-  int64_t noff = 0;   // a serial pass over the operators (thousands at most)
-  for (int k = 0; k < n_ops; ++k) {
-    const int64_t b = scanned[d[k].roff];
-    const int64_t n = scanned[d[k].roff + d[k].rows] - b;
-    d[k].base = b;
-    d[k].noff = noff;
-    if (totals) totals[k] = noff;
-    noff += n + (n & 1);
+  const int lane = threadIdx.x;
+  int64_t carry = 0;
+  for (int k0 = 0; k0 < n_ops; k0 += 64) {
+    const int k = k0 + lane;
+    int64_t b = 0, n = 0;
+    if (k < n_ops) {
+      b = scanned[d[k].roff];
+      n = scanned[d[k].roff + d[k].rows] - b;
+    }
+    int64_t incl = n + (n & 1);
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int64_t v = __shfl_up(incl, off, 64);
+      if (lane >= off) incl += v;
+    }
+    const int64_t noff = carry + incl - (n + (n & 1));
+    if (k < n_ops) {
+      d[k].base = b;
+      d[k].noff = noff;
+      if (totals) totals[k] = noff;
+    }
+    carry += __shfl(incl, 63, 64);
   }
-  if (totals) totals[n_ops] = noff;
+  if (totals && lane == 0) totals[n_ops] = carry;
 }
 
-// columns (local) / sources at the global positions, then the row pointer made operator-relative in place
+// Wave-cooperative copy of the 64 row segments a wave holds (lane l: len[l] entries): the segments' entries
+// are numbered through a wave prefix sum and every lane takes entries lane, lane + 64, ...; copy(seg, off)
+// handles entry off of segment seg.  Consecutive lanes then write consecutive positions of the
+// (operator-contiguous) destination and read runs of the source, instead of 64 lanes each walking its own row
+// (64 cache lines per instruction).  Whole waves call it (the slot loops below are wave-uniform).
+template <class F>
+__device__ __forceinline__ void wave_segments(int len, int* s_end, F&& copy)
+{
+  const int lane = threadIdx.x & 63;
+  int incl = len;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int v = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += v;
+  }
+  s_end[lane] = incl;
+  const int total = __shfl(incl, 63, 64);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  for (int p = lane; p < total; p += 64) {
+    int lo = 0, hi = 63;   // the first segment whose inclusive end exceeds p
+    while (lo < hi) {
+      const int m = (lo + hi) >> 1;
+      if (s_end[m] > p) hi = m;
+      else lo = m + 1;
+    }
+    copy(lo, p - (lo ? s_end[lo - 1] : 0));
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+struct SegShared {
+  int64_t src[4][64], dst[4][64], c0[4][64];
+  int end[4][64];
+};
+
+// columns (local) / sources at the operators' positions, then the row pointer made operator-relative in place
 // (each slot reads only itself: its count is recomputed, the base comes from the descriptor)
 __global__ void __launch_bounds__(256) ops_fill_kernel(const int64_t* __restrict__ rp, const int32_t* __restrict__ col,
                                                        const OpDesc* __restrict__ d, int n_ops, int64_t n_slots,
                                                        int64_t* __restrict__ out_rp, int32_t* __restrict__ out_col,
                                                        int64_t* __restrict__ out_src)
 {
-  for (int64_t x = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; x < n_slots; x += int64_t(gridDim.x) * blockDim.x) {
-    const OpDesc o = d[op_of_slot(d, n_ops, x)];
-    const int64_t j = x - o.roff;
-    const int64_t end = out_rp[x] - o.base;   // operator-relative end of row j - 1
-    if (j > 0 && (out_col || out_src)) {
-      const int64_t a = rp[o.r0 + j - 1], b = rp[o.r0 + j];
-      const int64_t lo = lower_bound_col(col, a, b, o.c0);
-      const int64_t len = lower_bound_col(col, lo, b, o.c1) - lo;
-      for (int64_t i = 0; i < len; ++i) {
-        const int64_t g = o.noff + end - len + i;
-        if (out_col) out_col[g] = int32_t(int64_t(col[lo + i]) - o.c0);
-        if (out_src) out_src[g] = lo + i;
-      }
+  __shared__ SegShared sh;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int64_t xb = int64_t(blockIdx.x) * blockDim.x; xb < n_slots; xb += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t x = xb + threadIdx.x;
+    int64_t lo = 0, len = 0, dst = 0, c0 = 0;
+    if (x < n_slots) {
+      const OpDesc o = d[op_of_slot(d, n_ops, x)];
+      const int64_t j = x - o.roff;
+      const int64_t end = out_rp[x] - o.base;   // operator-relative end of row j - 1
+      if (j > 0) row_range(col, rp[o.r0 + j - 1], rp[o.r0 + j], o.c0, o.c1, lo, len);
+      dst = o.noff + end - len;
+      c0 = o.c0;
+      out_rp[x] = end;
     }
-    out_rp[x] = end;
+    if (out_col || out_src) {
+      sh.src[w][lane] = lo;
+      sh.dst[w][lane] = dst;
+      sh.c0[w][lane] = c0;   // a wave's segments may belong to two operators
+      wave_segments(int(len), sh.end[w], [&](int seg, int off) {
+        const int64_t si = sh.src[w][seg] + off, di = sh.dst[w][seg] + off;
+        if (out_col) out_col[di] = int32_t(int64_t(col[si]) - sh.c0[w][seg]);
+        if (out_src) out_src[di] = si;
+      });
+    }
   }
 }
 
-// values: thread per row slot; operator k's entries at noff_k + its (relative) row pointer
+// values: operator k's entries at noff_k + its (relative) row pointer, copied wave-cooperatively
 __global__ void __launch_bounds__(256) ops_values_kernel(const int64_t* __restrict__ rp, const int32_t* __restrict__ col,
                                                          const OpDesc* __restrict__ d, int n_ops, int64_t n_slots,
                                                          const int64_t* __restrict__ out_rp, ValPtrs v, int nc)
 {
-  for (int64_t x = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; x < n_slots; x += int64_t(gridDim.x) * blockDim.x) {
-    const OpDesc o = d[op_of_slot(d, n_ops, x)];
-    const int64_t j = x - o.roff;
-    if (j == 0) continue;
-    const int64_t k0 = o.noff + out_rp[x - 1], len = out_rp[x] - out_rp[x - 1];
-    if (len == 0) continue;
-    const int64_t lo = lower_bound_col(col, rp[o.r0 + j - 1], rp[o.r0 + j], o.c0);
-    for (int c = 0; c < nc; ++c)
-      for (int64_t i = 0; i < len; ++i) v.out[c][k0 + i] = v.in[c][lo + i];
+  __shared__ SegShared sh;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int64_t xb = int64_t(blockIdx.x) * blockDim.x; xb < n_slots; xb += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t x = xb + threadIdx.x;
+    int64_t lo = 0, len = 0, dst = 0;
+    if (x < n_slots) {
+      const OpDesc o = d[op_of_slot(d, n_ops, x)];
+      const int64_t j = x - o.roff;
+      if (j > 0) {
+        const int64_t r0 = out_rp[x - 1];
+        len = out_rp[x] - r0;
+        dst = o.noff + r0;
+        if (len) lo = lower_bound_col(col, rp[o.r0 + j - 1], rp[o.r0 + j], o.c0);
+      }
+    }
+    sh.src[w][lane] = lo;
+    sh.dst[w][lane] = dst;
+    wave_segments(int(len), sh.end[w], [&](int seg, int off) {
+      const int64_t si = sh.src[w][seg] + off, di = sh.dst[w][seg] + off;
+      for (int c = 0; c < nc; ++c) v.out[c][di] = v.in[c][si];
+    });
   }
 }
 }  // namespace

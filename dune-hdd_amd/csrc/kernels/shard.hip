@@ -403,12 +403,19 @@ struct hdd_shard {
   // host copies of the plan (hdd_shard_halo_lists / hdd_shard_tile_lists)
   std::vector<int32_t> send_idx, tiles_in, tiles_bd;
   bool host_only = false;          // created without a context: no device arrays
+  // side stream of the loopback study (HDD_SHARD_NO_TRANSFER): pack + copies off the assembly stream, as the
+  // RCCL path runs them on the transfer stream; created on first use
+  hipStream_t aux = nullptr;
+  hipEvent_t ev_in = nullptr, ev_out = nullptr;
 };
 
 extern "C" void hdd_shard_destroy(hdd_shard* sh)
 {
   if (!sh) return;
   if (!sh->host_only) (void)hipSetDevice(sh->device);
+  if (sh->aux) (void)hipStreamDestroy(sh->aux);
+  if (sh->ev_in) (void)hipEventDestroy(sh->ev_in);
+  if (sh->ev_out) (void)hipEventDestroy(sh->ev_out);
   for (void* p : {static_cast<void*>(sh->d_coords), static_cast<void*>(sh->d_nbrs), static_cast<void*>(sh->d_finfo),
                   static_cast<void*>(sh->d_gid), static_cast<void*>(sh->d_send_idx), static_cast<void*>(sh->d_sbuf),
                   static_cast<void*>(sh->d_rbuf), static_cast<void*>(sh->d_tiles_in),
@@ -715,11 +722,38 @@ extern "C" int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm*
 
   hipError_t e = hipSetDevice(sh->device);
   if (e != hipSuccess) return hip_fail(e, "hdd_block_assemble_sharded: hipSetDevice");
+  const bool split = (flags & HDD_SHARD_SPLIT_TILES) != 0;
+  bool overlap = !(flags & HDD_SHARD_NO_OVERLAP) && sh->gi.elem_type != HDD_HEX && (split ? sh->n_in > 0 : true);
+  // The pack and the transfer leave the assembly stream when the assembly overlaps them: the RCCL transfer
+  // stream (or, in the loopback study, the shard's side stream) waits for the inputs, packs and sends while
+  // `stream` starts the assembly at once -- the pack launch is off the critical path.  (The host transport
+  // stages through the host on `stream` anyway.)
+  hipStream_t ps = s;
+  if (overlap && !split && (transfer ? comm->kind != hdd_comm::HOST : true)) {
+    if (transfer) {
+      ps = comm->xfer;
+    } else {
+      if (!sh->aux) {
+        e = hipStreamCreateWithFlags(&sh->aux, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&sh->ev_in, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&sh->ev_out, hipEventDisableTiming);
+        if (e != hipSuccess) return hip_fail(e, "hdd_block_assemble_sharded: side stream");
+      }
+      ps = sh->aux;
+    }
+    if (!sh->ev_in) {
+      e = hipEventCreateWithFlags(&sh->ev_in, hipEventDisableTiming);
+      if (e != hipSuccess) return hip_fail(e, "hdd_block_assemble_sharded: event");
+    }
+    e = hipEventRecord(sh->ev_in, s);
+    if (e == hipSuccess) e = hipStreamWaitEvent(ps, sh->ev_in, 0);
+    if (e != hipSuccess) return hip_fail(e, "hdd_block_assemble_sharded: order pack after inputs");
+  }
   // 1. pack the records the peers need (one launch for every peer)
   for (int k = 0; k <= h.n_peers; ++k) h.prefix[k] = sh->send_prefix[k];
   h.idx = sh->d_send_idx;
   h.buf = sh->d_sbuf;
-  e = launch_halo(true, h, s);
+  e = launch_halo(true, h, ps);
   if (e != hipSuccess) return hip_fail(e, "hdd_block_assemble_sharded: pack");
   // 2. post the exchange.  The receives land straight in the ghost columns: the ghosts of one owner are
   // contiguous (recv_col0), so peer k's message is R row messages [row r][count_k], each received into
@@ -744,7 +778,7 @@ extern "C" int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm*
         mrn.push_back(rcnt);
       }
     }
-    rc = hdd_comm_post(comm, int32_t(mp.size()), mp.data(), ms.data(), mn.data(), mr.data(), mrn.data(), stream);
+    rc = hdd_comm_post(comm, int32_t(mp.size()), mp.data(), ms.data(), mn.data(), mr.data(), mrn.data(), ps);
   } else {   // timing studies: the receive buffers get this rank's own messages (stream-ordered device copies)
     std::vector<const double*> sp(size_t(h.n_peers));
     std::vector<double*> rp(size_t(h.n_peers));
@@ -757,17 +791,17 @@ extern "C" int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm*
     }
     for (int k = 0; k < h.n_peers && rc == HDD_OK; ++k) {
       const int64_t n = std::min(sn[k], rn[k]);
-      if (n > 0 && hipMemcpyAsync(rp[k], sp[k], size_t(n) * sizeof(double), hipMemcpyDeviceToDevice, s) != hipSuccess)
+      if (n > 0 && hipMemcpyAsync(rp[k], sp[k], size_t(n) * sizeof(double), hipMemcpyDeviceToDevice, ps) != hipSuccess)
         rc = set_error(HDD_ERR_HIP, "hdd_block_assemble_sharded: loopback copy");
     }
+    if (rc == HDD_OK && ps != s && hipEventRecord(sh->ev_out, ps) != hipSuccess)
+      rc = set_error(HDD_ERR_HIP, "hdd_block_assemble_sharded: loopback event");
   }
   if (rc) return rc;
   // 3. the assembly overlaps the transfer.  Default: EVERY tile (one full-size launch at full rate; the row
   // blocks of the ghost-adjacent elements read ghost columns the receives are still writing and are recomputed
   // in 5).  HDD_SHARD_SPLIT_TILES: the interior tiles only (the kernels that take lists: P1 / Q1 persistent
   // policies) -- a second launch of whole boundary tiles later, which on thin strips is a large fraction.
-  const bool split = (flags & HDD_SHARD_SPLIT_TILES) != 0;
-  bool overlap = !(flags & HDD_SHARD_NO_OVERLAP) && sh->gi.elem_type != HDD_HEX && (split ? sh->n_in > 0 : true);
   if (overlap) {
     rc = split ? hdd_swipdg_assemble_tiles(ctx, &m, kappa, n_comp, tensor, params, pattern, d_vals, sh->d_tiles_in,
                                            sh->n_in, stream)
@@ -783,6 +817,8 @@ extern "C" int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm*
     rc = hdd_comm_wait(comm, stream);
     if (rc) return rc;
   } else {
+    if (ps != s && hipStreamWaitEvent(s, sh->ev_out, 0) != hipSuccess)
+      return set_error(HDD_ERR_HIP, "hdd_block_assemble_sharded: wait loopback");
     for (int k = 0; k <= h.n_peers; ++k) h.prefix[k] = sh->recv_prefix[k];
     for (int k = 0; k < h.n_peers; ++k) h.col0[k] = sh->recv_col0[k];
     h.idx = nullptr;

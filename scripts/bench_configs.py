@@ -198,6 +198,19 @@ def ops(args):
         res["device_ms_" + ("known_nnz" if known else "sync_nnz")] = float(np.median(ts)) * 1e3
     n = sum(int(o[1].numel()) for o in out)
     assert n == sum(nnz_of[p] for p in pairs)
+    # (iii) all operators in one batched call (hdd_block_operators_map_device / _values_device)
+    for known in (False, True):
+        H.block_operators(ctx, grid, dp, [vals], pairs, nnz=nnz_of if known else None)
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(max(3, args.steps // 4)):
+            t0 = time.perf_counter()
+            b = H.block_operators(ctx, grid, dp, [vals], pairs, nnz=nnz_of if known else None)
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        res["batched_ms_" + ("known_nnz" if known else "sync_nnz")] = float(np.median(ts)) * 1e3
+    for p, o in zip(pairs, out):
+        assert all(torch.equal(x, y) for x, y in zip(b[p][:2], o[:2])) and torch.equal(b[p][2][0], o[2][0])
     rp, col, _ = dp.host
     t0 = time.perf_counter()
     for ss, nn in pairs:
@@ -211,7 +224,8 @@ def ops(args):
     t_host = time.perf_counter() - t0
     return dict(config="ops_block_swipdg_q1_%dx%d_8x8" % (nx, ny), operators=len(pairs), values=n, global_nnz=dp.nnz,
                 nnz_host_pass_s=t_nnz, host_map_s=t_host, **res,
-                device_GBps_known_nnz=(8 + 8 + 4) * n / (res["device_ms_known_nnz"] * 1e-3) / 1e9)
+                device_GBps_known_nnz=(8 + 8 + 4) * n / (res["device_ms_known_nnz"] * 1e-3) / 1e9,
+                batched_GBps_known_nnz=(8 + 8 + 4) * n / (res["batched_ms_known_nnz"] * 1e-3) / 1e9)
 
 
 def c5(args):
