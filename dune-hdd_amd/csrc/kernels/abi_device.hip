@@ -592,30 +592,21 @@ extern "C" int hdd_pattern_elem_ptr_device(hdd_ctx* ctx, const hdd_mesh* m, int3
   if (e != hipSuccess) return hip_fail(e, "hdd_pattern_elem_ptr_device: hipSetDevice");
   const hipStream_t s = static_cast<hipStream_t>(stream);
   const int64_t n_own = m->own_end - m->own_begin;
-  e = hipMemsetAsync(d_elem_ptr, 0, sizeof(int64_t), s);
-  if (e != hipSuccess) return hip_fail(e, "hdd_pattern_elem_ptr_device: memset");
-  if (n_own > 0) {
-    e = hdd::dev::launch_pattern_counts(m->neighbors, nf, m->n_local, m->own_begin, m->own_end, int64_t(nb) * nb,
-                                        d_elem_ptr + 1, s);
-    if (e != hipSuccess) return hip_fail(e, "hdd_pattern_elem_ptr_device: counts");
-    size_t tmp_bytes = 0;
-    e = hipcub::DeviceScan::InclusiveSum(nullptr, tmp_bytes, d_elem_ptr + 1, d_elem_ptr + 1, n_own, s);
-    if (e != hipSuccess) return hip_fail(e, "hdd_pattern_elem_ptr_device: scan size");
-    if (tmp_bytes > ctx->scan_ws_bytes) {   // the context keeps the scratch (one stream at a time per context)
-      (void)hipStreamSynchronize(s);
-      if (ctx->scan_ws) (void)hipFree(ctx->scan_ws);
-      ctx->scan_ws = nullptr;
-      ctx->scan_ws_bytes = 0;
-      e = hipMalloc(&ctx->scan_ws, tmp_bytes);
-      if (e != hipSuccess) return hip_fail(e, "hdd_pattern_elem_ptr_device: scan scratch");
-      ctx->scan_ws_bytes = tmp_bytes;
-    }
-    e = hipcub::DeviceScan::InclusiveSum(ctx->scan_ws, tmp_bytes, d_elem_ptr + 1, d_elem_ptr + 1, n_own, s);
-    const hipError_t e2 = hipStreamSynchronize(s);
-    if (e != hipSuccess) return hip_fail(e, "hdd_pattern_elem_ptr_device: scan");
-    if (e2 != hipSuccess) return hip_fail(e2, "hdd_pattern_elem_ptr_device: synchronize");
+  const size_t tmp_bytes = size_t(hdd::dev::pattern_elem_ptr_scratch(n_own) + 1) * sizeof(int64_t);
+  if (tmp_bytes > ctx->scan_ws_bytes) {   // the context keeps the scratch (one stream at a time per context)
+    (void)hipStreamSynchronize(s);
+    if (ctx->scan_ws) (void)hipFree(ctx->scan_ws);
+    ctx->scan_ws = nullptr;
+    ctx->scan_ws_bytes = 0;
+    e = hipMalloc(&ctx->scan_ws, tmp_bytes);
+    if (e != hipSuccess) return hip_fail(e, "hdd_pattern_elem_ptr_device: scan scratch");
+    ctx->scan_ws_bytes = tmp_bytes;
   }
-  e = hipMemcpy(nnz, d_elem_ptr + n_own, sizeof(int64_t), hipMemcpyDeviceToHost);
+  e = hdd::dev::launch_pattern_elem_ptr(m->neighbors, nf, m->n_local, m->own_begin, m->own_end, int64_t(nb) * nb,
+                                        d_elem_ptr, static_cast<int64_t*>(ctx->scan_ws), s);
+  if (e != hipSuccess) return hip_fail(e, "hdd_pattern_elem_ptr_device: elem_ptr");
+  e = hipMemcpyAsync(nnz, d_elem_ptr + n_own, sizeof(int64_t), hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) return hip_fail(e, "hdd_pattern_elem_ptr_device: read nnz");
   return HDD_OK;
 }
@@ -766,6 +757,7 @@ extern "C" int hdd_swipdg_rhs(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_
   a.beta = p->beta;
   a.out = d_rhs;
   a.n_cu = ctx->n_cu;
+  a.generic = (ctx->debug_flags & 32768) ? 1 : 0;
   if (force) {
     const int order = fn_order(*force) + deg;
     a.nqv = m->elem_type == HDD_SIMPLEX ? simplex_rule(order, a.qv, 64) : tensor_rule(dim, order, a.qv, 64);

@@ -1248,6 +1248,139 @@ __global__ void __launch_bounds__(64) pattern_fill_tile_kernel(const int32_t* __
   }
 }
 
+// elem_ptr in three small launches instead of counts + a general-purpose device scan (which took 40 us of the
+// C2 pattern's 200): per-block sums of 1024 elements' counts, one workgroup scanning the block sums, then each
+// block re-counts its elements and writes their prefix (the neighbour ids are read twice: 2 x 4 B per face)
+constexpr int PE_THREADS = 256, PE_PER = 4, PE_BLOCK = PE_THREADS * PE_PER;
+
+__device__ __forceinline__ int64_t pe_count(const int32_t* __restrict__ nbrs, int32_t nf, int64_t n_local, int64_t e,
+                                            int64_t nb2)
+{
+  int blocks = 1;
+  for (int f = 0; f < nf; ++f) blocks += nbrs[f * n_local + e] >= 0;
+  return nb2 * blocks;
+}
+
+// block-wide exclusive scan of one value per thread (PE_THREADS threads); returns the block total too
+__device__ __forceinline__ int64_t pe_block_scan(int64_t v, int64_t* sh, int64_t& total)
+{
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  int64_t incl = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int64_t u = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += u;
+  }
+  if (lane == 63) sh[w] = incl;
+  __syncthreads();
+  int64_t before = 0;
+  total = 0;
+#pragma unroll
+  for (int k = 0; k < PE_THREADS / 64; ++k) {
+    before += k < w ? sh[k] : 0;
+    total += sh[k];
+  }
+  __syncthreads();
+  return before + incl - v;
+}
+
+__global__ void __launch_bounds__(PE_THREADS) pattern_block_sums_kernel(const int32_t* __restrict__ nbrs, int32_t nf,
+                                                                        int64_t n_local, int64_t own_begin,
+                                                                        int64_t n_own, int64_t nb2,
+                                                                        int64_t* __restrict__ sums)
+{
+  __shared__ int64_t sh[PE_THREADS / 64];
+  const int64_t b0 = int64_t(blockIdx.x) * PE_BLOCK + threadIdx.x;   // coalesced: element b0 + i * PE_THREADS
+  int64_t v = 0;
+#pragma unroll
+  for (int i = 0; i < PE_PER; ++i)
+    if (b0 + i * PE_THREADS < n_own) v += pe_count(nbrs, nf, n_local, own_begin + b0 + i * PE_THREADS, nb2);
+  int64_t total;
+  (void)pe_block_scan(v, sh, total);
+  if (threadIdx.x == 0) sums[blockIdx.x] = total;
+}
+
+// one workgroup: exclusive offsets of the block sums, in place (chunks of PE_THREADS x PE_PER with a carry)
+__global__ void __launch_bounds__(PE_THREADS) pattern_sums_scan_kernel(int64_t* __restrict__ sums, int64_t n)
+{
+  __shared__ int64_t sh[PE_THREADS / 64];
+  int64_t carry = 0;
+  for (int64_t c0 = 0; c0 < n; c0 += PE_BLOCK) {
+    const int64_t i0 = c0 + int64_t(threadIdx.x) * PE_PER;
+    int64_t v[PE_PER], s = 0;
+#pragma unroll
+    for (int i = 0; i < PE_PER; ++i) {
+      v[i] = i0 + i < n ? sums[i0 + i] : 0;
+      s += v[i];
+    }
+    int64_t total;
+    int64_t ex = carry + pe_block_scan(s, sh, total);
+#pragma unroll
+    for (int i = 0; i < PE_PER; ++i)
+      if (i0 + i < n) {
+        sums[i0 + i] = ex;
+        ex += v[i];
+      }
+    carry += total;
+  }
+}
+
+__global__ void __launch_bounds__(PE_THREADS) pattern_elem_ptr_kernel(const int32_t* __restrict__ nbrs, int32_t nf,
+                                                                      int64_t n_local, int64_t own_begin,
+                                                                      int64_t n_own, int64_t nb2,
+                                                                      const int64_t* __restrict__ offs,
+                                                                      int64_t* __restrict__ elem_ptr)
+{
+  __shared__ int64_t sh[PE_THREADS / 64];
+  __shared__ int64_t cnt[PE_BLOCK];
+  // counts read coalesced (element b0 + i * PE_THREADS), transposed through LDS so that each thread scans
+  // PE_PER consecutive elements, prefixes written back coalesced
+  const int64_t blk0 = int64_t(blockIdx.x) * PE_BLOCK;
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < PE_PER; ++i) {
+    const int64_t k = blk0 + t + i * PE_THREADS;
+    cnt[t + i * PE_THREADS] = k < n_own ? pe_count(nbrs, nf, n_local, own_begin + k, nb2) : 0;
+  }
+  __syncthreads();
+  int64_t c[PE_PER], s = 0;
+#pragma unroll
+  for (int i = 0; i < PE_PER; ++i) {
+    c[i] = cnt[t * PE_PER + i];
+    s += c[i];
+  }
+  int64_t total;
+  int64_t p = offs[blockIdx.x] + pe_block_scan(s, sh, total);   // (its barriers order the cnt reads above)
+#pragma unroll
+  for (int i = 0; i < PE_PER; ++i) {
+    p += c[i];
+    cnt[t * PE_PER + i] = p;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < PE_PER; ++i) {
+    const int64_t k = blk0 + t + i * PE_THREADS;
+    if (k < n_own) elem_ptr[k + 1] = cnt[t + i * PE_THREADS];
+  }
+  if (blockIdx.x == 0 && t == 0) elem_ptr[0] = 0;
+}
+
+int64_t pattern_elem_ptr_scratch(int64_t n_own) { return (n_own + PE_BLOCK - 1) / PE_BLOCK; }
+
+hipError_t launch_pattern_elem_ptr(const int32_t* nbrs, int32_t nf, int64_t n_local, int64_t own_begin,
+                                   int64_t own_end, int64_t nb2, int64_t* d_elem_ptr, int64_t* d_scratch, hipStream_t s)
+{
+  const int64_t n_own = own_end - own_begin;
+  if (n_own <= 0) return hipMemsetAsync(d_elem_ptr, 0, sizeof(int64_t), s);
+  const int64_t nblk = pattern_elem_ptr_scratch(n_own);
+  hipLaunchKernelGGL(pattern_block_sums_kernel, dim3(unsigned(nblk)), dim3(PE_THREADS), 0, s, nbrs, nf, n_local,
+                     own_begin, n_own, nb2, d_scratch);
+  hipLaunchKernelGGL(pattern_sums_scan_kernel, dim3(1), dim3(PE_THREADS), 0, s, d_scratch, nblk);
+  hipLaunchKernelGGL(pattern_elem_ptr_kernel, dim3(unsigned(nblk)), dim3(PE_THREADS), 0, s, nbrs, nf, n_local,
+                     own_begin, n_own, nb2, d_scratch, d_elem_ptr);
+  return hipGetLastError();
+}
+
 hipError_t launch_pattern_counts(const int32_t* nbrs, int32_t nf, int64_t n_local, int64_t own_begin, int64_t own_end,
                                  int64_t nb2, int64_t* d_counts, hipStream_t s)
 {

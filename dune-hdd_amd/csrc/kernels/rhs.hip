@@ -619,7 +619,7 @@ hipError_t launch_rhs(const RhsArgs& a, hipStream_t s)
     const int64_t blocks = std::min<int64_t>((n_own + 255) / 256, int64_t(a.n_cu) * 8);
     const bool tri = a.elem_type == HDD_SIMPLEX;
     // the ESV2007-type force (cos products) on the rules of order 4 (Dunavant 6 / Gauss 3 x 3): unrolled
-    if (a.has_force && a.force.kind == HDD_FN_COS_PRODUCT && a.nqv == (tri ? 6 : 9)) {
+    if (a.has_force && a.force.kind == HDD_FN_COS_PRODUCT && a.nqv == (tri ? 6 : 9) && !a.generic) {
       if (tri && a.ev) hipLaunchKernelGGL((rhs2d_kernel<true, true, 6, HDD_FN_COS_PRODUCT>), dim3(unsigned(blocks)), dim3(256), 0, s, a);
       else if (tri) hipLaunchKernelGGL((rhs2d_kernel<true, false, 6, HDD_FN_COS_PRODUCT>), dim3(unsigned(blocks)), dim3(256), 0, s, a);
       else if (a.ev) hipLaunchKernelGGL((rhs2d_kernel<false, true, 9, HDD_FN_COS_PRODUCT>), dim3(unsigned(blocks)), dim3(256), 0, s, a);

@@ -90,6 +90,11 @@ hipError_t launch_hex(const HexArgs& a, int degree, int nq1v, int nq1f, hipStrea
 // device pattern (any element type): blocks per element = 1 + interior faces
 hipError_t launch_pattern_counts(const int32_t* nbrs, int32_t nf, int64_t n_local, int64_t own_begin, int64_t own_end,
                                  int64_t nb2, int64_t* d_counts, hipStream_t s);
+// elem_ptr [n_own + 1] (exclusive prefix of the row-block sizes) in three launches; d_scratch holds
+// pattern_elem_ptr_scratch(n_own) int64
+int64_t pattern_elem_ptr_scratch(int64_t n_own);
+hipError_t launch_pattern_elem_ptr(const int32_t* nbrs, int32_t nf, int64_t n_local, int64_t own_begin,
+                                   int64_t own_end, int64_t nb2, int64_t* d_elem_ptr, int64_t* d_scratch, hipStream_t s);
 hipError_t launch_pattern_fill(const int32_t* nbrs, int32_t nf, int32_t nb, int64_t n_local, int64_t own_begin,
                                int64_t own_end, const int64_t* gid, const int64_t* elem_ptr, int64_t* row_ptr,
                                int32_t* col, int n_cu, hipStream_t s);
@@ -106,6 +111,7 @@ struct RhsArgs {
   int32_t has_force, has_dirichlet, has_neumann, pad;
   double sigma_boundary, beta;
   int32_t nqv, nqd, nqn, n_cu;
+  int32_t generic, pad_g;   // 1: the run-time-rule kernel only (HDD_DEBUG_FLAGS bit 32768: A/B of the unrolled path)
   double qv[64][4];    // volume rule: reference point (3) + weight
   double qd[16][3];    // Dirichlet face rule: face parameters (2) + weight
   double qn[16][3];    // Neumann face rule

@@ -16,6 +16,17 @@ import hdd_amd as H
 def workload(cfg, ctx):
     rng = np.random.default_rng(10)
     perm = 10.0 ** rng.uniform(-3, 3, 2000)
+    if cfg in ("rhs", "pattern"):   # the f rows on the C2 mesh (scripts/bench_configs.py f)
+        grid = H.Grid.structured(H.SIMPLEX, 3200, 640, (0, 0), (5, 1))
+        local = grid.local()
+        dm = H.DeviceMesh(local)
+        if cfg == "pattern":
+            return lambda: H.DevicePattern(local, ctx=ctx, dmesh=dm, on_device=True)
+        k = torch.from_numpy(local.checkerboard((0, 0), (5, 1), 100, 20, perm)).cuda()
+        ten = H.tensor_fn(H.TENSOR_ISO_PER_ELEM, per_elem=k)
+        out = torch.empty(3 * local.n_own, dtype=torch.float64, device="cuda")
+        return lambda: H.rhs(ctx, dm, force=H.esv2007_force(), kappa=H.scalar_fn(H.FN_CONST, 1.0), tensor=ten,
+                             dirichlet=H.scalar_fn(H.FN_CONST, 1.0), out=out)
     if cfg == "c3":
         grid = H.Grid.structured(H.SIMPLEX, 1024, 1024, (-1, -1), (1, 1))
         local = grid.local()
