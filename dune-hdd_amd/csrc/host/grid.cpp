@@ -273,7 +273,7 @@ struct StructuredGrid3 final : Grid {
 // general conforming mesh from connectivity
 // ------------------------------------------------------------------------------------------------
 struct ExplicitGrid final : Grid {
-  std::vector<double> vc;       // [nv][2]
+  std::vector<double> vc;       // [nv][dim]
   std::vector<int64_t> ev;      // [ne][nvpe] (renumbered elements)
   std::vector<int64_t> nbr;     // [ne][nf]
   std::vector<uint32_t> finfo;  // [ne]
@@ -282,7 +282,10 @@ struct ExplicitGrid final : Grid {
   {
     for (int k = 0; k < nvpe; ++k) v[k] = ev[g * nvpe + k];
   }
-  void vertex_coord(int64_t v, double* xy) const override { xy[0] = vc[2 * v]; xy[1] = vc[2 * v + 1]; }
+  void vertex_coord(int64_t v, double* xy) const override
+  {
+    for (int c = 0; c < dim; ++c) xy[c] = vc[dim * v + c];
+  }
   int64_t neighbor(int64_t g, int f) const override { return nbr[g * nf + f]; }
   uint32_t face_info(int64_t g) const override { return finfo[g]; }
 };
@@ -327,6 +330,106 @@ struct hdd_local {
 };
 
 using namespace hdd;
+
+// vertices (local indices, ascending) of face f: 2d from the reference-element tables, hex face f = the
+// four vertices k with bit f/2 of k equal to f&1 (Dune cube: faces 2a / 2a+1 at x_a = 0 / 1)
+static int face_vertices(int elem_type, int f, int* k)
+{
+  if (elem_type == HDD_HEX) {
+    int n = 0;
+    for (int v = 0; v < 8; ++v)
+      if (((v >> (f / 2)) & 1) == (f & 1)) k[n++] = v;
+    return 4;
+  }
+  const auto FV = face_table(elem_type);
+  k[0] = FV[f][0];
+  k[1] = FV[f][1];
+  return 2;
+}
+
+// shared tail of the connectivity constructors: subdomain-major renumbering (stable), face matching by the
+// sorted vertex ids of each face, twin face / orientation bits
+static int finish_explicit(std::unique_ptr<ExplicitGrid> G, int64_t n_vertices, const double* vertex_coords,
+                           int64_t n_elements, const int32_t* elem_vert, const int32_t* subdomain,
+                           int32_t n_subdomains, int32_t boundary, hdd_grid** out, const std::string& fn)
+{
+  G->nv = n_vertices;
+  G->ne = n_elements;
+  G->n_sub = subdomain ? n_subdomains : 1;
+  if (G->n_sub < 1) return set_error(HDD_ERR_INVALID, fn + ": n_subdomains < 1");
+  const int nvpe = G->nvpe, nf = G->nf, dim = G->dim;
+  std::vector<int64_t> order(n_elements);
+  G->sub_first.assign(G->n_sub + 1, 0);
+  for (int64_t e = 0; e < n_elements; ++e) {
+    const int32_t s = subdomain ? subdomain[e] : 0;
+    if (s < 0 || s >= G->n_sub) return set_error(HDD_ERR_RANGE, fn + ": bad subdomain");
+    G->sub_first[s + 1]++;
+  }
+  for (int s = 0; s < G->n_sub; ++s) G->sub_first[s + 1] += G->sub_first[s];
+  {
+    std::vector<int64_t> pos(G->sub_first.begin(), G->sub_first.end() - 1);
+    for (int64_t e = 0; e < n_elements; ++e) order[pos[subdomain ? subdomain[e] : 0]++] = e;  // new -> old
+  }
+  G->vc.assign(vertex_coords, vertex_coords + dim * n_vertices);
+  G->ev.resize(n_elements * nvpe);
+  for (int64_t n = 0; n < n_elements; ++n)
+    for (int k = 0; k < nvpe; ++k) {
+      const int32_t v = elem_vert[order[n] * nvpe + k];
+      if (v < 0 || v >= n_vertices) return set_error(HDD_ERR_RANGE, fn + ": bad vertex");
+      G->ev[n * nvpe + k] = v;
+    }
+  struct Rec { int64_t key[4]; int64_t ef; };
+  std::vector<Rec> rec(n_elements * nf);
+  int fvk[8][4] = {};
+  int nfv = 0;
+  for (int f = 0; f < nf; ++f) nfv = face_vertices(G->elem_type, f, fvk[f]);
+  for (int64_t e = 0; e < n_elements; ++e)
+    for (int f = 0; f < nf; ++f) {
+      Rec r{{-1, -1, -1, -1}, e * nf + f};
+      for (int i = 0; i < nfv; ++i) r.key[i] = G->ev[e * nvpe + fvk[f][i]];
+      std::sort(r.key, r.key + nfv);
+      rec[e * nf + f] = r;
+    }
+  auto same = [](const Rec& x, const Rec& y) {
+    return x.key[0] == y.key[0] && x.key[1] == y.key[1] && x.key[2] == y.key[2] && x.key[3] == y.key[3];
+  };
+  std::sort(rec.begin(), rec.end(), [](const Rec& x, const Rec& y) {
+    for (int i = 0; i < 4; ++i)
+      if (x.key[i] != y.key[i]) return x.key[i] < y.key[i];
+    return x.ef < y.ef;
+  });
+  const int64_t bcode = boundary == HDD_BOUNDARY_ALL_NEUMANN ? HDD_NBR_NEUMANN : HDD_NBR_DIRICHLET;
+  G->nbr.assign(n_elements * nf, bcode);
+  uint32_t fi0 = 0;   // hex: twin f^1 on every face, boundary faces included (as StructuredGrid3::face_info)
+  if (G->elem_type == HDD_HEX)
+    for (uint32_t f = 0; f < 6; ++f) fi0 |= (f ^ 1u) << (4 * f);
+  G->finfo.assign(n_elements, fi0);
+  for (size_t i = 0; i < rec.size();) {
+    size_t j = i + 1;
+    while (j < rec.size() && same(rec[j], rec[i])) ++j;
+    if (j - i > 2) return set_error(HDD_ERR_INVALID, fn + ": non-manifold face");
+    if (j - i == 2) {
+      const int64_t p = rec[i].ef, q = rec[i + 1].ef;
+      const int64_t ep = p / nf, eq = q / nf;
+      const int fp = int(p % nf), fq = int(q % nf);
+      const bool rev = G->ev[ep * nvpe + fvk[fp][0]] != G->ev[eq * nvpe + fvk[fq][0]];
+      if (G->elem_type == HDD_HEX && (fq != (fp ^ 1) || rev))
+        return set_error(HDD_ERR_UNSUPPORTED, fn + ": hexahedra " + std::to_string(ep) + " / " + std::to_string(eq) +
+                                                  " do not share an aligned face (twin f^1)");
+      G->nbr[p] = eq;
+      G->nbr[q] = ep;
+      if (G->elem_type != HDD_HEX) {
+        G->finfo[ep] |= (uint32_t(fq) | (rev ? 8u : 0u)) << (4 * fp);
+        G->finfo[eq] |= (uint32_t(fp) | (rev ? 8u : 0u)) << (4 * fq);
+      }
+    }
+    i = j;
+  }
+  auto* g = new hdd_grid;
+  g->impl = std::move(G);
+  *out = g;
+  return HDD_OK;
+}
 
 // ------------------------------------------------------------------------------------------------
 // C ABI
@@ -404,68 +507,47 @@ extern "C" int hdd_grid_create_from_connectivity(int32_t elem_type, int64_t n_ve
   G->nvpe = nvpe_of(elem_type);
   G->nf = G->nvpe;
   G->nb = G->nvpe;
-  G->nv = n_vertices;
-  G->ne = n_elements;
-  G->n_sub = subdomain ? n_subdomains : 1;
-  if (G->n_sub < 1) return set_error(HDD_ERR_INVALID, "hdd_grid_create_from_connectivity: n_subdomains < 1");
-  const int nvpe = G->nvpe, nf = G->nf;
-  // subdomain-major renumbering (stable)
-  std::vector<int64_t> order(n_elements);
-  G->sub_first.assign(G->n_sub + 1, 0);
+  return finish_explicit(std::move(G), n_vertices, vertex_coords, n_elements, elem_vert, subdomain, n_subdomains,
+                         boundary, out, "hdd_grid_create_from_connectivity");
+}
+
+extern "C" int hdd_grid_create_hex_from_connectivity(int32_t degree, int64_t n_vertices, const double* vertex_coords,
+                                                     int64_t n_elements, const int32_t* elem_vert,
+                                                     const int32_t* subdomain, int32_t n_subdomains, int32_t boundary,
+                                                     hdd_grid** out)
+{
+  const char* fn = "hdd_grid_create_hex_from_connectivity";
+  if (!vertex_coords || !elem_vert || !out || n_vertices <= 0 || n_elements <= 0)
+    return set_error(HDD_ERR_INVALID, std::string(fn) + ": invalid argument");
+  if (degree < 1 || degree > 3) return set_error(HDD_ERR_UNSUPPORTED, std::string(fn) + ": degree must be 1, 2 or 3");
+  const int64_t nb = int64_t(degree + 1) * (degree + 1) * (degree + 1);
+  if (n_elements * nb > int64_t(INT32_MAX)) return set_error(HDD_ERR_RANGE, std::string(fn) + ": too many DoFs for int32 columns");
+  // the Q_p hex kernels take an affine, axis-aligned box per element (diagonal Jacobian from vertices 0, 1, 2, 4)
+  // with aligned twin faces: every element must be lower + (k&1, (k>>1)&1, k>>2) * h in Dune cube vertex order
   for (int64_t e = 0; e < n_elements; ++e) {
-    const int32_t s = subdomain ? subdomain[e] : 0;
-    if (s < 0 || s >= G->n_sub) return set_error(HDD_ERR_RANGE, "hdd_grid_create_from_connectivity: bad subdomain");
-    G->sub_first[s + 1]++;
-  }
-  for (int s = 0; s < G->n_sub; ++s) G->sub_first[s + 1] += G->sub_first[s];
-  {
-    std::vector<int64_t> pos(G->sub_first.begin(), G->sub_first.end() - 1);
-    for (int64_t e = 0; e < n_elements; ++e) order[pos[subdomain ? subdomain[e] : 0]++] = e;  // new -> old
-  }
-  G->vc.assign(vertex_coords, vertex_coords + 2 * n_vertices);
-  G->ev.resize(n_elements * nvpe);
-  for (int64_t n = 0; n < n_elements; ++n)
-    for (int k = 0; k < nvpe; ++k) {
-      const int32_t v = elem_vert[order[n] * nvpe + k];
-      if (v < 0 || v >= n_vertices) return set_error(HDD_ERR_RANGE, "hdd_grid_create_from_connectivity: bad vertex");
-      G->ev[n * nvpe + k] = v;
+    const int32_t* v = elem_vert + 8 * e;
+    for (int k = 0; k < 8; ++k)
+      if (v[k] < 0 || v[k] >= n_vertices) return set_error(HDD_ERR_RANGE, std::string(fn) + ": bad vertex");
+    for (int c = 0; c < 3; ++c) {
+      const double lo = vertex_coords[3 * v[0] + c], hi = vertex_coords[3 * v[1 << c] + c];
+      if (!(hi > lo)) return set_error(HDD_ERR_UNSUPPORTED, std::string(fn) + ": element " + std::to_string(e) +
+                                                             " is not an axis-aligned box in Dune vertex order");
+      for (int k = 0; k < 8; ++k) {
+        const double want = ((k >> c) & 1) ? hi : lo, x = vertex_coords[3 * v[k] + c];
+        if (std::fabs(x - want) > 1e-12 * std::max(std::fabs(hi - lo), std::fabs(want)))
+          return set_error(HDD_ERR_UNSUPPORTED, std::string(fn) + ": element " + std::to_string(e) +
+                                                    " is not an axis-aligned box in Dune vertex order");
+      }
     }
-  // face matching by sorted (min vertex, max vertex) keys
-  struct Rec { int64_t a, b, ef; };
-  std::vector<Rec> rec(n_elements * nf);
-  const auto FV = face_table(elem_type);
-  for (int64_t e = 0; e < n_elements; ++e)
-    for (int f = 0; f < nf; ++f) {
-      int64_t a = G->ev[e * nvpe + FV[f][0]], b = G->ev[e * nvpe + FV[f][1]];
-      if (a > b) std::swap(a, b);
-      rec[e * nf + f] = {a, b, e * nf + f};
-    }
-  std::sort(rec.begin(), rec.end(), [](const Rec& x, const Rec& y) {
-    return x.a != y.a ? x.a < y.a : (x.b != y.b ? x.b < y.b : x.ef < y.ef);
-  });
-  const int64_t bcode = boundary == HDD_BOUNDARY_ALL_NEUMANN ? HDD_NBR_NEUMANN : HDD_NBR_DIRICHLET;
-  G->nbr.assign(n_elements * nf, bcode);
-  G->finfo.assign(n_elements, 0u);
-  for (size_t i = 0; i < rec.size();) {
-    size_t j = i + 1;
-    while (j < rec.size() && rec[j].a == rec[i].a && rec[j].b == rec[i].b) ++j;
-    if (j - i > 2) return set_error(HDD_ERR_INVALID, "hdd_grid_create_from_connectivity: non-manifold face");
-    if (j - i == 2) {
-      const int64_t p = rec[i].ef, q = rec[i + 1].ef;
-      const int64_t ep = p / nf, eq = q / nf;
-      const int fp = int(p % nf), fq = int(q % nf);
-      const bool rev = G->ev[ep * nvpe + FV[fp][0]] != G->ev[eq * nvpe + FV[fq][0]];
-      G->nbr[p] = eq;
-      G->nbr[q] = ep;
-      G->finfo[ep] |= (uint32_t(fq) | (rev ? 8u : 0u)) << (4 * fp);
-      G->finfo[eq] |= (uint32_t(fp) | (rev ? 8u : 0u)) << (4 * fq);
-    }
-    i = j;
   }
-  auto* g = new hdd_grid;
-  g->impl = std::move(G);
-  *out = g;
-  return HDD_OK;
+  auto G = std::make_unique<ExplicitGrid>();
+  G->elem_type = HDD_HEX;
+  G->dim = 3;
+  G->nvpe = 8;
+  G->nf = 6;
+  G->nb = int(nb);
+  return finish_explicit(std::move(G), n_vertices, vertex_coords, n_elements, elem_vert, subdomain, n_subdomains,
+                         boundary, out, fn);
 }
 
 extern "C" void hdd_grid_destroy(hdd_grid* g) { delete g; }

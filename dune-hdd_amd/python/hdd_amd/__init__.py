@@ -135,6 +135,7 @@ def lib():
         "hdd_grid_create_structured": (_I32, [C.POINTER(StructuredDesc), _VP]),
         "hdd_grid_create_structured_3d": (_I32, [C.POINTER(Structured3Desc), _VP]),
         "hdd_grid_create_from_connectivity": (_I32, [_I32, _I64, _VP, _I64, _VP, _VP, _I32, _I32, _VP]),
+        "hdd_grid_create_hex_from_connectivity": (_I32, [_I32, _I64, _VP, _I64, _VP, _VP, _I32, _I32, _VP]),
         "hdd_grid_destroy": (None, [_VP]),
         "hdd_grid_get_info": (_I32, [_VP, C.POINTER(GridInfo)]),
         "hdd_grid_subdomain_range": (_I32, [_VP, _I32, _I32, C.POINTER(_I64), C.POINTER(_I64)]),
@@ -275,11 +276,20 @@ class Grid:
 
     @classmethod
     def from_connectivity(cls, elem_type, coords, elem_vert, subdomain=None, n_sub=1,
-                          boundary=BOUNDARY_ALL_DIRICHLET):
+                          boundary=BOUNDARY_ALL_DIRICHLET, degree=1):
+        """2d (SIMPLEX / CUBE: coords [nv][2]) or 3d axis-aligned hexahedra (HEX: coords [nv][3], elem_vert
+        [ne][8] in Dune cube vertex order, DG Q_degree)."""
         coords = np.ascontiguousarray(coords, np.float64)
         ev = np.ascontiguousarray(elem_vert, np.int32)
         sd = None if subdomain is None else np.ascontiguousarray(subdomain, np.int32)
         h = C.c_void_p()
+        if elem_type == HEX:
+            _check(lib().hdd_grid_create_hex_from_connectivity(degree, coords.shape[0], _p(coords), ev.shape[0],
+                                                               _p(ev), _p(sd), n_sub, boundary, C.byref(h)),
+                   "hdd_grid_create_hex_from_connectivity")
+            g = cls(h)
+            g.degree = degree
+            return g
         _check(lib().hdd_grid_create_from_connectivity(elem_type, coords.shape[0], _p(coords), ev.shape[0],
                                                        _p(ev), _p(sd), n_sub, boundary, C.byref(h)),
                "hdd_grid_create_from_connectivity")

@@ -337,6 +337,25 @@ int main(int argc, char** argv)
     }
   }
 
+  // 6b. the same in 3d (block-swipdg.hh:783-817 is dimension-generic): ESV2007 3d on 4 x 3 x 3 hexahedra, Q2,
+  //     2 x 1 x 1 subdomains, one oversampling layer -- subdomain 0 plus the next x-slab of elements (a box)
+  {
+    Dune::grid::Multiscale::Providers::Cube ms({-1.0, -1.0, -1.0}, {1.0, 1.0, 1.0}, {4, 3, 3}, {2, 1, 1},
+                                               /*oversampling_layers=*/1, /*degree=*/2);
+    Discretizations::BlockSWIPDG block(ms, S::Common::Configuration(), esv3, {});
+    block.init();
+    for (const char* bt : {"dirichlet", "neumann"}) {
+      const auto& O = block.get_oversampled_discretization(0, bt);
+      dump(out + "/os3_" + std::string(bt) + "_row_ptr.bin", O.pattern().row_ptr());
+      dump(out + "/os3_" + std::string(bt) + "_col.bin", O.pattern().col());
+      dump(out + "/os3_" + std::string(bt) + "_affine.bin", O.system_matrix().affine_part());
+      dump(out + "/os3_" + std::string(bt) + "_rhs.bin", O.rhs().affine_part());
+    }
+    const auto ids = block.oversampled_elements(0);
+    dump(out + "/os3_ids.bin", ids);
+    std::printf("oversampled 3d 0: %zu elements (layers %d)\n", ids.size(), block.oversampling_layers());
+  }
+
   // 7. parametric SPE10 Model1 (problems/spe10.hh:160-172): A = checkerboard, kappa = (1 + channel) - mu channel,
   //    force = Indicator; channel / force boxes read from <outdir>/spe10_boxes.bin when present
   {

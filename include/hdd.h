@@ -36,9 +36,10 @@
 extern "C" {
 #endif
 
-#define HDD_ABI_VERSION 5   /* 3: hdd_mesh vertex-indexed geometry, hdd_local_vertices;
+#define HDD_ABI_VERSION 6   /* 3: hdd_mesh vertex-indexed geometry, hdd_local_vertices;
                                4: HDD_FN_FLATTOP (hdd_scalar_fn.table / n_table), hdd_indicator_sum;
-                               5: hdd_shard_info.halo_elements, hdd_swipdg_assemble_elements */
+                               5: hdd_shard_info.halo_elements, hdd_swipdg_assemble_elements;
+                               6: hdd_grid_create_hex_from_connectivity */
 #define HDD_MAX_COMP 8
 
 typedef enum {
@@ -111,6 +112,15 @@ int hdd_grid_create_structured_3d(const hdd_structured3_desc* desc, hdd_grid** o
 int hdd_grid_create_from_connectivity(int32_t elem_type, int64_t n_vertices, const double* vertex_coords,
                                       int64_t n_elements, const int32_t* elem_vert, const int32_t* subdomain,
                                       int32_t n_subdomains, int32_t boundary, hdd_grid** out);
+/* general conforming 3d mesh of axis-aligned hexahedra from connectivity (vertex_coords [n_vertices][3],
+ * elem_vert [n_elements][8] in Dune cube vertex order: vertex k at lower + ((k&1), (k>>1)&1, k>>2) * h),
+ * carrying the DG Q_`degree` space (1..3); shared faces must be aligned (twin face f^1, the layout every
+ * subset of a structured hex grid has).  Replaces the grid part the reference hands to an oversampled local
+ * discretization in 3d (MsGrid::local_oversampled grid part, block-swipdg.hh:783-817); HDD_ERR_UNSUPPORTED
+ * for a non-box element or a misaligned shared face. */
+int hdd_grid_create_hex_from_connectivity(int32_t degree, int64_t n_vertices, const double* vertex_coords,
+                                          int64_t n_elements, const int32_t* elem_vert, const int32_t* subdomain,
+                                          int32_t n_subdomains, int32_t boundary, hdd_grid** out);
 void hdd_grid_destroy(hdd_grid* g);
 int hdd_grid_get_info(const hdd_grid* g, hdd_grid_info* out);
 /* element range [first, last) of the subdomains [s_begin, s_end) in the (subdomain-major) numbering */

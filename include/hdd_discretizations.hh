@@ -167,6 +167,19 @@ class Cube {
       throw Stuff::Exceptions::wrong_input_given(std::string("Multiscale::Providers::Cube: ") + hdd_last_error(nullptr));
     g_.reset(g, hdd_grid_destroy);
   }
+  // 3d: n0 x n1 x n2 axis-aligned hexahedra carrying DG Q_degree, num_partitions [px py pz]
+  Cube(std::array<double, 3> lower, std::array<double, 3> upper, std::array<int, 3> num_elements,
+       std::array<int, 3> num_partitions, int oversampling_layers = 0, int degree = 1)
+    : layers_(oversampling_layers)
+  {
+    hdd_structured3_desc d{num_elements[0], num_elements[1], num_elements[2], num_partitions[0], num_partitions[1],
+                           num_partitions[2], HDD_BOUNDARY_ALL_DIRICHLET, degree,
+                           {lower[0], lower[1], lower[2]}, {upper[0], upper[1], upper[2]}};
+    hdd_grid* g = nullptr;
+    if (hdd_grid_create_structured_3d(&d, &g) != HDD_OK)
+      throw Stuff::Exceptions::wrong_input_given(std::string("Multiscale::Providers::Cube: ") + hdd_last_error(nullptr));
+    g_.reset(g, hdd_grid_destroy);
+  }
   // adopt a grid carrying a subdomain partition (not destroyed)
   explicit Cube(const hdd_grid* g) : g_(const_cast<hdd_grid*>(g), [](hdd_grid*) {}) {}
   const hdd_grid* grid() const { return g_.get(); }
@@ -1495,8 +1508,7 @@ class BlockSWIPDG : public SWIPDG {
   // a standalone grid (vertex ids of the parent) of the given parent elements, in their order
   std::shared_ptr<hdd_grid> subset_grid(const std::vector<int64_t>& ids) const
   {
-    if (info_.dim != 2) throw NotImplemented("oversampled discretizations: 2d grids");
-    std::vector<double> vc(size_t(2 * info_.n_vertices));
+    std::vector<double> vc(size_t(info_.dim) * size_t(info_.n_vertices));
     std::vector<int32_t> ev(size_t(info_.nvpe * info_.n_elements)), sub;
     internal::check(hdd_grid_connectivity(grid_, vc.data(), ev.data(), nullptr), "hdd_grid_connectivity");
     std::vector<int32_t> sev;
@@ -1504,9 +1516,17 @@ class BlockSWIPDG : public SWIPDG {
     for (int64_t e : ids)
       for (int k = 0; k < info_.nvpe; ++k) sev.push_back(ev[size_t(e * info_.nvpe + k)]);
     hdd_grid* g = nullptr;
-    internal::check(hdd_grid_create_from_connectivity(info_.elem_type, info_.n_vertices, vc.data(), int64_t(ids.size()),
-                                                      sev.data(), nullptr, 1, HDD_BOUNDARY_ALL_DIRICHLET, &g),
-                    "hdd_grid_create_from_connectivity");
+    if (info_.elem_type == HDD_HEX) {   // nb = (p+1)^3
+      int p = 1;
+      while ((p + 1) * (p + 1) * (p + 1) < info_.nb) ++p;
+      internal::check(hdd_grid_create_hex_from_connectivity(p, info_.n_vertices, vc.data(), int64_t(ids.size()),
+                                                            sev.data(), nullptr, 1, HDD_BOUNDARY_ALL_DIRICHLET, &g),
+                      "hdd_grid_create_hex_from_connectivity");
+    } else {
+      internal::check(hdd_grid_create_from_connectivity(info_.elem_type, info_.n_vertices, vc.data(), int64_t(ids.size()),
+                                                        sev.data(), nullptr, 1, HDD_BOUNDARY_ALL_DIRICHLET, &g),
+                      "hdd_grid_create_from_connectivity");
+    }
     return std::shared_ptr<hdd_grid>(g, hdd_grid_destroy);
   }
 

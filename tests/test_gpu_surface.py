@@ -271,6 +271,35 @@ def test_cpp_block_oversampled_discretization(surface_run):
         assert np.max(np.abs(_ld(d, "os0_%s_rhs" % bt) - b)) <= 1e-12 * np.max(np.abs(b))
 
 
+@pytest.mark.gpu
+def test_cpp_block_oversampled_discretization_3d(surface_run):
+    """get_oversampled_discretization in 3d (block-swipdg.hh:783-817 is dimension-generic; VERDICT r02 missing
+    #2): ESV2007 3d, Q2 on 4 x 3 x 3 hexahedra of [-1,1]^3, 2 x 1 x 1 subdomains, one oversampling layer.  The
+    grid part is subdomain 0 (x-columns 0, 1) plus the face-neighbour x-column 2 -- a 3 x 3 x 3 box, so the Q_p
+    oracle on that box (Dirichlet / Neumann on its whole boundary, ZeroBoundary(ESV2007)) is the reference."""
+    r, d = surface_run
+    ids = _ld(d, "os3_ids", np.int64)
+    assert "oversampled 3d 0: 27 elements (layers 1)" in r.stdout
+    g = H.Grid.structured3d((4, 3, 3), (-1, -1, -1), (1, 1, 1), p=(2, 1, 1), degree=2)
+    coords, ev, _ = g.connectivity()
+    lo, up, n = (-1.0, -1.0, -1.0), (0.5, 1.0, 1.0), (3, 3, 3)
+    v0 = coords[ev[ids, 0]]
+    ijk = np.rint((v0 - np.asarray(lo)) / (2.0 / np.array([4, 3, 3]))).astype(np.int64)
+    assert ijk[:, 0].max() == 2
+    lex = ijk[:, 0] + 3 * (ijk[:, 1] + 3 * ijk[:, 2])
+    ei = np.empty(27, np.int64)
+    ei[lex] = np.arange(27)
+    q = O.QpGrid(3, 2, n, lo, up)
+    for bt, kind in (("dirichlet", O.BOUNDARY_DIRICHLET), ("neumann", O.BOUNDARY_NEUMANN)):
+        prm = O.qp_params(q, boundary=kind)
+        rp, col, val = O.qp_assemble(q, O.scalar(), O.qp_tensor(), prm, elem_index=ei)
+        assert np.array_equal(_ld(d, "os3_%s_row_ptr" % bt, np.int64), rp)
+        assert np.array_equal(_ld(d, "os3_%s_col" % bt, np.int32), col)
+        assert compare_rows(rp, _ld(d, "os3_%s_affine" % bt), val, 1e-12)[1]
+        b = O.qp_rhs_swipdg(q, force=O.esv2007_force(3), prm=prm, elem_index=ei)
+        assert np.max(np.abs(_ld(d, "os3_%s_rhs" % bt) - b)) <= 1e-12 * np.max(np.abs(b))
+
+
 def _checksum(t):
     """sum_k bits[k] * (2k + 1) mod 2^64 over a device tensor (examples/surface_main.cpp: checksum)"""
     import torch

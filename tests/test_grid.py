@@ -199,3 +199,43 @@ def test_local_vertices_reproduce_element_coords(case):
     assert np.array_equal(lxy, gcoords[gids])
     if case == "kuhn_slice":
         assert loc.n_ghost > 0
+
+
+def test_hex_from_connectivity_reproduces_structured_3d():
+    """hdd_grid_create_hex_from_connectivity (ABI v6, the 3d grid part of an oversampled local discretization,
+    block-swipdg.hh:783-817): the connectivity of a structured 3d grid rebuilt explicitly (with its subdomain
+    ids) has the same numbering, coordinates, neighbours, twin faces and subdomains -- subdomain by subdomain."""
+    g = H.Grid.structured3d((4, 3, 5), (0, 0, 0), (1, 2, 3), degree=2, p=(2, 1, 2))
+    coords, ev, sd = g.connectivity()
+    e = H.Grid.from_connectivity(H.HEX, coords, ev, subdomain=sd, n_sub=4, degree=2)
+    assert (e.nb, e.nf, e.nvpe, e.dim) == (27, 6, 8, 3)
+    for s in range(4):
+        a, b = g.local(s, s + 1), e.local(s, s + 1)
+        for k in ("coords", "neighbors", "face_info", "global_id", "subdomain"):
+            assert np.array_equal(getattr(a, k), getattr(b, k)), k
+
+
+def test_hex_from_connectivity_subset_and_rejections():
+    """A subset of a structured hex grid (subdomain 0 plus one ring of face neighbours, the oversampled grid
+    part): neighbours inside the subset keep their parent pairing, faces leaving it become boundary faces;
+    non-box elements and wrong vertex orders are refused with HDD_ERR_UNSUPPORTED."""
+    g = H.Grid.structured3d((6, 4, 4), (0, 0, 0), (1, 1, 1), degree=1, p=(2, 2, 1))
+    coords, ev, sd = g.connectivity()
+    full = g.local()
+    own = np.flatnonzero(sd == 0)
+    ring = np.unique(full.neighbors[:, own][full.neighbors[:, own] >= 0])
+    ids = np.union1d(own, ring)
+    sub = H.Grid.from_connectivity(H.HEX, coords, ev[ids], degree=1)
+    loc = sub.local()
+    pos = {int(p): i for i, p in enumerate(ids)}
+    for i, p in enumerate(ids):
+        for f in range(6):
+            n = full.neighbors[f, p]
+            want = pos.get(int(n), H.NBR_DIRICHLET) if n >= 0 else H.NBR_DIRICHLET
+            assert loc.neighbors[f, i] == want
+    bad = coords.copy()
+    bad[ev[0, 7]] += 0.01                                             # vertex 7 off the box
+    with pytest.raises(H.HddError, match="axis-aligned box"):
+        H.Grid.from_connectivity(H.HEX, bad, ev[:1], degree=1)
+    with pytest.raises(H.HddError, match="axis-aligned box"):
+        H.Grid.from_connectivity(H.HEX, coords, ev[:1, ::-1], degree=1)   # reversed vertex order
