@@ -15,9 +15,9 @@ if [ -z "${NOTRAFFIC:-}" ]; then
   bash scripts/traffic.sh "$TAG" > "$OUT/traffic.log" 2>&1
   rc=$?; echo "traffic rc=$rc"; tail -3 "$OUT/traffic.log"; [ $rc -eq 0 ] || exit $rc
 fi
-timeout -k 10 300 python bench.py --steps 20 --warmup 5 ${TRAFFIC_JSON:+--traffic-json $TRAFFIC_JSON} > "$OUT/bench.log" 2>&1
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 --traffic-json ${TRAFFIC_JSON:-profiles/$TAG/traffic.json} > "$OUT/bench.log" 2>&1
 rc=$?; echo "bench rc=$rc"; tail -1 "$OUT/bench.log" | cut -c1-600; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python bench.py --workload c4 --steps 20 --warmup 5 --no-cpu-baseline ${TRAFFIC_JSON:+--traffic-json $TRAFFIC_JSON} > "$OUT/bench_c4.log" 2>&1
+timeout -k 10 300 python bench.py --workload c4 --steps 20 --warmup 5 --no-cpu-baseline --traffic-json ${TRAFFIC_JSON:-profiles/$TAG/traffic.json} > "$OUT/bench_c4.log" 2>&1
 rc=$?; echo "bench c4 rc=$rc"; tail -1 "$OUT/bench_c4.log" | cut -c1-600; [ $rc -eq 0 ] || exit $rc
 if [ -n "${CFG:-}" ]; then
   timeout -k 10 400 python -u scripts/bench_configs.py $CFG > "$OUT/configs.log" 2>&1

@@ -79,6 +79,18 @@ def main():
                 res["d step, no transfer, hipGraph"] = timeit(g.replay)
             except Exception as e:   # report, keep the other numbers
                 print("  graph capture failed: %s" % e)
+            # (f) the element-list fixup alone, (g) one full launch, on the same rank-local layout through the
+            # Python front-end's LocalMesh (grid.local(s0, s1) = the shard's element range)
+            s0, s1 = sh.info.s_begin, sh.info.s_end
+            loc = grid.local(s0, s1)
+            dm, dp = H.DeviceMesh(loc), H.DevicePattern(loc)
+            kl = torch.from_numpy(loc.checkerboard(lo, up, ncx, ncy, perm)).cuda()
+            tl = H.tensor_fn(H.TENSOR_ISO_PER_ELEM, per_elem=kl)
+            vl = [torch.empty(dp.nnz, dtype=torch.float64, device="cuda")]
+            fix = torch.from_numpy(H.halo_elements(loc)).cuda()
+            res["f fixup launch alone"] = timeit(lambda: H.assemble_tiles(ctx, dm, dp, kap, tl, fix, vl, elements=True))
+            res["g full launch (LocalMesh)"] = timeit(lambda: H.assemble(ctx, dm, dp, kap, tl, vals=vl))
+            del dm, dp, loc
             i = sh.info
             print("%s N=%d rank %d: %d owned, %d ghosts, tiles %d interior + %d boundary, %d ghost-adjacent "
                   "elements, halo %d/%d elements"
