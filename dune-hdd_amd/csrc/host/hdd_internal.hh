@@ -11,3 +11,13 @@ std::string& last_error_slot();
 int set_error(int code, const std::string& msg);
 int ctx_device(const hdd_ctx* ctx);   // HIP device ordinal a context is bound to
 }  // namespace hdd
+
+// Sharded-step fixup off the assembly stream (abi_device.hip, used by shard.hip): the element-list pass into side
+// buffers of hdd_fix_rb(elem_type) doubles per listed element (n + 1 slots per component), and the copy of those
+// row blocks into the value arrays.
+int hdd_fix_rb(int32_t elem_type);
+int hdd_assemble_elements_buf(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_fn* kappa, int32_t n_comp,
+                              const hdd_tensor_fn* tensor, const hdd_swipdg_params* p, const hdd_csr* pattern,
+                              double* const* d_bufs, const int32_t* d_elems, int64_t n_elems, void* stream);
+int hdd_scatter_fix(hdd_ctx* ctx, const hdd_csr* pattern, int32_t rb, double* const* d_bufs, int32_t n_comp,
+                    const int32_t* d_elems, int64_t n_elems, double* const* d_vals, void* stream);

@@ -241,7 +241,7 @@ static int assemble_hex(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_fn* ka
 static int assemble_impl(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_fn* kappa, int32_t n_comp,
                          const hdd_tensor_fn* tensor, const hdd_swipdg_params* p, const hdd_csr* pattern,
                          double* const* d_vals, const int32_t* d_tiles, int64_t n_tiles, void* stream,
-                         bool list_elements = false)
+                         int list_elements = 0)
 {
   using namespace hdd::dev;
   if (!ctx || !m || !kappa || !tensor || !p || !pattern || !d_vals)
@@ -292,7 +292,8 @@ static int assemble_impl(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_fn* k
   a.beta = p->beta;
   a.tile_list = d_tiles;
   a.n_tile_list = n_tiles;
-  a.list_elements = list_elements ? 1 : 0;
+  a.list_elements = list_elements;
+  a.fix_rb = (m->elem_type == HDD_SIMPLEX ? 3 * 3 * 4 : 4 * 4 * 5);
   if (!m->elem_vertices != !m->vertex_coords)
     return set_error(HDD_ERR_INVALID, "hdd_swipdg_assemble: mesh elem_vertices / vertex_coords: both or neither");
   // vertex-indexed geometry (bit 16384 of HDD_DEBUG_FLAGS: A/B against the element-major coords)
@@ -360,7 +361,47 @@ extern "C" int hdd_swipdg_assemble_elements(hdd_ctx* ctx, const hdd_mesh* m, con
 {
   if (!d_elems && n_elems) return set_error(HDD_ERR_INVALID, "hdd_swipdg_assemble_elements: null element list");
   if (n_elems == 0) return HDD_OK;
-  return assemble_impl(ctx, m, kappa, n_comp, tensor, p, pattern, d_vals, d_elems, n_elems, stream, true);
+  return assemble_impl(ctx, m, kappa, n_comp, tensor, p, pattern, d_vals, d_elems, n_elems, stream, 1);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Sharded-step fixup off the assembly stream (shard.hip): the element-list pass writes each listed element's row
+// block into a side buffer (slot fix_rb(m) doubles, one buffer of n + 1 slots per component) on the transfer
+// stream while the full-range assembly runs; after the join, fix_scatter_kernel copies the blocks into place.
+// ------------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(64) fix_scatter_kernel(const double* __restrict__ buf, int32_t rb,
+                                                         const int32_t* __restrict__ list, int64_t n,
+                                                         const int64_t* __restrict__ elem_ptr, double* vals)
+{
+  for (int64_t i = blockIdx.x; i < n; i += gridDim.x) {
+    const int64_t el = list[i];
+    const int64_t b = elem_ptr[el], len = elem_ptr[el + 1] - b;
+    for (int64_t k = threadIdx.x; k < len; k += 64) vals[b + k] = buf[i * rb + k];
+  }
+}
+
+int hdd_fix_rb(int32_t elem_type) { return elem_type == HDD_SIMPLEX ? 3 * 3 * 4 : 4 * 4 * 5; }
+
+int hdd_assemble_elements_buf(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_fn* kappa, int32_t n_comp,
+                              const hdd_tensor_fn* tensor, const hdd_swipdg_params* p, const hdd_csr* pattern,
+                              double* const* d_bufs, const int32_t* d_elems, int64_t n_elems, void* stream)
+{
+  if (n_elems == 0) return HDD_OK;
+  return assemble_impl(ctx, m, kappa, n_comp, tensor, p, pattern, d_bufs, d_elems, n_elems, stream, 2);
+}
+
+int hdd_scatter_fix(hdd_ctx* ctx, const hdd_csr* pattern, int32_t rb, double* const* d_bufs, int32_t n_comp,
+                    const int32_t* d_elems, int64_t n_elems, double* const* d_vals, void* stream)
+{
+  if (n_elems == 0) return HDD_OK;
+  const unsigned grid = unsigned(std::min<int64_t>(n_elems, int64_t(ctx->n_cu) * 8));
+  for (int32_t c = 0; c < n_comp; ++c) {
+    hipLaunchKernelGGL(fix_scatter_kernel, dim3(grid), dim3(64), 0, static_cast<hipStream_t>(stream), d_bufs[c], rb,
+                       d_elems, n_elems, pattern->elem_ptr, d_vals[c]);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "hdd_scatter_fix");
+  }
+  return HDD_OK;
 }
 
 // ------------------------------------------------------------------------------------------------

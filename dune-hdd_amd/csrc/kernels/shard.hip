@@ -407,6 +407,8 @@ struct hdd_shard {
   // RCCL path runs them on the transfer stream; created on first use
   hipStream_t aux = nullptr;
   hipEvent_t ev_in = nullptr, ev_out = nullptr;
+  double* d_fixbuf = nullptr;          // side buffers of the off-stream fixup (n_comp x (n_fix + 1) x fix_rb)
+  size_t fixbuf_doubles = 0;
 };
 
 extern "C" void hdd_shard_destroy(hdd_shard* sh)
@@ -420,7 +422,7 @@ extern "C" void hdd_shard_destroy(hdd_shard* sh)
                   static_cast<void*>(sh->d_gid), static_cast<void*>(sh->d_send_idx), static_cast<void*>(sh->d_sbuf),
                   static_cast<void*>(sh->d_rbuf), static_cast<void*>(sh->d_tiles_in),
                   static_cast<void*>(sh->d_tiles_bd), static_cast<void*>(sh->d_ev), static_cast<void*>(sh->d_vxy),
-                  static_cast<void*>(sh->d_fix)})
+                  static_cast<void*>(sh->d_fix), static_cast<void*>(sh->d_fixbuf)})
     if (p) (void)hipFree(p);
   if (sh->local) hdd_local_destroy(sh->local);
   delete sh;
@@ -729,10 +731,11 @@ extern "C" int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm*
   // `stream` starts the assembly at once -- the pack launch is off the critical path.  (The host transport
   // stages through the host on `stream` anyway.)
   hipStream_t ps = s;
-  if (overlap && !split && (transfer ? comm->kind != hdd_comm::HOST : true)) {
-    if (transfer) {
+  const bool side = overlap && !split;
+  if (side) {
+    if (transfer && comm->kind != hdd_comm::HOST) {
       ps = comm->xfer;
-    } else {
+    } else {   // loopback study, host transport (which stages through the host on this stream)
       if (!sh->aux) {
         e = hipStreamCreateWithFlags(&sh->aux, hipStreamNonBlocking);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&sh->ev_in, hipEventDisableTiming);
@@ -745,9 +748,28 @@ extern "C" int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm*
       e = hipEventCreateWithFlags(&sh->ev_in, hipEventDisableTiming);
       if (e != hipSuccess) return hip_fail(e, "hdd_block_assemble_sharded: event");
     }
+    if (!sh->ev_out) {
+      e = hipEventCreateWithFlags(&sh->ev_out, hipEventDisableTiming);
+      if (e != hipSuccess) return hip_fail(e, "hdd_block_assemble_sharded: event");
+    }
     e = hipEventRecord(sh->ev_in, s);
     if (e == hipSuccess) e = hipStreamWaitEvent(ps, sh->ev_in, 0);
     if (e != hipSuccess) return hip_fail(e, "hdd_block_assemble_sharded: order pack after inputs");
+  }
+  const bool offfix = side && !(flags & HDD_SHARD_FIX_INLINE) && sh->n_fix > 0;
+  const int32_t rb = hdd_fix_rb(sh->gi.elem_type);
+  std::vector<double*> fbufs;
+  if (offfix) {
+    const size_t slot = size_t(sh->n_fix + 1) * size_t(rb), need = slot * size_t(n_comp);
+    if (need > sh->fixbuf_doubles) {   // first step (or more components): grow; warm up before graph capture
+      if (sh->d_fixbuf) (void)hipFree(sh->d_fixbuf);
+      sh->d_fixbuf = nullptr;
+      sh->fixbuf_doubles = 0;
+      e = hipMalloc(reinterpret_cast<void**>(&sh->d_fixbuf), need * sizeof(double));
+      if (e != hipSuccess) return hip_fail(e, "hdd_block_assemble_sharded: fixup buffer");
+      sh->fixbuf_doubles = need;
+    }
+    for (int32_t c = 0; c < n_comp; ++c) fbufs.push_back(sh->d_fixbuf + size_t(c) * slot);
   }
   // 1. pack the records the peers need (one launch for every peer)
   for (int k = 0; k <= h.n_peers; ++k) h.prefix[k] = sh->send_prefix[k];
@@ -779,6 +801,10 @@ extern "C" int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm*
       }
     }
     rc = hdd_comm_post(comm, int32_t(mp.size()), mp.data(), ms.data(), mn.data(), mr.data(), mrn.data(), ps);
+    // host transport on the side stream, fixup on `stream`: the ghost columns were written on ps
+    if (rc == HDD_OK && side && !offfix && ps != s && comm->kind == hdd_comm::HOST &&
+        hipEventRecord(sh->ev_out, ps) != hipSuccess)
+      rc = set_error(HDD_ERR_HIP, "hdd_block_assemble_sharded: host transport event");
   } else {   // timing studies: the receive buffers get this rank's own messages (stream-ordered device copies)
     std::vector<const double*> sp(size_t(h.n_peers));
     std::vector<double*> rp(size_t(h.n_peers));
@@ -798,6 +824,30 @@ extern "C" int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm*
       rc = set_error(HDD_ERR_HIP, "hdd_block_assemble_sharded: loopback event");
   }
   if (rc) return rc;
+  // 2b. off-stream fixup (default with a side stream): on the stream the halo lands on, right after it, the
+  // ghost-adjacent elements into the side buffer -- concurrent with the assembly below, which needs the LDS this
+  // pass does without; the loopback study unpacks there first
+  bool fix_pending = false, fix_unsupported = false;
+  if (offfix) {
+    if (!transfer) {
+      for (int k = 0; k <= h.n_peers; ++k) h.prefix[k] = sh->recv_prefix[k];
+      for (int k = 0; k < h.n_peers; ++k) h.col0[k] = sh->recv_col0[k];
+      h.idx = nullptr;
+      h.buf = sh->d_rbuf;
+      e = launch_halo(false, h, ps);
+      if (e != hipSuccess) return hip_fail(e, "hdd_block_assemble_sharded: unpack");
+    }
+    rc = hdd_assemble_elements_buf(ctx, &m, kappa, n_comp, tensor, params, pattern, fbufs.data(), sh->d_fix, sh->n_fix,
+                                   ps);
+    if (rc == HDD_ERR_UNSUPPORTED) fix_unsupported = true;   // no list kernel for these rules: range again below
+    else if (rc) {
+      if (transfer) (void)hdd_comm_wait(comm, stream);
+      return rc;
+    }
+    e = hipEventRecord(sh->ev_out, ps);
+    if (e != hipSuccess) return hip_fail(e, "hdd_block_assemble_sharded: record fixup");
+    fix_pending = true;
+  }
   // 3. the assembly overlaps the transfer.  Default: EVERY tile (one full-size launch at full rate; the row
   // blocks of the ghost-adjacent elements read ghost columns the receives are still writing and are recomputed
   // in 5).  HDD_SHARD_SPLIT_TILES: the interior tiles only (the kernels that take lists: P1 / Q1 persistent
@@ -816,7 +866,17 @@ extern "C" int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm*
   if (transfer) {
     rc = hdd_comm_wait(comm, stream);
     if (rc) return rc;
-  } else {
+    if (side && !offfix && ps != s && comm->kind == hdd_comm::HOST && hipStreamWaitEvent(s, sh->ev_out, 0) != hipSuccess)
+      return set_error(HDD_ERR_HIP, "hdd_block_assemble_sharded: wait host transport");
+  }
+  if (fix_pending) {   // join the off-stream fixup, move its row blocks into place
+    e = hipStreamWaitEvent(s, sh->ev_out, 0);
+    if (e != hipSuccess) return hip_fail(e, "hdd_block_assemble_sharded: join fixup");
+    if (!fix_unsupported)
+      return hdd_scatter_fix(ctx, pattern, rb, fbufs.data(), n_comp, sh->d_fix, sh->n_fix, d_vals, stream);
+    return hdd_swipdg_assemble(ctx, &m, kappa, n_comp, tensor, params, pattern, d_vals, stream);
+  }
+  if (!transfer) {
     if (ps != s && hipStreamWaitEvent(s, sh->ev_out, 0) != hipSuccess)
       return set_error(HDD_ERR_HIP, "hdd_block_assemble_sharded: wait loopback");
     for (int k = 0; k <= h.n_peers; ++k) h.prefix[k] = sh->recv_prefix[k];

@@ -1943,6 +1943,38 @@ __global__ void __launch_bounds__(64) swipdg_elements_kernel(const AssembleArgs 
   }
 }
 
+// Element-list pass into a side buffer (a.list_elements == 2): lane i writes the row block of listed element i
+// straight to a.vals[c] + i RB (slot n: the inactive lanes' dummy), no LDS image -- so that the pass can run
+// on the transfer stream beside a persistent assembly that holds the LDS, and fix_scatter_kernel moves the
+// blocks into place afterwards (sharded step, shard.hip).
+template <class P>
+__global__ void __launch_bounds__(64) swipdg_elements_buf_kernel(const AssembleArgs a, int64_t n)
+{
+  constexpr int RB = P::RB;
+  constexpr bool FUSED = fused_of<P>::value;
+  const int lane = threadIdx.x;
+  for (int64_t i0 = int64_t(blockIdx.x) * 64; i0 < n; i0 += int64_t(gridDim.x) * 64) {
+    const int64_t i = i0 + lane;
+    const bool act = i < n;
+    const int64_t e = a.own_begin + int64_t(a.tile_list[act ? i : i0]);
+    const int64_t slot = act ? i : n;
+    typename P::Own own;
+    typename P::Gat gat;
+    P::load_own(a, e, own);
+    P::load_gat(a, e, own, gat);
+    P::load_gat2(a, gat);
+    [[maybe_unused]] typename fused_of<P>::Shared shv;
+    if constexpr (FUSED) P::prepare(a, own, shv);
+    const int ncomp = FUSED ? a.n_comp : 1;
+    for (int c = 0; c < ncomp; ++c) {
+      double* img = a.vals[c] + slot * RB;
+      if constexpr (FUSED) P::emit_component(a, c, e, own, gat, shv, img);
+      else if constexpr (P::PAD) P::compute(a, e, own, gat, RotImg<RB>{img, 0});
+      else P::compute(a, e, own, gat, img);
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------------------
 // host-side launch
 // ------------------------------------------------------------------------------------------------
@@ -1984,6 +2016,21 @@ static hipError_t launch_persistent(const AssembleArgs& a, hipStream_t s)
   if (a.list_elements) {   // element-list fixup pass: one lane per element
     const size_t lds_e = size_t(64) * P::RB * sizeof(double);
     const int64_t ge = std::min<int64_t>((a.n_tile_list + 63) / 64, int64_t(cus) * 4);
+    if (a.list_elements == 2) {   // into the side buffers (slot RB doubles), no LDS
+      if (a.fix_rb != P::RB) return hipErrorInvalidValue;
+      for (int c = 0; c < n_launch; ++c) {
+        AssembleArgs ac = a;
+        if (!fused_of<P>::value) {
+          ac.n_comp = 1;
+          ac.kappa[0] = a.kappa[c];
+          ac.vals[0] = a.vals[c];
+        }
+        hipLaunchKernelGGL((swipdg_elements_buf_kernel<P>), dim3(unsigned(ge)), dim3(64), 0, s, ac, a.n_tile_list);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+      }
+      return hipSuccess;
+    }
     for (int c = 0; c < n_launch; ++c) {
       AssembleArgs ac = a;
       if (!fused_of<P>::value) {

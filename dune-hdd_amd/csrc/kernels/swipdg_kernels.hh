@@ -33,7 +33,9 @@ struct AssembleArgs {
   int32_t debug_flags, wgcu;   // ablation switches (HDD_DEBUG_FLAGS, 0 in production); wgcu: tiles per CU override (0: policy default)
   const int32_t* tile_list;    // optional: 64-element tiles to assemble (relative to own_begin)
   int64_t n_tile_list;         // entries of tile_list (tile_list == nullptr: all tiles)
-  int32_t list_elements, pad_le;   // 1: tile_list holds single owned elements (relative to own_begin), not tiles
+  int32_t list_elements;       // 1: tile_list holds single owned elements (relative to own_begin), not tiles;
+                               // 2: the same, row blocks into side buffers vals[c] of fix_rb doubles per element
+  int32_t fix_rb;
   const int32_t* ev;           // optional vertex-indexed geometry: element -> local vertex ids [nvpe][n_local]
   const double* vxy;           //   and the vertex coordinates [n_vertices][2] (hdd_mesh elem_vertices / vertex_coords)
   KappaArg kappa[HDD_MAX_COMP];

@@ -64,6 +64,9 @@ CASES = {
     "p1_sym_two_comp": (H.SIMPLEX, 36, 12, 4, 2, H.TENSOR_SYM_PER_ELEM, 0, True),
     "q1_iso_overlap_2x2": (H.CUBE, 44, 15, 4, 2, H.TENSOR_ISO_PER_ELEM, 0, True),
     "q1_iso_split_tiles": (H.CUBE, 44, 15, 4, 2, H.TENSOR_ISO_PER_ELEM, H.SHARD_SPLIT_TILES, True),
+    # default overlap = the fixup on the side stream into a side buffer + the copy kernel; FIX_INLINE = round 2's
+    "q1_iso_fix_inline": (H.CUBE, 44, 15, 4, 2, H.TENSOR_ISO_PER_ELEM, H.SHARD_FIX_INLINE, True),
+    "p1_sym_fix_inline": (H.SIMPLEX, 36, 12, 4, 2, H.TENSOR_SYM_PER_ELEM, H.SHARD_FIX_INLINE, False),
 }
 
 
@@ -248,3 +251,10 @@ def test_no_transfer_flag_keeps_interior_rows():
     assert touches.any() and not touches.all()
     for e in np.flatnonzero(~touches)[:: 7]:
         assert np.array_equal(got[epv[e]:epv[e + 1]], want[epv[e]:epv[e + 1]]), e
+    # the same (loopback) ghost values through the three step schedules: off-stream fixup + copy kernel
+    # (default), fixup on the stream after the join (FIX_INLINE), exchange first (NO_OVERLAP) -- bit for bit
+    for fl in (H.SHARD_FIX_INLINE, H.SHARD_NO_OVERLAP):
+        w = [torch.full((sh.info.nnz,), float("nan"), dtype=torch.float64, device="cuda")]
+        H.assemble_sharded(ctx, sh, None, kap, tensor, pat, w, flags=H.SHARD_NO_TRANSFER | fl)
+        torch.cuda.synchronize()
+        assert np.array_equal(w[0].cpu().numpy().view(np.int64), got.view(np.int64)), fl

@@ -45,3 +45,59 @@ def test_trig_phase_matches_libm(tmp_path):
     v = np.frombuffer(out, np.float64).reshape(-1, 2)
     assert np.max(np.abs(v[:, 0] - np.sin(x))) <= 4.5e-16
     assert np.max(np.abs(v[:, 1] - np.cos(x))) <= 4.5e-16
+
+
+DRIVER_NEAR = r"""
+#include <cstdio>
+#include <cstdlib>
+#include "trig_phase.hh"
+int main(int argc, char** argv) {
+  FILE* f = std::fopen(argv[1], "rb");
+  long n = std::atol(argv[2]);
+  double* x = (double*)std::malloc(2 * n * sizeof(double));
+  if (std::fread(x, sizeof(double), 2 * n, f) != (size_t)(2 * n)) return 2;
+  std::fclose(f);
+  for (long i = 0; i < n; ++i) {
+    double s0, c0;
+    hdd::dev::sincos_phase(x[2 * i], s0, c0);
+    double v[4] = {s0, c0, hdd::dev::sin_near(s0, c0, x[2 * i + 1]), hdd::dev::cos_near(s0, c0, x[2 * i + 1])};
+    std::fwrite(v, sizeof(double), 4, stdout);
+  }
+  return 0;
+}
+"""
+
+
+def test_sincos_phase_and_small_offsets(tmp_path):
+    """sincos_phase == (sin_phase, cos_phase) bit for bit; sin / cos of phi0 + d by the per-element reduction
+    and the Taylor offsets (|d| <= SMALL_PHASE = 0.125, the smooth-coefficient kernels' fast path) within a few
+    ulp of libm -- the same accuracy class as sin_phase itself."""
+    src = tmp_path / "drv.cpp"
+    src.write_text(DRIVER_NEAR)
+    exe = tmp_path / "drv"
+    subprocess.check_call(["g++", "-O2", "-ffp-contract=off", "-D__host__=", "-D__device__=",
+                           "-D__forceinline__=inline", "-I" + HDR, str(src), "-o", str(exe)])
+    rng = np.random.default_rng(4)
+    n = 200000
+    phi = np.concatenate([rng.uniform(-6 * np.pi, 6 * np.pi, n - 129), np.arange(-64, 65) * (np.pi / 4)])
+    d = rng.uniform(-0.125, 0.125, n)
+    d[:1000] = 0.0
+    inp = tmp_path / "x.bin"
+    np.stack([phi, d], 1).tofile(inp)
+    out = subprocess.run([str(exe), str(inp), str(n)], check=True, capture_output=True).stdout
+    v = np.frombuffer(out, np.float64).reshape(-1, 4)
+    # bit-identical to the single-value kernels
+    ref = tmp_path / "ref.cpp"
+    ref.write_text(DRIVER)
+    rexe = tmp_path / "ref"
+    subprocess.check_call(["g++", "-O2", "-ffp-contract=off", "-D__host__=", "-D__device__=",
+                           "-D__forceinline__=inline", "-I" + HDR, str(ref), "-o", str(rexe)])
+    phi.tofile(tmp_path / "p.bin")
+    r = np.frombuffer(subprocess.run([str(rexe), str(tmp_path / "p.bin"), str(n)], check=True,
+                                     capture_output=True).stdout, np.float64).reshape(-1, 2)
+    assert np.array_equal(v[:, :2].view(np.int64), r.view(np.int64))
+    # phi0 + d (not representable: compare with libm's addition formula, accurate to ~2 ulp of the values)
+    sref = np.sin(phi) * np.cos(d) + np.cos(phi) * np.sin(d)
+    cref = np.cos(phi) * np.cos(d) - np.sin(phi) * np.sin(d)
+    assert np.max(np.abs(v[:, 2] - sref)) <= 9e-16
+    assert np.max(np.abs(v[:, 3] - cref)) <= 9e-16
