@@ -266,13 +266,31 @@ __global__ __launch_bounds__(256) void rhs2d_kernel(RhsArgs a)
 #pragma unroll
     for (int i = 0; i < NB; ++i) acc[i] = 0.0;
     double v[NB], gx[NB], gy[NB], xq[2];
+    // cos products on elements small against the wavelength (wave-uniform): one sincos per direction and
+    // element, Taylor offsets per point (trig_phase.hh)
+    [[maybe_unused]] double sx0 = 0.0, cx0 = 0.0, sy0 = 0.0, cy0 = 0.0;
+    [[maybe_unused]] bool near = false;
+    if constexpr (FK == HDD_FN_COS_PRODUCT && NQ > 0) {
+      const double kx = a.force.kx, ky = a.force.ky;
+      near = __all(fabs(kx * j00) + fabs(kx * j01) <= SMALL_PHASE && fabs(ky * j10) + fabs(ky * j11) <= SMALL_PHASE);
+      if (near) {
+        sincos_phase(kx * x0, sx0, cx0);
+        sincos_phase(ky * y0, sy0, cy0);
+      }
+    }
     auto vol_point = [&](int q) {
       const double xh = a.qv[q][0], yh = a.qv[q][1];
       xq[0] = x0 + j00 * xh + j01 * yh;
       xq[1] = y0 + j10 * xh + j11 * yh;
       rhs2d_shape<TRI>(xh, yh, v, gx, gy);
       double f;
-      if constexpr (FK == HDD_FN_COS_PRODUCT) f = a.force.c * cos_phase(a.force.kx * xq[0]) * cos_phase(a.force.ky * xq[1]);
+      if constexpr (FK == HDD_FN_COS_PRODUCT) {
+        if (near)
+          f = a.force.c * cos_near(sx0, cx0, a.force.kx * (j00 * xh + j01 * yh)) *
+              cos_near(sy0, cy0, a.force.ky * (j10 * xh + j11 * yh));
+        else
+          f = a.force.c * cos_phase(a.force.kx * xq[0]) * cos_phase(a.force.ky * xq[1]);
+      }
       else f = rhs_fn(a.force, e, xq, 2);
       const double fv = a.qv[q][3] * adet * f;
 #pragma unroll

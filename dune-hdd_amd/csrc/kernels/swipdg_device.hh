@@ -1348,6 +1348,23 @@ struct P1SmoothPolicy {
     };
     const double j00 = o.X[1] - o.X[0], j01 = o.X[2] - o.X[0], j10 = o.Y[1] - o.Y[0], j11 = o.Y[2] - o.Y[0];
     double kv = 0.0;   // sum_q w_q kappa(x_q), Dunavant 6
+    if constexpr (KK == HDD_FN_SINUSOID) {   // small elements: one reduction per element (see the fused policy)
+      const double d1 = K.kx * j00 + K.ky * j10, d2 = K.kx * j01 + K.ky * j11;
+      if (__all(fabs(d1) + fabs(d2) <= SMALL_PHASE)) {
+        double s0, c0;
+        sincos_phase(K.kx * o.X[0] + K.ky * o.Y[0], s0, c0);
+#pragma unroll
+        for (int q = 0; q < 6; ++q)
+          kv += VolRule<Simplex, 6>::w(q) *
+                (K.c + K.b * sin_near(s0, c0, VolRule<Simplex, 6>::x(q) * d1 + VolRule<Simplex, 6>::y(q) * d2));
+        const double dv[3] = {0.0, d1, d2};
+        emit(a, e, o, gt, img, kv, [&](int f, double, double, int q) {
+          const double da = dv[Simplex::fv(f, 0)], db = dv[Simplex::fv(f, 1)];
+          return K.c + K.b * sin_near(s0, c0, da + Gauss01<3>::s(q) * (db - da));
+        });
+        return;
+      }
+    }
 #pragma unroll
     for (int q = 0; q < 6; ++q) {
       const double xh = VolRule<Simplex, 6>::x(q), yh = VolRule<Simplex, 6>::y(q);
@@ -1509,6 +1526,25 @@ struct P1SmoothFusedPolicy : P1SmoothPolicy<TK, VX> {
     const KappaArg& K = a.kappa[0];   // the phase (kx, ky) every fused component shares
     const double j00 = o.X[1] - o.X[0], j01 = o.X[2] - o.X[0], j10 = o.Y[1] - o.Y[0], j11 = o.Y[2] - o.Y[0];
     sh.sv = 0.0;
+    // phase = p0 + xh d1 + yh d2 on the element; when every lane's element is small against the wavelength
+    // (|d1| + |d2| <= SMALL_PHASE, wave-uniform), one reduction per element (sincos of p0) and Taylor offsets
+    // per point (trig_phase.hh) instead of 15 full reductions
+    const double d1 = K.kx * j00 + K.ky * j10, d2 = K.kx * j01 + K.ky * j11;
+    if (__all(fabs(d1) + fabs(d2) <= SMALL_PHASE)) {
+      double s0, c0;
+      sincos_phase(K.kx * o.X[0] + K.ky * o.Y[0], s0, c0);
+#pragma unroll
+      for (int q = 0; q < 6; ++q)
+        sh.sv += VolRule<Simplex, 6>::w(q) * sin_near(s0, c0, VolRule<Simplex, 6>::x(q) * d1 + VolRule<Simplex, 6>::y(q) * d2);
+      const double dv[3] = {0.0, d1, d2};
+#pragma unroll
+      for (int f = 0; f < 3; ++f) {
+        const double da = dv[E::fv(f, 0)], db = dv[E::fv(f, 1)];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) sh.sf[f][q] = sin_near(s0, c0, da + Gauss01<3>::s(q) * (db - da));
+      }
+      return;
+    }
 #pragma unroll
     for (int q = 0; q < 6; ++q) {
       const double xh = VolRule<Simplex, 6>::x(q), yh = VolRule<Simplex, 6>::y(q);

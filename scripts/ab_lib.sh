@@ -8,7 +8,7 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout
 rc=$?; echo "pytest rc=$rc"; tail -2 $OUT/pytest.log; [ $rc -eq 0 ] || exit $rc
 for rep in 1 2 3; do
   for L in $A $B; do
-    n=$(basename $L .so)
+    n=$(basename $(dirname $L))_$(basename $L .so)
     HDD_AMD_LIB=$PWD/$L timeout -k 10 200 python scripts/bench_configs.py ${CONFIGS:-c3} --samples 16 > $OUT/${n}_$rep.log 2>&1
     rc=$?; [ $rc -eq 0 ] || { echo "$n rc=$rc"; exit $rc; }
     echo "$n $(grep -oE '"(assembly_ms|rhs_ms|pattern_ms)": [0-9.]*' $OUT/${n}_$rep.log | tr '\n' ' ')"
