@@ -21,3 +21,10 @@ int hdd_assemble_elements_buf(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_
                               double* const* d_bufs, const int32_t* d_elems, int64_t n_elems, void* stream);
 int hdd_scatter_fix(hdd_ctx* ctx, const hdd_csr* pattern, int32_t rb, double* const* d_bufs, int32_t n_comp,
                     const int32_t* d_elems, int64_t n_elems, double* const* d_vals, void* stream);
+// the same pass in place (no side buffer), beside a full-range assembly that skips those elements' row blocks
+int hdd_assemble_elements_inplace(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_fn* kappa, int32_t n_comp,
+                                  const hdd_tensor_fn* tensor, const hdd_swipdg_params* p, const hdd_csr* pattern,
+                                  double* const* d_vals, const int32_t* d_elems, int64_t n_elems, void* stream);
+int hdd_assemble_skip_ghost(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_fn* kappa, int32_t n_comp,
+                            const hdd_tensor_fn* tensor, const hdd_swipdg_params* p, const hdd_csr* pattern,
+                            double* const* d_vals, void* stream);

@@ -757,9 +757,15 @@ extern "C" int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm*
     if (e != hipSuccess) return hip_fail(e, "hdd_block_assemble_sharded: order pack after inputs");
   }
   const bool offfix = side && !(flags & HDD_SHARD_FIX_INLINE) && sh->n_fix > 0;
+  // where the fixup writes: in place beside a tile launch that skips those row blocks, or a side buffer + one
+  // copy kernel after the join.  Default by element type, from the one-card step study (profiles/r03/ab_skip/,
+  // worst rank of N = 8): Q1 in place (+10 % middle / +21 % end rank vs +21 / +15 %), P1 side buffer (+8 % vs
+  // +12 % middle rank: the P1 tiles' two waves per SIMD leave the element pass no registers beside them)
+  const bool scatter = offfix && !(flags & HDD_SHARD_FIX_INPLACE) &&
+                       ((flags & HDD_SHARD_FIX_SCATTER) || sh->gi.elem_type == HDD_SIMPLEX);
   const int32_t rb = hdd_fix_rb(sh->gi.elem_type);
   std::vector<double*> fbufs;
-  if (offfix) {
+  if (scatter) {
     const size_t slot = size_t(sh->n_fix + 1) * size_t(rb), need = slot * size_t(n_comp);
     if (need > sh->fixbuf_doubles) {   // first step (or more components): grow; warm up before graph capture
       if (sh->d_fixbuf) (void)hipFree(sh->d_fixbuf);
@@ -837,8 +843,10 @@ extern "C" int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm*
       e = launch_halo(false, h, ps);
       if (e != hipSuccess) return hip_fail(e, "hdd_block_assemble_sharded: unpack");
     }
-    rc = hdd_assemble_elements_buf(ctx, &m, kappa, n_comp, tensor, params, pattern, fbufs.data(), sh->d_fix, sh->n_fix,
-                                   ps);
+    rc = scatter ? hdd_assemble_elements_buf(ctx, &m, kappa, n_comp, tensor, params, pattern, fbufs.data(), sh->d_fix,
+                                             sh->n_fix, ps)
+                 : hdd_assemble_elements_inplace(ctx, &m, kappa, n_comp, tensor, params, pattern, d_vals, sh->d_fix,
+                                                 sh->n_fix, ps);
     if (rc == HDD_ERR_UNSUPPORTED) fix_unsupported = true;   // no list kernel for these rules: range again below
     else if (rc) {
       if (transfer) (void)hdd_comm_wait(comm, stream);
@@ -853,9 +861,12 @@ extern "C" int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm*
   // in 5).  HDD_SHARD_SPLIT_TILES: the interior tiles only (the kernels that take lists: P1 / Q1 persistent
   // policies) -- a second launch of whole boundary tiles later, which on thin strips is a large fraction.
   if (overlap) {
+    // in-place fixup running: the tiles leave the ghost-adjacent elements' row blocks to it
+    const bool skip = fix_pending && !scatter && !fix_unsupported;
     rc = split ? hdd_swipdg_assemble_tiles(ctx, &m, kappa, n_comp, tensor, params, pattern, d_vals, sh->d_tiles_in,
                                            sh->n_in, stream)
-               : hdd_swipdg_assemble(ctx, &m, kappa, n_comp, tensor, params, pattern, d_vals, stream);
+         : skip ? hdd_assemble_skip_ghost(ctx, &m, kappa, n_comp, tensor, params, pattern, d_vals, stream)
+                : hdd_swipdg_assemble(ctx, &m, kappa, n_comp, tensor, params, pattern, d_vals, stream);
     if (rc == HDD_ERR_UNSUPPORTED && split) overlap = false;   // no tile-list kernel: everything after the halo
     else if (rc) {
       if (transfer) (void)hdd_comm_wait(comm, stream);
@@ -872,9 +883,9 @@ extern "C" int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm*
   if (fix_pending) {   // join the off-stream fixup, move its row blocks into place
     e = hipStreamWaitEvent(s, sh->ev_out, 0);
     if (e != hipSuccess) return hip_fail(e, "hdd_block_assemble_sharded: join fixup");
-    if (!fix_unsupported)
-      return hdd_scatter_fix(ctx, pattern, rb, fbufs.data(), n_comp, sh->d_fix, sh->n_fix, d_vals, stream);
-    return hdd_swipdg_assemble(ctx, &m, kappa, n_comp, tensor, params, pattern, d_vals, stream);
+    if (fix_unsupported) return hdd_swipdg_assemble(ctx, &m, kappa, n_comp, tensor, params, pattern, d_vals, stream);
+    if (scatter) return hdd_scatter_fix(ctx, pattern, rb, fbufs.data(), n_comp, sh->d_fix, sh->n_fix, d_vals, stream);
+    return HDD_OK;   // in place: the join alone completes the step on `stream`
   }
   if (!transfer) {
     if (ps != s && hipStreamWaitEvent(s, sh->ev_out, 0) != hipSuccess)

@@ -74,10 +74,10 @@ hipError_t launch_assemble(const AssembleArgs& a, int nqv, int nqf, hipStream_t 
   *supported = true;
   if (!(a.debug_flags & 64)) {
     const hipError_t e = launch_components(a, nqv, nqf, s, supported);
-    if (*supported || a.tile_list) return e;
+    if (*supported || a.tile_list || a.skip_ghost) return e;
     *supported = true;   // fall through to the wave-per-row kernels for the remaining rules
   }
-  if (a.tile_list) {
+  if (a.tile_list || a.skip_ghost) {   // (the wave-per-row kernels take neither lists nor skipped elements)
     *supported = false;
     return hipSuccess;
   }

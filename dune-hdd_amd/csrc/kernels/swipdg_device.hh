@@ -862,6 +862,7 @@ __device__ __forceinline__ void p1_compute(const AssembleArgs& a, int64_t e, con
 }
 
 typedef int ivec4 __attribute__((ext_vector_type(4)));
+typedef int ivec2 __attribute__((ext_vector_type(2)));
 
 // ------------------------------------------------------------------------------------------------
 // Generic thread-per-element policy (Q1 parallelograms, smooth coefficients): quadrature at compile-time
@@ -1738,7 +1739,9 @@ struct fused_of<P, std::void_t<decltype(P::FUSED)>> : std::bool_constant<P::FUSE
   using Shared = typename P::Shared;
 };
 
-template <class P, bool TL>   // TL: tiles come from a.tile_list, else 0..n_tiles-1
+// TL: tiles come from a.tile_list, else 0..n_tiles-1; SKIP: the sharded step's full-range launch, which leaves
+// the row blocks of elements with a ghost face neighbour to the concurrent element pass (a.skip_ghost)
+template <class P, bool TL, bool SKIP = false>
 __global__ void __launch_bounds__(64, P::MINW)
 swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
 {
@@ -1828,6 +1831,15 @@ swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
     const int64_t base_al = base & ~int64_t(1);
     const int off = tile_offset<P::NB>(P::n_interior(own), active) + int(base - base_al);
     const int tlen = int(tile_end - base);
+    // sharded step (a.skip_ghost): the row blocks of elements with a ghost face neighbour are written by the
+    // element pass on the transfer stream, concurrently -- this tile must not store them (wave-uniform mask)
+    uint64_t gmask = 0;
+    if constexpr (SKIP) {
+      bool g = false;
+#pragma unroll
+      for (int f = 0; f < P::NF; ++f) g |= own.nbr[f] >= 0 && (own.nbr[f] < a.own_begin || own.nbr[f] >= a.own_end);
+      gmask = __ballot(active && g);
+    }
     const bool uni = P::PAD && tlen == RB * int(a.own_end - t0 < 64 ? a.own_end - t0 : 64);   // wave-uniform
     if constexpr (P::PAD) {
       const RotImg<RB> img{uni ? lds + lane * RB : (active ? lds + off : scratch), uni ? 2 * ((lane >> 1) & 15) : 0};
@@ -1852,7 +1864,75 @@ swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
     // store chunks k < ksplit go out before the gathers of tile t+1, the rest after them (production: all
     // after; the HDD_ABLATION study bits 128 / 256 move half / all of them in front)
     const int ksplit = HDD_ABL(a, 128) ? STORES / 2 : (HDD_ABL(a, 256) ? STORES : 0);
+    // tiles with skipped elements: uniform rotated tiles drop the skipped elements' chunks (element blocks are RB
+    // doubles apart and RB is even, so no 16-byte chunk straddles two elements); contiguous images test each
+    // chunk against the skipped elements' ranges
+    auto stores_skip = [&]() {
+      if (P::PAD && uni) {   // (Q1 row blocks are multiples of 16 doubles: base is even, start == base)
+        auto at = [](int d) {
+          const int l = d / RB, j = d - l * RB;
+          const int q = j + 2 * ((l >> 1) & 15);
+          return l * RB + (q < RB ? q : q - RB);
+        };
+        if (!(gmask & 1)) out[base] = lds[at(0)];
+        if (!((gmask >> ((tlen - 1) / RB)) & 1)) out[tile_end - 1] = lds[at(tlen - 1)];
+        const int dmax = tlen - 2;
+#pragma unroll 1   // (a rolled loop: the unrolled form's 40 offsets cost the main path 90 AGPRs)
+        for (int k = 0; k < STORES; ++k) {
+          const int d = 2 * (lane + 64 * k);
+          const dvec2 v = *reinterpret_cast<const dvec2*>(lds + at(d <= dmax ? d : 0));
+          const int o8 = ((gmask >> (d <= dmax ? d / RB : 0)) & 1) ? nbytes : d * 8;
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ivec4, v), rsrc, o8, 0, 2);
+        }
+      } else if (!uni) {
+        // contiguous image: the image ranges [b, e) of the skipped elements (a tile holds one or two -- a strip's
+        // row end and the next row's start) go to scalar registers, and each chunk tests its two doubles against
+        // them: one 16-byte store when neither is skipped, one 8-byte store when exactly one is
+        const int bo = off, be = off + P::NB * P::NB * (P::n_interior(own) + 1);
+        constexpr int NR = 4;
+        int rb[NR], re[NR];
+        uint64_t m = gmask;
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+          rb[i] = re[i] = 0;
+          if (m) {
+            const int l = __builtin_ctzll(m);
+            m &= m - 1;
+            rb[i] = __builtin_amdgcn_readlane(bo, l);
+            re[i] = __builtin_amdgcn_readlane(be, l);
+          }
+        }
+        auto skipped = [&](int d) {   // image position d inside a skipped element's block
+          bool r = false;
+#pragma unroll
+          for (int i = 0; i < NR; ++i) r |= d >= rb[i] && d < re[i];
+          for (uint64_t mm = m; mm; mm &= mm - 1) {   // more than NR skipped elements (uniform loop)
+            const int l = __builtin_ctzll(mm);
+            r |= d >= __builtin_amdgcn_readlane(bo, l) && d < __builtin_amdgcn_readlane(be, l);
+          }
+          return r;
+        };
+        const int a0 = int(start - base_al);   // image position of the first chunk
+        if (!skipped(int(base - base_al))) out[base] = lds[base - base_al];
+        if (!skipped(int(tile_end - 1 - base_al))) out[tile_end - 1] = lds[tile_end - 1 - base_al];
+#pragma unroll
+        for (int k = 0; k < STORES; ++k) {
+          const int idx = 2 * (lane + 64 * k);
+          const int li = idx < IMG ? idx : 0;
+          const dvec2 v = *reinterpret_cast<const dvec2*>(lds + a0 + li);
+          const bool s0 = skipped(a0 + li), s1 = skipped(a0 + li + 1);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ivec4, v), rsrc, s0 || s1 ? nbytes : idx * 8, 0, 2);
+          // mixed chunk: the unskipped half alone
+          const int o8 = s0 == s1 ? nbytes : (s0 ? idx * 8 + 8 : idx * 8);
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(ivec2, s0 ? v.y : v.x), rsrc, o8, 0, 2);
+        }
+      }
+    };
     auto stores = [&](bool front) {
+      if (gmask) {
+        if (!front) stores_skip();
+        return;
+      }
       if (P::PAD && uni) {
         auto at = [](int d) {   // rotated slot of the tile's CSR value d
           const int l = d / RB, j = d - l * RB;
@@ -1979,10 +2059,11 @@ __global__ void __launch_bounds__(64) swipdg_elements_kernel(const AssembleArgs 
   }
 }
 
-// Element-list pass into a side buffer (a.list_elements == 2): lane i writes the row block of listed element i
-// straight to a.vals[c] + i RB (slot n: the inactive lanes' dummy), no LDS image -- so that the pass can run
-// on the transfer stream beside a persistent assembly that holds the LDS, and fix_scatter_kernel moves the
-// blocks into place afterwards (sharded step, shard.hip).
+// Element-list pass without LDS, so that it runs on the transfer stream beside a persistent assembly that holds
+// the LDS (sharded step, shard.hip).  a.list_elements == 3: lane i writes the row block of listed element i in
+// place (the concurrent assembly runs with a.skip_ghost and leaves those blocks alone; inactive lanes repeat
+// lane 0's element); == 2: into side buffers a.vals[c] + i RB (slot n: the inactive lanes' dummy), which
+// fix_scatter_kernel copies into place after the join (round-3 A/B variant).
 template <class P>
 __global__ void __launch_bounds__(64) swipdg_elements_buf_kernel(const AssembleArgs a, int64_t n)
 {
@@ -2002,8 +2083,9 @@ __global__ void __launch_bounds__(64) swipdg_elements_buf_kernel(const AssembleA
     [[maybe_unused]] typename fused_of<P>::Shared shv;
     if constexpr (FUSED) P::prepare(a, own, shv);
     const int ncomp = FUSED ? a.n_comp : 1;
+    const int64_t dst = a.list_elements == 3 ? a.elem_ptr[e - a.own_begin] : slot * RB;
     for (int c = 0; c < ncomp; ++c) {
-      double* img = a.vals[c] + slot * RB;
+      double* img = a.vals[c] + dst;
       if constexpr (FUSED) P::emit_component(a, c, e, own, gat, shv, img);
       else if constexpr (P::PAD) P::compute(a, e, own, gat, RotImg<RB>{img, 0});
       else P::compute(a, e, own, gat, img);
@@ -2052,8 +2134,8 @@ static hipError_t launch_persistent(const AssembleArgs& a, hipStream_t s)
   if (a.list_elements) {   // element-list fixup pass: one lane per element
     const size_t lds_e = size_t(64) * P::RB * sizeof(double);
     const int64_t ge = std::min<int64_t>((a.n_tile_list + 63) / 64, int64_t(cus) * 4);
-    if (a.list_elements == 2) {   // into the side buffers (slot RB doubles), no LDS
-      if (a.fix_rb != P::RB) return hipErrorInvalidValue;
+    if (a.list_elements >= 2) {   // no LDS: into the side buffers (2: slot RB doubles) or in place (3)
+      if (a.list_elements == 2 && a.fix_rb != P::RB) return hipErrorInvalidValue;
       for (int c = 0; c < n_launch; ++c) {
         AssembleArgs ac = a;
         if (!fused_of<P>::value) {
@@ -2089,6 +2171,8 @@ static hipError_t launch_persistent(const AssembleArgs& a, hipStream_t s)
     }
     if (a.tile_list)
       hipLaunchKernelGGL((swipdg_persistent_kernel<P, true>), dim3(unsigned(G)), dim3(64), lds, s, ac, tiles);
+    else if (a.skip_ghost)
+      hipLaunchKernelGGL((swipdg_persistent_kernel<P, false, true>), dim3(unsigned(G)), dim3(64), lds, s, ac, tiles);
     else
       hipLaunchKernelGGL((swipdg_persistent_kernel<P, false>), dim3(unsigned(G)), dim3(64), lds, s, ac, tiles);
     const hipError_t e = hipGetLastError();

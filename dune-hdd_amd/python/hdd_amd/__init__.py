@@ -107,7 +107,8 @@ class ShardInfo(C.Structure):
 HOST_EXCHANGE_FN = C.CFUNCTYPE(C.c_int32, C.c_void_p, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_void_p),
                                C.POINTER(C.c_int64), C.POINTER(C.c_void_p), C.POINTER(C.c_int64))
 RCCL_ID_BYTES = 128
-SHARD_NO_OVERLAP, SHARD_HALO_GEOMETRY, SHARD_NO_HALO, SHARD_NO_TRANSFER, SHARD_SPLIT_TILES, SHARD_FIX_INLINE = 1, 2, 4, 8, 16, 32
+(SHARD_NO_OVERLAP, SHARD_HALO_GEOMETRY, SHARD_NO_HALO, SHARD_NO_TRANSFER, SHARD_SPLIT_TILES, SHARD_FIX_INLINE,
+ SHARD_FIX_SCATTER, SHARD_FIX_INPLACE) = 1, 2, 4, 8, 16, 32, 64, 128
 
 
 _LIB = None

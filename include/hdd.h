@@ -471,17 +471,21 @@ enum {
   HDD_SHARD_SPLIT_TILES = 16,   /* overlap by tiles (round 2): interior tiles during the exchange, the tiles with a
                                    ghost-adjacent element after it (default: every tile during the exchange, then
                                    the ghost-adjacent ELEMENTS again, hdd_swipdg_assemble_elements) */
-  HDD_SHARD_FIX_INLINE = 32     /* study (round 3 A/B): the ghost-adjacent elements recomputed on `stream` after
+  HDD_SHARD_FIX_INLINE = 32,    /* study (round 3 A/B): the ghost-adjacent elements recomputed on `stream` after
                                    the wait (default: on the transfer stream right after the receives, beside the
-                                   assembly, into a side buffer that one copy kernel moves into place after it) */
+                                   assembly) */
+  HDD_SHARD_FIX_SCATTER = 64,   /* the off-stream fixup into a side buffer, copied into place by one kernel after
+                                   the join (the assembly's tiles store every row block): default for P1 */
+  HDD_SHARD_FIX_INPLACE = 128   /* the off-stream fixup in place, the assembly's tiles skip those row blocks:
+                                   default for Q1 */
 };
 /* One sharded assembly step -- the LHS of BlockSWIPDG::init() for the owned subdomains: pack the halo
  * records (per-element tensor / kappa rows, [+ coordinates]) of the elements the peers need -> post the
  * exchange, one message per (peer, halo row), received straight into the ghost columns (the ghosts of one
- * owner are contiguous, recv_col0) -> every tile (the row blocks of ghost-adjacent elements read stale ghost
- * columns and are discarded); the ghost-adjacent elements (hdd_shard_info.halo_elements of them, one lane each)
- * are recomputed on the transfer stream as soon as their halo has landed, concurrently with the assembly, into
- * a shard-owned side buffer -> join -> one copy kernel overwrites their row blocks.  The per-element arrays
+ * owner are contiguous, recv_col0) -> every tile except the row blocks that read a ghost column; those
+ * elements (hdd_shard_info.halo_elements of them, one lane each) are computed on
+ * the transfer stream as soon as their halo has landed, concurrently with the assembly, whose tiles leave those
+ * row blocks to them -> join.  The per-element arrays
  * of `kappa` / `tensor` must span n_local columns: their owned columns are read and their GHOST COLUMNS ARE
  * WRITTEN by the receives.  comm may be NULL when the shard has no peers. */
 int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm* comm, const hdd_scalar_fn* kappa,

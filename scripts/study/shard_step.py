@@ -6,9 +6,10 @@ the assembly), for rank r of an N-rank decomposition of
 timed as
   (a) NO_HALO       -- the whole owned range in one launch (ghost columns valid): the kernel alone,
   (b) step          -- pack, loopback copy instead of the transfer (HDD_SHARD_NO_TRANSFER), unpack and the
-                       ghost-adjacent elements into a side buffer on the side stream, every tile on the main
-                       stream, join, one copy kernel: every launch of the real step, RCCL excluded,
-  (b') the same with the fixup after the join on the main stream (HDD_SHARD_FIX_INLINE, round 3 A/B),
+                       ghost-adjacent elements in place on the side stream, every other row block on the main
+                       stream, join: every launch of the real step, RCCL excluded,
+  (b') the same with the fixup after the join on the main stream (HDD_SHARD_FIX_INLINE, round 2),
+  (b'') the fixup into a side buffer, every tile, join, one copy kernel (HDD_SHARD_FIX_SCATTER),
   (c) serial step   -- the same without the overlap (one launch of all tiles after the unpack),
   (d) step, graph   -- (b) captured once into a hipGraph (torch.cuda.CUDAGraph) and replayed,
   (e) split tiles   -- round 2's overlap (HDD_SHARD_SPLIT_TILES): interior tiles, unpack, boundary tiles.
@@ -61,7 +62,9 @@ def main():
             runs = {
                 "a NO_HALO (one launch)": H.SHARD_NO_HALO,
                 "b step, no transfer": H.SHARD_NO_TRANSFER,
-                "b' step, fixup inline (round 3 A)": H.SHARD_NO_TRANSFER | H.SHARD_FIX_INLINE,
+                "b' step, fixup inline (round 2)": H.SHARD_NO_TRANSFER | H.SHARD_FIX_INLINE,
+                "b'' step, fixup + copy kernel": H.SHARD_NO_TRANSFER | H.SHARD_FIX_SCATTER,
+                "b''' step, fixup in place": H.SHARD_NO_TRANSFER | H.SHARD_FIX_INPLACE,
                 "c serial step, no transfer": H.SHARD_NO_TRANSFER | H.SHARD_NO_OVERLAP,
                 "e split tiles, no transfer": H.SHARD_NO_TRANSFER | H.SHARD_SPLIT_TILES,
             }

@@ -67,6 +67,8 @@ CASES = {
     # default overlap = the fixup on the side stream into a side buffer + the copy kernel; FIX_INLINE = round 2's
     "q1_iso_fix_inline": (H.CUBE, 44, 15, 4, 2, H.TENSOR_ISO_PER_ELEM, H.SHARD_FIX_INLINE, True),
     "p1_sym_fix_inline": (H.SIMPLEX, 36, 12, 4, 2, H.TENSOR_SYM_PER_ELEM, H.SHARD_FIX_INLINE, False),
+    "q1_sym_fix_scatter": (H.CUBE, 44, 15, 4, 2, H.TENSOR_SYM_PER_ELEM, H.SHARD_FIX_SCATTER, True),
+    "p1_iso_fix_inplace": (H.SIMPLEX, 40, 10, 4, 1, H.TENSOR_ISO_PER_ELEM, H.SHARD_FIX_INPLACE, False),
 }
 
 
@@ -253,7 +255,7 @@ def test_no_transfer_flag_keeps_interior_rows():
         assert np.array_equal(got[epv[e]:epv[e + 1]], want[epv[e]:epv[e + 1]]), e
     # the same (loopback) ghost values through the three step schedules: off-stream fixup + copy kernel
     # (default), fixup on the stream after the join (FIX_INLINE), exchange first (NO_OVERLAP) -- bit for bit
-    for fl in (H.SHARD_FIX_INLINE, H.SHARD_NO_OVERLAP):
+    for fl in (H.SHARD_FIX_INLINE, H.SHARD_FIX_SCATTER, H.SHARD_FIX_INPLACE, H.SHARD_NO_OVERLAP):
         w = [torch.full((sh.info.nnz,), float("nan"), dtype=torch.float64, device="cuda")]
         H.assemble_sharded(ctx, sh, None, kap, tensor, pat, w, flags=H.SHARD_NO_TRANSFER | fl)
         torch.cuda.synchronize()
