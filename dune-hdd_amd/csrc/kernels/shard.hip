@@ -758,11 +758,12 @@ extern "C" int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm*
   }
   const bool offfix = side && !(flags & HDD_SHARD_FIX_INLINE) && sh->n_fix > 0;
   // where the fixup writes: in place beside a tile launch that skips those row blocks, or a side buffer + one
-  // copy kernel after the join.  Default by element type, from the one-card step study (profiles/r03/ab_skip/,
-  // worst rank of N = 8): Q1 in place (+10 % middle / +21 % end rank vs +21 / +15 %), P1 side buffer (+8 % vs
-  // +12 % middle rank: the P1 tiles' two waves per SIMD leave the element pass no registers beside them)
+  // copy kernel after the join.  Default from the one-card step study (profiles/r03/shard_step/final/, N = 2 and
+  // 8): in place, except P1 ranks with two peers (C2 middle ranks: +10 % with the side buffer vs +14 % in place,
+  // the P1 tiles' two waves per SIMD leaving the element pass no registers beside them; end ranks +4 % in place
+  // vs +8 %); Q1 in place everywhere (+9 % middle / +15 % end rank at N = 8 vs +20 / +13 %)
   const bool scatter = offfix && !(flags & HDD_SHARD_FIX_INPLACE) &&
-                       ((flags & HDD_SHARD_FIX_SCATTER) || sh->gi.elem_type == HDD_SIMPLEX);
+                       ((flags & HDD_SHARD_FIX_SCATTER) || (sh->gi.elem_type == HDD_SIMPLEX && sh->peers.size() >= 2));
   const int32_t rb = hdd_fix_rb(sh->gi.elem_type);
   std::vector<double*> fbufs;
   if (scatter) {

@@ -475,9 +475,10 @@ enum {
                                    the wait (default: on the transfer stream right after the receives, beside the
                                    assembly) */
   HDD_SHARD_FIX_SCATTER = 64,   /* the off-stream fixup into a side buffer, copied into place by one kernel after
-                                   the join (the assembly's tiles store every row block): default for P1 */
+                                   the join (the assembly's tiles store every row block): default for P1 shards
+                                   with two or more peers */
   HDD_SHARD_FIX_INPLACE = 128   /* the off-stream fixup in place, the assembly's tiles skip those row blocks:
-                                   default for Q1 */
+                                   default otherwise */
 };
 /* One sharded assembly step -- the LHS of BlockSWIPDG::init() for the owned subdomains: pack the halo
  * records (per-element tensor / kappa rows, [+ coordinates]) of the elements the peers need -> post the
