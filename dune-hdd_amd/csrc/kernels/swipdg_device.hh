@@ -1920,7 +1920,8 @@ swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
           const int idx = 2 * (lane + 64 * k);
           const int li = idx < IMG ? idx : 0;
           const dvec2 v = *reinterpret_cast<const dvec2*>(lds + a0 + li);
-          const bool s0 = skipped(a0 + li), s1 = skipped(a0 + li + 1);
+          // (even blocks, Q1: a chunk's two doubles always share an element)
+          const bool s0 = skipped(a0 + li), s1 = (P::NB * P::NB) % 2 == 1 ? skipped(a0 + li + 1) : s0;
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ivec4, v), rsrc, s0 || s1 ? nbytes : idx * 8, 0, 2);
           if constexpr ((P::NB * P::NB) % 2 == 1) {   // odd blocks (P1): a mixed chunk's unskipped half alone
             const int o8 = s0 == s1 ? nbytes : (s0 ? idx * 8 + 8 : idx * 8);
