@@ -38,7 +38,6 @@ struct AssembleArgs {
                                // 3: the same, in place without LDS (beside a skip_ghost assembly)
   int32_t fix_rb;
   int32_t skip_ghost, pad_sg;  // 1: tiles do not store the row blocks of elements with a ghost face neighbour
-  const double* rec;           // study (HDD_ABLATION, bit 1024): element-major Q1 records [n_local][10] (4 vertices, 4 neighbour ids)
   const int32_t* ev;           // optional vertex-indexed geometry: element -> local vertex ids [nvpe][n_local]
   const double* vxy;           //   and the vertex coordinates [n_vertices][2] (hdd_mesh elem_vertices / vertex_coords)
   KappaArg kappa[HDD_MAX_COMP];
