@@ -34,6 +34,8 @@ struct hdd_ctx {
   void* ops_h = nullptr;       //   its pinned host staging copy (reused once the last upload has completed)
   size_t ops_bytes = 0;
   hipEvent_t ops_evt = nullptr;
+  void* rhs_ws = nullptr;      // 2d RHS boundary-element list (counters zero between calls)
+  size_t rhs_ws_bytes = 0;
 };
 
 int hdd::ctx_device(const hdd_ctx* ctx) { return ctx ? ctx->device : 0; }
@@ -88,6 +90,7 @@ extern "C" void hdd_ctx_destroy(hdd_ctx* ctx)
   if (ctx && ctx->ws) (void)hipFree(ctx->ws);
   if (ctx && ctx->q3g_tab) (void)hipFree(ctx->q3g_tab);
   if (ctx && ctx->scan_ws) (void)hipFree(ctx->scan_ws);
+  if (ctx && ctx->rhs_ws) (void)hipFree(ctx->rhs_ws);
   if (ctx && ctx->ops_d) (void)hipFree(ctx->ops_d);
   if (ctx && ctx->ops_h) (void)hipHostFree(ctx->ops_h);
   if (ctx && ctx->ops_evt) (void)hipEventDestroy(ctx->ops_evt);
@@ -831,6 +834,26 @@ extern "C" int hdd_swipdg_rhs(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_
   }
   hipError_t e = hipSetDevice(ctx->device);
   if (e != hipSuccess) return hip_fail(e, "hdd_swipdg_rhs: hipSetDevice");
+  const int64_t n_own = m->own_end - m->own_begin;
+  // split path (HDD_DEBUG_FLAGS bit 65536: the fused kernel, A/B): the list is kept in the context, allocated
+  // (and its counters zeroed) on the first call of a size class -- warm up before hipGraph capture
+  if (m->elem_type != HDD_HEX && (dirichlet || neumann) && n_own > 0 && n_own < (int64_t(1) << 31) &&
+      !(ctx->debug_flags & 65536)) {
+    const size_t bytes = hdd::dev::rhs_list_bytes(n_own);
+    if (bytes > ctx->rhs_ws_bytes) {
+      if (ctx->rhs_ws) {
+        if ((e = hipDeviceSynchronize()) != hipSuccess) return hip_fail(e, "hdd_swipdg_rhs: list sync");
+        (void)hipFree(ctx->rhs_ws);
+      }
+      ctx->rhs_ws = nullptr;
+      ctx->rhs_ws_bytes = 0;
+      if ((e = hipMalloc(&ctx->rhs_ws, bytes + bytes / 4)) != hipSuccess) return hip_fail(e, "hdd_swipdg_rhs: list");
+      if ((e = hipMemset(ctx->rhs_ws, 0, hdd::dev::RHS_LIST_OFS * sizeof(uint32_t))) != hipSuccess)
+        return hip_fail(e, "hdd_swipdg_rhs: list counters");
+      ctx->rhs_ws_bytes = bytes + bytes / 4;
+    }
+    a.bnd_list = static_cast<uint32_t*>(ctx->rhs_ws);
+  }
   e = launch_rhs(a, static_cast<hipStream_t>(stream));
   return e == hipSuccess ? HDD_OK : hip_fail(e, "hdd_swipdg_rhs: launch");
 }

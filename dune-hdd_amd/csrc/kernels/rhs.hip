@@ -234,13 +234,89 @@ __device__ __forceinline__ void rhs2d_shape(double x, double y, double* v, doubl
   }
 }
 
+// Dirichlet / Neumann faces of element e, added to acc in face order (the same rounding wherever it runs)
+template <bool TRI>
+__device__ __forceinline__ void rhs2d_faces(const RhsArgs& a, int64_t e, double x0, double y0, double j00, double j10,
+                                            double j01, double j11, double det, double* acc)
+{
+  constexpr int NB = TRI ? 3 : 4, NF = TRI ? 3 : 4;
+  const int64_t n = a.n_local;
+  double v[NB], gx[NB], gy[NB], xq[2];
+  const double i00 = j11 / det, i01 = -j01 / det, i10 = -j10 / det, i11 = j00 / det;
+#pragma unroll
+  for (int f = 0; f < NF; ++f) {
+    const int32_t nbr = a.nbrs[f * n + e];
+    const bool dir = nbr == HDD_NBR_DIRICHLET && a.has_dirichlet;
+    const bool neu = nbr == HDD_NBR_NEUMANN && a.has_neumann;
+    if (!dir && !neu) continue;
+    double r0[2] = {0, 0}, t1[2] = {0, 0}, nr[2] = {0, 0};
+    if constexpr (TRI) {
+      const double P[3][2] = {{0, 0}, {1, 0}, {0, 1}};
+      const int fv[3][2] = {{0, 1}, {0, 2}, {1, 2}};
+      const double N[3][2] = {{0, -1}, {-1, 0}, {1, 1}};
+      for (int c = 0; c < 2; ++c) {
+        r0[c] = P[fv[f][0]][c];
+        t1[c] = P[fv[f][1]][c] - P[fv[f][0]][c];
+        nr[c] = N[f][c];
+      }
+    } else {
+      const int af = f >> 1, sd = f & 1;
+      r0[af] = sd;
+      nr[af] = sd ? 1.0 : -1.0;
+      t1[1 - af] = 1.0;
+    }
+    double nvx = i00 * nr[0] + i10 * nr[1], nvy = i01 * nr[0] + i11 * nr[1];
+    const double nn = sqrt(nvx * nvx + nvy * nvy);
+    nvx /= nn;
+    nvy /= nn;
+    const double dx = j00 * t1[0] + j01 * t1[1], dy = j10 * t1[0] + j11 * t1[1];
+    const double fvol = sqrt(dx * dx + dy * dy);
+    const double* qs = dir ? &a.qd[0][0] : &a.qn[0][0];
+    const int nq = dir ? a.nqd : a.nqn;
+    double cr0 = 0.0, cr1 = 0.0, gamma = 0.0, hpow = 1.0;
+    if (dir) {
+      double A00, A01, A11;
+      if (a.tkind == HDD_TENSOR_ISO_PER_ELEM) {
+        A00 = A11 = a.tper[e];
+        A01 = 0.0;
+      } else if (a.tkind == HDD_TENSOR_SYM_PER_ELEM) {
+        A00 = a.tper[e]; A01 = a.tper[n + e]; A11 = a.tper[2 * n + e];
+      } else {
+        A00 = a.tc[0]; A01 = a.tc[1]; A11 = a.tc[2];
+      }
+      const double Anx = A00 * nvx + A01 * nvy, Any = A01 * nvx + A11 * nvy;
+      gamma = nvx * Anx + nvy * Any;
+      cr0 = i00 * Anx + i01 * Any;   // (A grad phi_i) . n = (J^{-1} A n) . grad_ref phi_i
+      cr1 = i10 * Anx + i11 * Any;
+      hpow = a.beta == 1.0 ? fvol : pow(fvol, a.beta);   // 2d: beta = 1/(d-1) = 1 (pow(x, 1) = x exactly)
+    }
+    for (int q = 0; q < nq; ++q) {
+      const double s0 = qs[3 * q], w = qs[3 * q + 2];
+      const double xh = r0[0] + s0 * t1[0], yh = r0[1] + s0 * t1[1];
+      xq[0] = x0 + j00 * xh + j01 * yh;
+      xq[1] = y0 + j10 * xh + j11 * yh;
+      rhs2d_shape<TRI>(xh, yh, v, gx, gy);
+      const double gv = w * fvol * rhs_fn(dir ? a.dirichlet : a.neumann, e, xq, 2);
+      if (dir) {
+        const double kap = rhs_fn(a.kappa, e, xq, 2);
+        const double pen = a.sigma_boundary * kap * gamma / hpow;
+#pragma unroll
+        for (int i = 0; i < NB; ++i) acc[i] += gv * (-kap * (cr0 * gx[i] + cr1 * gy[i]) + pen * v[i]);
+      } else {
+#pragma unroll
+        for (int i = 0; i < NB; ++i) acc[i] += gv * v[i];
+      }
+    }
+  }
+}
+
 // Thread per element (VALU-bound: the force's cos products at the quadrature points).  VX: the vertex-indexed
 // geometry (vertex ids + 16-byte vertex rows) instead of the element-major coordinates -- neutral here (same
 // box 0.1345 ms both), kept so that one mesh serves every kernel.  (Staging the chunk's values in LDS for
 // 16-byte stores was slower: 0.102 -> 0.135 ms.)
 // NQ > 0: the force's volume rule has NQ points (unrolled: the points' trig evaluations are independent and
 // interleave); FK: the force kind at compile time (-1: any, by a run-time switch)
-template <bool TRI, bool VX, int NQ = 0, int FK = -1>
+template <bool TRI, bool VX, int NQ = 0, int FK = -1, bool SPLIT = false>
 __global__ __launch_bounds__(256) void rhs2d_kernel(RhsArgs a)
 {
   constexpr int NB = TRI ? 3 : 4, NF = TRI ? 3 : 4;
@@ -305,75 +381,72 @@ __global__ __launch_bounds__(256) void rhs2d_kernel(RhsArgs a)
       }
     }
     if (a.has_dirichlet || a.has_neumann) {
-      const double i00 = j11 / det, i01 = -j01 / det, i10 = -j10 / det, i11 = j00 / det;
+      if constexpr (SPLIT) {
+        // boundary elements (~0.4 % at C2) go to rhs2d_face_kernel: the face code's registers (203 VGPRs
+        // fused, 2 waves per SIMD) stay out of this kernel (63 VGPRs, 7 waves per SIMD)
+        bool bnd = false;
 #pragma unroll
-      for (int f = 0; f < NF; ++f) {
-        const int32_t nbr = a.nbrs[f * n + e];
-        const bool dir = nbr == HDD_NBR_DIRICHLET && a.has_dirichlet;
-        const bool neu = nbr == HDD_NBR_NEUMANN && a.has_neumann;
-        if (!dir && !neu) continue;
-        double r0[2] = {0, 0}, t1[2] = {0, 0}, nr[2] = {0, 0};
-        if constexpr (TRI) {
-          const double P[3][2] = {{0, 0}, {1, 0}, {0, 1}};
-          const int fv[3][2] = {{0, 1}, {0, 2}, {1, 2}};
-          const double N[3][2] = {{0, -1}, {-1, 0}, {1, 1}};
-          for (int c = 0; c < 2; ++c) {
-            r0[c] = P[fv[f][0]][c];
-            t1[c] = P[fv[f][1]][c] - P[fv[f][0]][c];
-            nr[c] = N[f][c];
-          }
-        } else {
-          const int af = f >> 1, sd = f & 1;
-          r0[af] = sd;
-          nr[af] = sd ? 1.0 : -1.0;
-          t1[1 - af] = 1.0;
+        for (int f = 0; f < NF; ++f) {
+          const int32_t nbr = a.nbrs[f * n + e];
+          bnd |= (nbr == HDD_NBR_DIRICHLET && a.has_dirichlet) || (nbr == HDD_NBR_NEUMANN && a.has_neumann);
         }
-        double nvx = i00 * nr[0] + i10 * nr[1], nvy = i01 * nr[0] + i11 * nr[1];
-        const double nn = sqrt(nvx * nvx + nvy * nvy);
-        nvx /= nn;
-        nvy /= nn;
-        const double dx = j00 * t1[0] + j01 * t1[1], dy = j10 * t1[0] + j11 * t1[1];
-        const double fvol = sqrt(dx * dx + dy * dy);
-        const double* qs = dir ? &a.qd[0][0] : &a.qn[0][0];
-        const int nq = dir ? a.nqd : a.nqn;
-        double cr0 = 0.0, cr1 = 0.0, gamma = 0.0, hpow = 1.0;
-        if (dir) {
-          double A00, A01, A11;
-          if (a.tkind == HDD_TENSOR_ISO_PER_ELEM) {
-            A00 = A11 = a.tper[e];
-            A01 = 0.0;
-          } else if (a.tkind == HDD_TENSOR_SYM_PER_ELEM) {
-            A00 = a.tper[e]; A01 = a.tper[n + e]; A11 = a.tper[2 * n + e];
-          } else {
-            A00 = a.tc[0]; A01 = a.tc[1]; A11 = a.tc[2];
-          }
-          const double Anx = A00 * nvx + A01 * nvy, Any = A01 * nvx + A11 * nvy;
-          gamma = nvx * Anx + nvy * Any;
-          cr0 = i00 * Anx + i01 * Any;   // (A grad phi_i) . n = (J^{-1} A n) . grad_ref phi_i
-          cr1 = i10 * Anx + i11 * Any;
-          hpow = pow(fvol, a.beta);
+        const uint64_t m = __ballot(bnd);
+        if (m) {   // one atomic per wave
+          const int lead = __ffsll((unsigned long long)m) - 1;
+          uint32_t base = 0;
+          if (int(__lane_id()) == lead) base = atomicAdd(a.bnd_list, uint32_t(__popcll(m)));
+          base = __shfl(base, lead);
+          if (bnd) a.bnd_list[RHS_LIST_OFS + base + __popcll(m & ((1ull << __lane_id()) - 1))] = uint32_t(k);
         }
-        for (int q = 0; q < nq; ++q) {
-          const double s0 = qs[3 * q], w = qs[3 * q + 2];
-          const double xh = r0[0] + s0 * t1[0], yh = r0[1] + s0 * t1[1];
-          xq[0] = x0 + j00 * xh + j01 * yh;
-          xq[1] = y0 + j10 * xh + j11 * yh;
-          rhs2d_shape<TRI>(xh, yh, v, gx, gy);
-          const double gv = w * fvol * rhs_fn(dir ? a.dirichlet : a.neumann, e, xq, 2);
-          if (dir) {
-            const double kap = rhs_fn(a.kappa, e, xq, 2);
-            const double pen = a.sigma_boundary * kap * gamma / hpow;
-#pragma unroll
-            for (int i = 0; i < NB; ++i) acc[i] += gv * (-kap * (cr0 * gx[i] + cr1 * gy[i]) + pen * v[i]);
-          } else {
-#pragma unroll
-            for (int i = 0; i < NB; ++i) acc[i] += gv * v[i];
-          }
-        }
+      } else {
+        rhs2d_faces<TRI>(a, e, x0, y0, j00, j10, j01, j11, det, acc);
       }
     }
 #pragma unroll
     for (int i = 0; i < NB; ++i) __builtin_nontemporal_store(acc[i], a.out + k * NB + i);
+  }
+}
+
+// the faces of the elements rhs2d_kernel<.., SPLIT> listed, added to their stored volume values in the same
+// order as the fused kernel (bit-identical).  The last workgroup to finish resets the list's counters for the
+// next call (no memset launch per call).
+template <bool TRI, bool VX>
+__global__ __launch_bounds__(256) void rhs2d_face_kernel(RhsArgs a)
+{
+  constexpr int NB = TRI ? 3 : 4;
+  const int64_t n = a.n_local;
+  const uint32_t count = __atomic_load_n(a.bnd_list, __ATOMIC_RELAXED);
+  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < count; t += gridDim.x * blockDim.x) {
+    const int64_t k = a.bnd_list[RHS_LIST_OFS + t];
+    const int64_t e = a.own_begin + k;
+    double x0, y0, x1, y1, x2, y2;
+    if constexpr (VX) {
+      const double2 p0 = reinterpret_cast<const double2*>(a.vxy)[a.ev[e]];
+      const double2 p1 = reinterpret_cast<const double2*>(a.vxy)[a.ev[n + e]];
+      const double2 p2 = reinterpret_cast<const double2*>(a.vxy)[a.ev[2 * n + e]];
+      x0 = p0.x; y0 = p0.y; x1 = p1.x; y1 = p1.y; x2 = p2.x; y2 = p2.y;
+    } else {
+      x0 = a.coords[e]; y0 = a.coords[n + e];
+      x1 = a.coords[2 * n + e]; y1 = a.coords[3 * n + e];
+      x2 = a.coords[4 * n + e]; y2 = a.coords[5 * n + e];
+    }
+    const double j00 = x1 - x0, j10 = y1 - y0, j01 = x2 - x0, j11 = y2 - y0;
+    const double det = j00 * j11 - j01 * j10;
+    double acc[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) acc[i] = a.out[k * NB + i];
+    rhs2d_faces<TRI>(a, e, x0, y0, j00, j10, j01, j11, det, acc);
+#pragma unroll
+    for (int i = 0; i < NB; ++i) a.out[k * NB + i] = acc[i];
+  }
+  __syncthreads();
+  // no fence: a workgroup's count load has returned before its loop ended (the loop bound depends on it), and
+  // the reset is seen by the next call's kernels through the kernel boundary
+  if (threadIdx.x == 0) {
+    if (atomicAdd(a.bnd_list + 1, 1u) == gridDim.x - 1) {   // every workgroup has read the count
+      __atomic_store_n(a.bnd_list, 0u, __ATOMIC_RELAXED);
+      __atomic_store_n(a.bnd_list + 1, 0u, __ATOMIC_RELAXED);
+    }
   }
 }
 
@@ -636,7 +709,36 @@ hipError_t launch_rhs(const RhsArgs& a, hipStream_t s)
   if (a.elem_type != HDD_HEX && n_own > 0) {
     const int64_t blocks = std::min<int64_t>((n_own + 255) / 256, int64_t(a.n_cu) * 8);
     const bool tri = a.elem_type == HDD_SIMPLEX;
-    // the ESV2007-type force (cos products) on the rules of order 4 (Dunavant 6 / Gauss 3 x 3): unrolled
+    // the ESV2007-type force (cos products) on the rules of order 4 (Dunavant 6 / Gauss 3 x 3): unrolled.
+    // split: volume kernel + boundary-element list + face kernel (needs the context's list, see RhsArgs)
+    if (a.bnd_list && (a.has_dirichlet || a.has_neumann)) {
+      const dim3 g(static_cast<unsigned>(blocks)), b(256);
+      if (a.has_force && a.force.kind == HDD_FN_COS_PRODUCT && a.nqv == (tri ? 6 : 9) && !a.generic) {
+        if (tri && a.ev) hipLaunchKernelGGL((rhs2d_kernel<true, true, 6, HDD_FN_COS_PRODUCT, true>), g, b, 0, s, a);
+        else if (tri) hipLaunchKernelGGL((rhs2d_kernel<true, false, 6, HDD_FN_COS_PRODUCT, true>), g, b, 0, s, a);
+        else if (a.ev) hipLaunchKernelGGL((rhs2d_kernel<false, true, 9, HDD_FN_COS_PRODUCT, true>), g, b, 0, s, a);
+        else hipLaunchKernelGGL((rhs2d_kernel<false, false, 9, HDD_FN_COS_PRODUCT, true>), g, b, 0, s, a);
+      } else if (a.ev) {
+        if (tri) hipLaunchKernelGGL((rhs2d_kernel<true, true, 0, -1, true>), g, b, 0, s, a);
+        else hipLaunchKernelGGL((rhs2d_kernel<false, true, 0, -1, true>), g, b, 0, s, a);
+      } else {
+        if (tri) hipLaunchKernelGGL((rhs2d_kernel<true, false, 0, -1, true>), g, b, 0, s, a);
+        else hipLaunchKernelGGL((rhs2d_kernel<false, false, 0, -1, true>), g, b, 0, s, a);
+      }
+      hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return e;
+      // a quarter of the CUs (16 K threads: one list entry per thread at C2's 7,680 boundary elements); every
+      // workgroup, busy or not, pays the finish atomic
+      const dim3 gf(unsigned(std::max(1, a.n_cu / 4)));
+      if (a.ev) {
+        if (tri) hipLaunchKernelGGL((rhs2d_face_kernel<true, true>), gf, b, 0, s, a);
+        else hipLaunchKernelGGL((rhs2d_face_kernel<false, true>), gf, b, 0, s, a);
+      } else {
+        if (tri) hipLaunchKernelGGL((rhs2d_face_kernel<true, false>), gf, b, 0, s, a);
+        else hipLaunchKernelGGL((rhs2d_face_kernel<false, false>), gf, b, 0, s, a);
+      }
+      return hipGetLastError();
+    }
     if (a.has_force && a.force.kind == HDD_FN_COS_PRODUCT && a.nqv == (tri ? 6 : 9) && !a.generic) {
       if (tri && a.ev) hipLaunchKernelGGL((rhs2d_kernel<true, true, 6, HDD_FN_COS_PRODUCT>), dim3(unsigned(blocks)), dim3(256), 0, s, a);
       else if (tri) hipLaunchKernelGGL((rhs2d_kernel<true, false, 6, HDD_FN_COS_PRODUCT>), dim3(unsigned(blocks)), dim3(256), 0, s, a);

@@ -134,3 +134,40 @@ def test_rhs_vertex_indexed_equals_element_major(case):
                          neumann=H.scalar_fn(H.FN_CONST, 0.7)))
     torch.cuda.synchronize()
     assert torch.equal(out[0], out[1])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("et", [H.SIMPLEX, H.CUBE])
+def test_rhs_split_equals_fused(et):
+    """The split 2d path (volume kernel + boundary-element list + face kernel) equals the fused one-kernel path
+    (HDD_DEBUG_FLAGS bit 65536) bit for bit, on meshes from all-boundary (3 x 2) to ragged multi-chunk ones, with
+    Dirichlet + Neumann faces, repeated calls (the list's counters reset by the face kernel) and a growing list."""
+    import os
+    import torch
+    ctxs = []
+    old = os.environ.get("HDD_DEBUG_FLAGS")
+    for flags in ("0", "65536"):
+        os.environ["HDD_DEBUG_FLAGS"] = flags
+        ctxs.append(H.Context(0))
+    if old is None:
+        del os.environ["HDD_DEBUG_FLAGS"]
+    else:
+        os.environ["HDD_DEBUG_FLAGS"] = old
+    rng = np.random.default_rng(11)
+    for n in [(3, 2), (61, 23), (200, 37)]:
+        grid = H.Grid.structured(et, *n, (0, 0), (2, 1))
+        loc = grid.local()
+        bnd = loc.neighbors[0] == H.NBR_DIRICHLET
+        loc.neighbors[0][bnd] = H.NBR_NEUMANN
+        ten = H.tensor_fn(H.TENSOR_ISO_PER_ELEM, per_elem=torch.from_numpy(rng.uniform(0.5, 2.0, loc.n_local)).cuda())
+        dm = H.DeviceMesh(loc)
+        kw = dict(force=H.esv2007_force(), kappa=H.scalar_fn(H.FN_CONST, 1.3), tensor=ten,
+                  dirichlet=H.scalar_fn(H.FN_SINUSOID, 0.5, 1.0, 2.0, 1.0, order=3), neumann=H.scalar_fn(H.FN_CONST, 0.7))
+        fused = H.rhs(ctxs[1], dm, **kw)
+        for _ in range(3):
+            split = H.rhs(ctxs[0], dm, **kw)
+            torch.cuda.synchronize()
+            assert torch.equal(split, fused), n
+        # generic (run-time rule) variant of the split path: per-element force
+        kw.update(force=H.scalar_fn(H.FN_PER_ELEM, per_elem=torch.from_numpy(rng.uniform(-1, 1, loc.n_local)).cuda()))
+        assert torch.equal(H.rhs(ctxs[0], dm, **kw), H.rhs(ctxs[1], dm, **kw)), n
