@@ -818,6 +818,7 @@ extern "C" int hdd_swipdg_rhs(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_
   a.out = d_rhs;
   a.n_cu = ctx->n_cu;
   a.generic = (ctx->debug_flags & 32768) ? 1 : 0;
+  a.no_tiny = (ctx->debug_flags & 131072) ? 1 : 0;
   if (force) {
     const int order = fn_order(*force) + deg;
     a.nqv = m->elem_type == HDD_SIMPLEX ? simplex_rule(order, a.qv, 64) : tensor_rule(dim, order, a.qv, 64);

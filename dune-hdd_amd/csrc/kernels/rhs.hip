@@ -345,10 +345,12 @@ __global__ __launch_bounds__(256) void rhs2d_kernel(RhsArgs a)
     // cos products on elements small against the wavelength (wave-uniform): one sincos per direction and
     // element, Taylor offsets per point (trig_phase.hh)
     [[maybe_unused]] double sx0 = 0.0, cx0 = 0.0, sy0 = 0.0, cy0 = 0.0;
-    [[maybe_unused]] bool near = false;
+    [[maybe_unused]] bool near = false, tiny = false;
     if constexpr (FK == HDD_FN_COS_PRODUCT && NQ > 0) {
       const double kx = a.force.kx, ky = a.force.ky;
-      near = __all(fabs(kx * j00) + fabs(kx * j01) <= SMALL_PHASE && fabs(ky * j10) + fabs(ky * j11) <= SMALL_PHASE);
+      const double dm = fmax(fabs(kx * j00) + fabs(kx * j01), fabs(ky * j10) + fabs(ky * j11));
+      near = __all(dm <= SMALL_PHASE);
+      tiny = __all(dm <= TINY_PHASE) && !a.no_tiny;
       if (near) {
         sincos_phase(kx * x0, sx0, cx0);
         sincos_phase(ky * y0, sy0, cy0);
@@ -361,7 +363,10 @@ __global__ __launch_bounds__(256) void rhs2d_kernel(RhsArgs a)
       rhs2d_shape<TRI>(xh, yh, v, gx, gy);
       double f;
       if constexpr (FK == HDD_FN_COS_PRODUCT) {
-        if (near)
+        if (tiny)
+          f = a.force.c * cos_tiny(sx0, cx0, a.force.kx * (j00 * xh + j01 * yh)) *
+              cos_tiny(sy0, cy0, a.force.ky * (j10 * xh + j11 * yh));
+        else if (near)
           f = a.force.c * cos_near(sx0, cx0, a.force.kx * (j00 * xh + j01 * yh)) *
               cos_near(sy0, cy0, a.force.ky * (j10 * xh + j11 * yh));
         else

@@ -115,7 +115,8 @@ struct RhsArgs {
   int32_t has_force, has_dirichlet, has_neumann, pad;
   double sigma_boundary, beta;
   int32_t nqv, nqd, nqn, n_cu;
-  int32_t generic, pad_g;   // 1: the run-time-rule kernel only (HDD_DEBUG_FLAGS bit 32768: A/B of the unrolled path)
+  int32_t generic;   // 1: the run-time-rule kernel only (HDD_DEBUG_FLAGS bit 32768: A/B of the unrolled path)
+  int32_t no_tiny;   // 1: no TINY_PHASE tier for the force's cos products (HDD_DEBUG_FLAGS bit 131072: A/B)
   double qv[64][4];    // volume rule: reference point (3) + weight
   double qd[16][3];    // Dirichlet face rule: face parameters (2) + weight
   double qn[16][3];    // Neumann face rule

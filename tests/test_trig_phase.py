@@ -101,3 +101,52 @@ def test_sincos_phase_and_small_offsets(tmp_path):
     cref = np.cos(phi) * np.cos(d) - np.sin(phi) * np.sin(d)
     assert np.max(np.abs(v[:, 2] - sref)) <= 9e-16
     assert np.max(np.abs(v[:, 3] - cref)) <= 9e-16
+
+
+DRIVER_TINY = r"""
+#include <cstdio>
+#include <cstdlib>
+#include "trig_phase.hh"
+int main(int argc, char** argv) {
+  FILE* f = std::fopen(argv[1], "rb");
+  long n = std::atol(argv[2]);
+  double* x = (double*)std::malloc(2 * n * sizeof(double));
+  if (std::fread(x, sizeof(double), 2 * n, f) != (size_t)(2 * n)) return 2;
+  std::fclose(f);
+  for (long i = 0; i < n; ++i) {
+    double s0, c0;
+    hdd::dev::sincos_phase(x[2 * i], s0, c0);
+    const double d = x[2 * i + 1];
+    double v[4] = {hdd::dev::sin_tiny(s0, c0, d), hdd::dev::cos_tiny(s0, c0, d), hdd::dev::sin_near(s0, c0, d),
+                   hdd::dev::cos_near(s0, c0, d)};
+    std::fwrite(v, sizeof(double), 4, stdout);
+  }
+  return 0;
+}
+"""
+
+
+def test_tiny_offsets(tmp_path):
+    """sin / cos of phi0 + d by the short Taylor offsets (|d| <= TINY_PHASE = 1/64, the RHS kernel's tier for
+    fine meshes) within an ulp of the SMALL_PHASE polynomials and within ~2 ulp of libm's addition formula."""
+    src = tmp_path / "drv.cpp"
+    src.write_text(DRIVER_TINY)
+    exe = tmp_path / "drv"
+    subprocess.check_call(["g++", "-O2", "-ffp-contract=off", "-D__host__=", "-D__device__=",
+                           "-D__forceinline__=inline", "-I" + HDR, str(src), "-o", str(exe)])
+    rng = np.random.default_rng(5)
+    n = 200000
+    phi = np.concatenate([rng.uniform(-6 * np.pi, 6 * np.pi, n - 129), np.arange(-64, 65) * (np.pi / 4)])
+    d = rng.uniform(-1.0 / 64, 1.0 / 64, n)
+    d[:1000] = 0.0
+    d[1000:1010] = [1.0 / 64, -1.0 / 64] * 5
+    inp = tmp_path / "x.bin"
+    np.stack([phi, d], 1).tofile(inp)
+    v = np.frombuffer(subprocess.run([str(exe), str(inp), str(n)], check=True, capture_output=True).stdout,
+                      np.float64).reshape(-1, 4)
+    assert np.max(np.abs(v[:, 0] - v[:, 2])) <= 2.3e-16
+    assert np.max(np.abs(v[:, 1] - v[:, 3])) <= 2.3e-16
+    sref = np.sin(phi) * np.cos(d) + np.cos(phi) * np.sin(d)
+    cref = np.cos(phi) * np.cos(d) - np.sin(phi) * np.sin(d)
+    assert np.max(np.abs(v[:, 0] - sref)) <= 9e-16
+    assert np.max(np.abs(v[:, 1] - cref)) <= 9e-16
