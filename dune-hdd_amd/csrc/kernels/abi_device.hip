@@ -34,6 +34,8 @@ struct hdd_ctx {
   void* ops_h = nullptr;       //   its pinned host staging copy (reused once the last upload has completed)
   size_t ops_bytes = 0;
   hipEvent_t ops_evt = nullptr;
+  int64_t* nnz_h = nullptr;    // mapped pinned host word: the device pattern's nnz, written by the elem_ptr kernel
+  int64_t* nnz_hd = nullptr;   //   (its device address)
   void* rhs_ws = nullptr;      // 2d RHS boundary-element list (counters zero between calls)
   size_t rhs_ws_bytes = 0;
 };
@@ -91,6 +93,7 @@ extern "C" void hdd_ctx_destroy(hdd_ctx* ctx)
   if (ctx && ctx->q3g_tab) (void)hipFree(ctx->q3g_tab);
   if (ctx && ctx->scan_ws) (void)hipFree(ctx->scan_ws);
   if (ctx && ctx->rhs_ws) (void)hipFree(ctx->rhs_ws);
+  if (ctx && ctx->nnz_h) (void)hipHostFree(ctx->nnz_h);
   if (ctx && ctx->ops_d) (void)hipFree(ctx->ops_d);
   if (ctx && ctx->ops_h) (void)hipHostFree(ctx->ops_h);
   if (ctx && ctx->ops_evt) (void)hipEventDestroy(ctx->ops_evt);
@@ -662,12 +665,27 @@ extern "C" int hdd_pattern_elem_ptr_device(hdd_ctx* ctx, const hdd_mesh* m, int3
     if (e != hipSuccess) return hip_fail(e, "hdd_pattern_elem_ptr_device: scan scratch");
     ctx->scan_ws_bytes = tmp_bytes;
   }
+  // nnz reaches the host through a mapped pinned word the elem_ptr kernel writes (no copy launch);
+  // HDD_DEBUG_FLAGS bit 262144: the round-3 scheme (scan launch + device-to-host copy), A/B
+  const bool legacy = (ctx->debug_flags & 262144) != 0;
+  if (!legacy && !ctx->nnz_h && n_own > 0) {
+    if ((e = hipHostMalloc(reinterpret_cast<void**>(&ctx->nnz_h), sizeof(int64_t), hipHostMallocMapped)) != hipSuccess)
+      return hip_fail(e, "hdd_pattern_elem_ptr_device: pinned nnz");
+    if ((e = hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->nnz_hd), ctx->nnz_h, 0)) != hipSuccess) {
+      (void)hipHostFree(ctx->nnz_h);
+      ctx->nnz_h = nullptr;
+      return hip_fail(e, "hdd_pattern_elem_ptr_device: pinned nnz device address");
+    }
+  }
+  const bool mapped = !legacy && n_own > 0;
   e = hdd::dev::launch_pattern_elem_ptr(m->neighbors, nf, m->n_local, m->own_begin, m->own_end, int64_t(nb) * nb,
-                                        d_elem_ptr, static_cast<int64_t*>(ctx->scan_ws), s);
+                                        d_elem_ptr, static_cast<int64_t*>(ctx->scan_ws), s,
+                                        mapped ? ctx->nnz_hd : nullptr, legacy);
   if (e != hipSuccess) return hip_fail(e, "hdd_pattern_elem_ptr_device: elem_ptr");
-  e = hipMemcpyAsync(nnz, d_elem_ptr + n_own, sizeof(int64_t), hipMemcpyDeviceToHost, s);
+  if (!mapped) e = hipMemcpyAsync(nnz, d_elem_ptr + n_own, sizeof(int64_t), hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) return hip_fail(e, "hdd_pattern_elem_ptr_device: read nnz");
+  if (mapped) *nnz = *static_cast<volatile int64_t*>(ctx->nnz_h);
   return HDD_OK;
 }
 

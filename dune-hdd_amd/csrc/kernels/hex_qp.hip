@@ -1325,14 +1325,36 @@ __global__ void __launch_bounds__(PE_THREADS) pattern_sums_scan_kernel(int64_t* 
   }
 }
 
+// BASE_SUM: the block's offset is the sum of the preceding blocks' totals, read by every block (L2-resident:
+// 4,000 totals at C2, <= 16 loads per thread) -- no scan launch between the two passes; else offs[] holds the
+// scanned offsets.  host_nnz (optional, a mapped pinned host word): the total, written by the last element's
+// thread, so the caller reads nnz after a stream synchronisation without a copy launch.
+template <bool BASE_SUM>
 __global__ void __launch_bounds__(PE_THREADS) pattern_elem_ptr_kernel(const int32_t* __restrict__ nbrs, int32_t nf,
                                                                       int64_t n_local, int64_t own_begin,
                                                                       int64_t n_own, int64_t nb2,
                                                                       const int64_t* __restrict__ offs,
-                                                                      int64_t* __restrict__ elem_ptr)
+                                                                      int64_t* __restrict__ elem_ptr,
+                                                                      int64_t* __restrict__ host_nnz)
 {
   __shared__ int64_t sh[PE_THREADS / 64];
   __shared__ int64_t cnt[PE_BLOCK];
+  int64_t base = 0;
+  if constexpr (BASE_SUM) {
+    int64_t part[4] = {0, 0, 0, 0};
+    const int nb = int(blockIdx.x);
+    int i = int(threadIdx.x);
+    for (; i + 3 * PE_THREADS < nb; i += 4 * PE_THREADS) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) part[u] += offs[i + u * PE_THREADS];
+    }
+    for (; i < nb; i += PE_THREADS) part[0] += offs[i];
+    int64_t tot;
+    (void)pe_block_scan((part[0] + part[1]) + (part[2] + part[3]), sh, tot);
+    base = tot;
+  } else {
+    base = offs[blockIdx.x];
+  }
   // counts read coalesced (element b0 + i * PE_THREADS), transposed through LDS so that each thread scans
   // PE_PER consecutive elements, prefixes written back coalesced
   const int64_t blk0 = int64_t(blockIdx.x) * PE_BLOCK;
@@ -1350,7 +1372,7 @@ __global__ void __launch_bounds__(PE_THREADS) pattern_elem_ptr_kernel(const int3
     s += c[i];
   }
   int64_t total;
-  int64_t p = offs[blockIdx.x] + pe_block_scan(s, sh, total);   // (its barriers order the cnt reads above)
+  int64_t p = base + pe_block_scan(s, sh, total);   // (its barriers order the cnt reads above)
 #pragma unroll
   for (int i = 0; i < PE_PER; ++i) {
     p += c[i];
@@ -1361,6 +1383,7 @@ __global__ void __launch_bounds__(PE_THREADS) pattern_elem_ptr_kernel(const int3
   for (int i = 0; i < PE_PER; ++i) {
     const int64_t k = blk0 + t + i * PE_THREADS;
     if (k < n_own) elem_ptr[k + 1] = cnt[t + i * PE_THREADS];
+    if (host_nnz && k == n_own - 1) *host_nnz = cnt[t + i * PE_THREADS];
   }
   if (blockIdx.x == 0 && t == 0) elem_ptr[0] = 0;
 }
@@ -1368,16 +1391,23 @@ __global__ void __launch_bounds__(PE_THREADS) pattern_elem_ptr_kernel(const int3
 int64_t pattern_elem_ptr_scratch(int64_t n_own) { return (n_own + PE_BLOCK - 1) / PE_BLOCK; }
 
 hipError_t launch_pattern_elem_ptr(const int32_t* nbrs, int32_t nf, int64_t n_local, int64_t own_begin,
-                                   int64_t own_end, int64_t nb2, int64_t* d_elem_ptr, int64_t* d_scratch, hipStream_t s)
+                                   int64_t own_end, int64_t nb2, int64_t* d_elem_ptr, int64_t* d_scratch, hipStream_t s,
+                                   int64_t* host_nnz, bool scan_launch)
 {
   const int64_t n_own = own_end - own_begin;
   if (n_own <= 0) return hipMemsetAsync(d_elem_ptr, 0, sizeof(int64_t), s);
   const int64_t nblk = pattern_elem_ptr_scratch(n_own);
   hipLaunchKernelGGL(pattern_block_sums_kernel, dim3(unsigned(nblk)), dim3(PE_THREADS), 0, s, nbrs, nf, n_local,
                      own_begin, n_own, nb2, d_scratch);
-  hipLaunchKernelGGL(pattern_sums_scan_kernel, dim3(1), dim3(PE_THREADS), 0, s, d_scratch, nblk);
-  hipLaunchKernelGGL(pattern_elem_ptr_kernel, dim3(unsigned(nblk)), dim3(PE_THREADS), 0, s, nbrs, nf, n_local,
-                     own_begin, n_own, nb2, d_scratch, d_elem_ptr);
+  // the offsets summed per block up to 64 K blocks (67 M elements: <= 256 L2 loads per thread), else scanned
+  if (scan_launch || nblk > 65536) {
+    hipLaunchKernelGGL(pattern_sums_scan_kernel, dim3(1), dim3(PE_THREADS), 0, s, d_scratch, nblk);
+    hipLaunchKernelGGL(pattern_elem_ptr_kernel<false>, dim3(unsigned(nblk)), dim3(PE_THREADS), 0, s, nbrs, nf,
+                       n_local, own_begin, n_own, nb2, d_scratch, d_elem_ptr, host_nnz);
+  } else {
+    hipLaunchKernelGGL(pattern_elem_ptr_kernel<true>, dim3(unsigned(nblk)), dim3(PE_THREADS), 0, s, nbrs, nf,
+                       n_local, own_begin, n_own, nb2, d_scratch, d_elem_ptr, host_nnz);
+  }
   return hipGetLastError();
 }
 

@@ -94,11 +94,13 @@ hipError_t launch_hex(const HexArgs& a, int degree, int nq1v, int nq1f, hipStrea
 // device pattern (any element type): blocks per element = 1 + interior faces
 hipError_t launch_pattern_counts(const int32_t* nbrs, int32_t nf, int64_t n_local, int64_t own_begin, int64_t own_end,
                                  int64_t nb2, int64_t* d_counts, hipStream_t s);
-// elem_ptr [n_own + 1] (exclusive prefix of the row-block sizes) in three launches; d_scratch holds
-// pattern_elem_ptr_scratch(n_own) int64
+// elem_ptr [n_own + 1] (exclusive prefix of the row-block sizes) in two launches (three with scan_launch or
+// beyond 64 K blocks); d_scratch holds pattern_elem_ptr_scratch(n_own) int64; host_nnz (optional): a device
+// pointer to mapped pinned host memory receiving elem_ptr[n_own]
 int64_t pattern_elem_ptr_scratch(int64_t n_own);
 hipError_t launch_pattern_elem_ptr(const int32_t* nbrs, int32_t nf, int64_t n_local, int64_t own_begin,
-                                   int64_t own_end, int64_t nb2, int64_t* d_elem_ptr, int64_t* d_scratch, hipStream_t s);
+                                   int64_t own_end, int64_t nb2, int64_t* d_elem_ptr, int64_t* d_scratch, hipStream_t s,
+                                   int64_t* host_nnz = nullptr, bool scan_launch = false);
 hipError_t launch_pattern_fill(const int32_t* nbrs, int32_t nf, int32_t nb, int64_t n_local, int64_t own_begin,
                                int64_t own_end, const int64_t* gid, const int64_t* elem_ptr, int64_t* row_ptr,
                                int32_t* col, int n_cu, hipStream_t s);

@@ -206,3 +206,28 @@ def test_device_pattern_uniform_tiles_equal_host(ctx, et, px):
         assert np.array_equal(dpat.row_ptr.cpu().numpy(), host[0])
         assert np.array_equal(dpat.col.cpu().numpy(), host[1])
         assert np.array_equal(dpat.elem_ptr.cpu().numpy(), host[2])
+
+
+@pytest.mark.parametrize("et", [H.SIMPLEX, H.CUBE])
+def test_device_elem_ptr_block_sums_equal_scan(et):
+    """elem_ptr with per-block offset sums (no scan launch, > 768 blocks: the unrolled loads) and nnz through the
+    mapped host word equal the scan-launch + copy scheme (HDD_DEBUG_FLAGS bit 262144), pattern included."""
+    import os
+    torch = _torch()
+    ctxs = []
+    old = os.environ.get("HDD_DEBUG_FLAGS")
+    for flags in ("0", "262144"):
+        os.environ["HDD_DEBUG_FLAGS"] = flags
+        ctxs.append(H.Context(0))
+    if old is None:
+        del os.environ["HDD_DEBUG_FLAGS"]
+    else:
+        os.environ["HDD_DEBUG_FLAGS"] = old
+    g = H.Grid.structured(et, 1000 if et == H.SIMPLEX else 1800, 500, px=2, py=1)
+    loc = g.local()
+    assert loc.n_own > 768 * 1024
+    pats = [H.DevicePattern(loc, ctx=c, on_device=True) for c in ctxs]
+    torch.cuda.synchronize()
+    assert pats[0].nnz == pats[1].nnz == int(pats[1].elem_ptr[-1].item())
+    for name in ("elem_ptr", "row_ptr", "col"):
+        assert torch.equal(getattr(pats[0], name), getattr(pats[1], name)), name
