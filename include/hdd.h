@@ -268,7 +268,8 @@ typedef struct {
 
 /* Device pattern build (the pattern of a p=3 3d mesh is ~4 bytes x 28672 per
  * element, too large to build on the host).  Step 1 writes d_elem_ptr [n_own+1] and returns the total
- * nnz in *nnz (host; synchronises `stream`).  Step 2 writes d_row_ptr [nb*n_own+1] and d_col [nnz];
+ * nnz in *nnz (host; synchronises `stream`; the kernel writes nnz into a mapped pinned word the context
+ * allocates on its first call, so one stream at a time per context).  Step 2 writes d_row_ptr [nb*n_own+1] and d_col [nnz];
  * d_global_id [n_local] maps local to global element ids (NULL: local == global). */
 int hdd_pattern_elem_ptr_device(hdd_ctx* ctx, const hdd_mesh* mesh, int32_t nb, int64_t* d_elem_ptr,
                                 int64_t* nnz, void* stream);
@@ -304,7 +305,10 @@ int hdd_swipdg_assemble_elements(hdd_ctx* ctx, const hdd_mesh* mesh, const hdd_s
  * Writes d_rhs[k*nb + i] for every owned element k (local order) and basis function i; one call per
  * affine component of the right-hand side (the caller pairs kappa / dirichlet components as swipdg.hh
  * does).  Integration orders: ord(f) + p; Neumann ord(g_N) + p; Dirichlet max(ord(g_D) + p,
- * ord(kappa) + ord(A) + p - 1 + ord(g_D)). */
+ * ord(kappa) + ord(A) + p - 1 + ord(g_D)).  2d meshes with Dirichlet or Neumann data: two launches (volume
+ * kernel, then a face kernel over the boundary elements the first one listed) on a list the context holds
+ * (4 B per owned element, allocated on the first call of a size class: warm a context up before hipGraph
+ * capture; one stream at a time per context). */
 int hdd_swipdg_rhs(hdd_ctx* ctx, const hdd_mesh* mesh, const hdd_scalar_fn* force, const hdd_scalar_fn* kappa,
                    const hdd_tensor_fn* tensor, const hdd_scalar_fn* dirichlet, const hdd_scalar_fn* neumann,
                    const hdd_swipdg_params* params, double* d_rhs, void* stream);
