@@ -325,10 +325,12 @@ __global__ __launch_bounds__(256) void rhs2d_kernel(RhsArgs a)
   for (int64_t k = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; k < n_own; k += int64_t(gridDim.x) * blockDim.x) {
     const int64_t e = a.own_begin + k;
     double x0, y0, x1, y1, x2, y2;
+    [[maybe_unused]] int32_t vi0 = 0, vi1 = 0, vi2 = 0;
     if constexpr (VX) {
-      const double2 p0 = reinterpret_cast<const double2*>(a.vxy)[a.ev[e]];
-      const double2 p1 = reinterpret_cast<const double2*>(a.vxy)[a.ev[n + e]];
-      const double2 p2 = reinterpret_cast<const double2*>(a.vxy)[a.ev[2 * n + e]];
+      vi0 = a.ev[e]; vi1 = a.ev[n + e]; vi2 = a.ev[2 * n + e];
+      const double2 p0 = reinterpret_cast<const double2*>(a.vxy)[vi0];
+      const double2 p1 = reinterpret_cast<const double2*>(a.vxy)[vi1];
+      const double2 p2 = reinterpret_cast<const double2*>(a.vxy)[vi2];
       x0 = p0.x; y0 = p0.y; x1 = p1.x; y1 = p1.y; x2 = p2.x; y2 = p2.y;
     } else {
       x0 = a.coords[e]; y0 = a.coords[n + e];
@@ -401,7 +403,9 @@ __global__ __launch_bounds__(256) void rhs2d_kernel(RhsArgs a)
           uint32_t base = 0;
           if (int(__lane_id()) == lead) base = atomicAdd(a.bnd_list, uint32_t(__popcll(m)));
           base = __shfl(base, lead);
-          if (bnd) a.bnd_list[RHS_LIST_OFS + base + __popcll(m & ((1ull << __lane_id()) - 1))] = uint32_t(k);
+          if (bnd)   // the vertex ids ride along: the face kernel's geometry is one load away from its entry
+            reinterpret_cast<uint4*>(a.bnd_list + RHS_LIST_OFS)[base + __popcll(m & ((1ull << __lane_id()) - 1))] =
+                make_uint4(uint32_t(k), uint32_t(vi0), uint32_t(vi1), uint32_t(vi2));
         }
       } else {
         rhs2d_faces<TRI>(a, e, x0, y0, j00, j10, j01, j11, det, acc);
@@ -420,15 +424,19 @@ __global__ __launch_bounds__(256) void rhs2d_face_kernel(RhsArgs a)
 {
   constexpr int NB = TRI ? 3 : 4;
   const int64_t n = a.n_local;
+  const uint4* list = reinterpret_cast<const uint4*>(a.bnd_list + RHS_LIST_OFS);
+  const uint32_t n_own = uint32_t(a.own_end - a.own_begin), stride = gridDim.x * blockDim.x;
+  uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  uint4 ent = t < n_own ? list[t] : make_uint4(0, 0, 0, 0);   // loaded beside the count (stale beyond it)
   const uint32_t count = __atomic_load_n(a.bnd_list, __ATOMIC_RELAXED);
-  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < count; t += gridDim.x * blockDim.x) {
-    const int64_t k = a.bnd_list[RHS_LIST_OFS + t];
+  for (; t < count; t += stride) {
+    const int64_t k = ent.x;
     const int64_t e = a.own_begin + k;
     double x0, y0, x1, y1, x2, y2;
     if constexpr (VX) {
-      const double2 p0 = reinterpret_cast<const double2*>(a.vxy)[a.ev[e]];
-      const double2 p1 = reinterpret_cast<const double2*>(a.vxy)[a.ev[n + e]];
-      const double2 p2 = reinterpret_cast<const double2*>(a.vxy)[a.ev[2 * n + e]];
+      const double2 p0 = reinterpret_cast<const double2*>(a.vxy)[ent.y];
+      const double2 p1 = reinterpret_cast<const double2*>(a.vxy)[ent.z];
+      const double2 p2 = reinterpret_cast<const double2*>(a.vxy)[ent.w];
       x0 = p0.x; y0 = p0.y; x1 = p1.x; y1 = p1.y; x2 = p2.x; y2 = p2.y;
     } else {
       x0 = a.coords[e]; y0 = a.coords[n + e];
@@ -443,6 +451,7 @@ __global__ __launch_bounds__(256) void rhs2d_face_kernel(RhsArgs a)
     rhs2d_faces<TRI>(a, e, x0, y0, j00, j10, j01, j11, det, acc);
 #pragma unroll
     for (int i = 0; i < NB; ++i) a.out[k * NB + i] = acc[i];
+    if (t + stride < count) ent = list[t + stride];
   }
   __syncthreads();
   // no fence: a workgroup's count load has returned before its loop ended (the loop bound depends on it), and

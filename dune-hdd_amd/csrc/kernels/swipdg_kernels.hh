@@ -126,11 +126,12 @@ struct RhsArgs {
   const int32_t* ev;   // optional vertex-indexed geometry (2d): element -> vertex ids [nvpe][n_local]
   const double* vxy;   //   and vertex coordinates [n_vertices][2]
   // 2d: boundary-element list of the split path (volume kernel + face kernel); null: one fused kernel.
-  // [0] count, [1] finished face workgroups (both zero between calls), entries from RHS_LIST_OFS: own index k
+  // [0] count, [1] finished face workgroups (both zero between calls), entries from RHS_LIST_OFS (16-byte
+  // aligned): {own index k, the element's three vertex ids (vertex-indexed geometry)}
   uint32_t* bnd_list;
 };
 constexpr int RHS_LIST_OFS = 64;
-inline size_t rhs_list_bytes(int64_t n_own) { return size_t(RHS_LIST_OFS + n_own) * sizeof(uint32_t); }
+inline size_t rhs_list_bytes(int64_t n_own) { return size_t(RHS_LIST_OFS) * sizeof(uint32_t) + size_t(n_own) * 16; }
 hipError_t launch_rhs(const RhsArgs& a, hipStream_t s);
 
 // products (rhs.hip): l2, h1_semi, elliptic, boundary_l2 (element-local blocks) and the SWIPDG penalty

@@ -307,7 +307,7 @@ int hdd_swipdg_assemble_elements(hdd_ctx* ctx, const hdd_mesh* mesh, const hdd_s
  * does).  Integration orders: ord(f) + p; Neumann ord(g_N) + p; Dirichlet max(ord(g_D) + p,
  * ord(kappa) + ord(A) + p - 1 + ord(g_D)).  2d meshes with Dirichlet or Neumann data: two launches (volume
  * kernel, then a face kernel over the boundary elements the first one listed) on a list the context holds
- * (4 B per owned element, allocated on the first call of a size class: warm a context up before hipGraph
+ * (16 B per owned element, allocated on the first call of a size class: warm a context up before hipGraph
  * capture; one stream at a time per context). */
 int hdd_swipdg_rhs(hdd_ctx* ctx, const hdd_mesh* mesh, const hdd_scalar_fn* force, const hdd_scalar_fn* kappa,
                    const hdd_tensor_fn* tensor, const hdd_scalar_fn* dirichlet, const hdd_scalar_fn* neumann,
