@@ -1249,9 +1249,9 @@ __global__ void __launch_bounds__(64) pattern_fill_tile_kernel(const int32_t* __
 }
 
 // elem_ptr in three small launches instead of counts + a general-purpose device scan (which took 40 us of the
-// C2 pattern's 200): per-block sums of 1024 elements' counts, one workgroup scanning the block sums, then each
+// C2 pattern's 200): per-block sums of 2048 elements' counts, one workgroup scanning the block sums, then each
 // block re-counts its elements and writes their prefix (the neighbour ids are read twice: 2 x 4 B per face)
-constexpr int PE_THREADS = 256, PE_PER = 4, PE_BLOCK = PE_THREADS * PE_PER;
+constexpr int PE_THREADS = 256, PE_PER = 8, PE_BLOCK = PE_THREADS * PE_PER;   // 8: 2,000 blocks at C2
 
 __device__ __forceinline__ int64_t pe_count(const int32_t* __restrict__ nbrs, int32_t nf, int64_t n_local, int64_t e,
                                             int64_t nb2)
@@ -1326,7 +1326,7 @@ __global__ void __launch_bounds__(PE_THREADS) pattern_sums_scan_kernel(int64_t* 
 }
 
 // BASE_SUM: the block's offset is the sum of the preceding blocks' totals, read by every block (L2-resident:
-// 4,000 totals at C2, <= 16 loads per thread) -- no scan launch between the two passes; else offs[] holds the
+// 2,000 totals at C2, <= 8 loads per thread) -- no scan launch between the two passes; else offs[] holds the
 // scanned offsets.  host_nnz (optional, a mapped pinned host word): the total, written by the last element's
 // thread, so the caller reads nnz after a stream synchronisation without a copy launch.
 template <bool BASE_SUM>
@@ -1399,8 +1399,8 @@ hipError_t launch_pattern_elem_ptr(const int32_t* nbrs, int32_t nf, int64_t n_lo
   const int64_t nblk = pattern_elem_ptr_scratch(n_own);
   hipLaunchKernelGGL(pattern_block_sums_kernel, dim3(unsigned(nblk)), dim3(PE_THREADS), 0, s, nbrs, nf, n_local,
                      own_begin, n_own, nb2, d_scratch);
-  // the offsets summed per block up to 64 K blocks (67 M elements: <= 256 L2 loads per thread), else scanned
-  if (scan_launch || nblk > 65536) {
+  // the offsets summed per block up to 32 K blocks (67 M elements: <= 128 L2 loads per thread), else scanned
+  if (scan_launch || nblk > 32768) {
     hipLaunchKernelGGL(pattern_sums_scan_kernel, dim3(1), dim3(PE_THREADS), 0, s, d_scratch, nblk);
     hipLaunchKernelGGL(pattern_elem_ptr_kernel<false>, dim3(unsigned(nblk)), dim3(PE_THREADS), 0, s, nbrs, nf,
                        n_local, own_begin, n_own, nb2, d_scratch, d_elem_ptr, host_nnz);

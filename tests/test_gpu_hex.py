@@ -223,9 +223,9 @@ def test_device_elem_ptr_block_sums_equal_scan(et):
         del os.environ["HDD_DEBUG_FLAGS"]
     else:
         os.environ["HDD_DEBUG_FLAGS"] = old
-    g = H.Grid.structured(et, 1000 if et == H.SIMPLEX else 1800, 500, px=2, py=1)
+    g = H.Grid.structured(et, 1600 if et == H.SIMPLEX else 3200, 500, px=2, py=1)
     loc = g.local()
-    assert loc.n_own > 768 * 1024
+    assert loc.n_own > 768 * 2048
     pats = [H.DevicePattern(loc, ctx=c, on_device=True) for c in ctxs]
     torch.cuda.synchronize()
     assert pats[0].nnz == pats[1].nnz == int(pats[1].elem_ptr[-1].item())
