@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <fstream>
 #include <memory>
 #include <numeric>
 #include <string>
@@ -828,6 +829,26 @@ extern "C" int hdd_checkerboard(int64_t n, const double* centers, const double l
     cy = std::min<int64_t>(std::max<int64_t>(cy, 0), ncy - 1);
     out[e] = cell_values[cy * ncx + cx];
   }
+  return HDD_OK;
+}
+
+extern "C" int hdd_spe10_model1_read(const char* filename, double min_value, double max_value, double* cells)
+{
+  if (!filename || !cells) return set_error(HDD_ERR_INVALID, "hdd_spe10_model1_read: null argument");
+  if (!(max_value > min_value))
+    return set_error(HDD_ERR_INVALID, "hdd_spe10_model1_read: max (is " + std::to_string(max_value) +
+                                          ") has to be larger than min (is " + std::to_string(min_value) + ")!");
+  std::ifstream in(filename);
+  if (!in.is_open()) return set_error(HDD_ERR_INVALID, std::string("hdd_spe10_model1_read: could not open '") + filename + "'!");
+  const double scale = (max_value - min_value) / (HDD_SPE10_MODEL1_MAX - HDD_SPE10_MODEL1_MIN);
+  const double shift = min_value - scale * HDD_SPE10_MODEL1_MIN;
+  int64_t k = 0;
+  double v = 0.0;
+  while (k < HDD_SPE10_MODEL1_CELLS && in >> v) cells[k++] = v * scale + shift;
+  if (k != HDD_SPE10_MODEL1_CELLS)
+    return set_error(HDD_ERR_INVALID, std::string("hdd_spe10_model1_read: '") + filename + "' holds " +
+                                          std::to_string(k) + " values, " + std::to_string(HDD_SPE10_MODEL1_CELLS) +
+                                          " expected");
   return HDD_OK;
 }
 

@@ -38,6 +38,9 @@ struct hdd_ctx {
   int64_t* nnz_hd = nullptr;   //   (its device address)
   void* rhs_ws = nullptr;      // 2d RHS boundary-element list (counters zero between calls)
   size_t rhs_ws_bytes = 0;
+  hipStream_t rhs_stream = nullptr;   // stream of the last split RHS call, and an event behind its face kernel:
+  hipEvent_t rhs_evt = nullptr;       //   a call on another stream waits for it (the list is shared state)
+  bool rhs_used = false;
 };
 
 int hdd::ctx_device(const hdd_ctx* ctx) { return ctx ? ctx->device : 0; }
@@ -87,12 +90,20 @@ extern "C" int hdd_ctx_create(int hip_device, hdd_ctx** out)
   return HDD_OK;
 }
 
+extern "C" int hdd_ctx_set_debug_flags(hdd_ctx* ctx, int32_t flags)
+{
+  if (!ctx) return set_error(HDD_ERR_INVALID, "hdd_ctx_set_debug_flags: null context");
+  ctx->debug_flags = flags;
+  return HDD_OK;
+}
+
 extern "C" void hdd_ctx_destroy(hdd_ctx* ctx)
 {
   if (ctx && ctx->ws) (void)hipFree(ctx->ws);
   if (ctx && ctx->q3g_tab) (void)hipFree(ctx->q3g_tab);
   if (ctx && ctx->scan_ws) (void)hipFree(ctx->scan_ws);
   if (ctx && ctx->rhs_ws) (void)hipFree(ctx->rhs_ws);
+  if (ctx && ctx->rhs_evt) (void)hipEventDestroy(ctx->rhs_evt);
   if (ctx && ctx->nnz_h) (void)hipHostFree(ctx->nnz_h);
   if (ctx && ctx->ops_d) (void)hipFree(ctx->ops_d);
   if (ctx && ctx->ops_h) (void)hipHostFree(ctx->ops_h);
@@ -873,7 +884,26 @@ extern "C" int hdd_swipdg_rhs(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_
     }
     a.bnd_list = static_cast<uint32_t*>(ctx->rhs_ws);
   }
-  e = launch_rhs(a, static_cast<hipStream_t>(stream));
+  a.skip_face = (ctx->debug_flags & 524288) ? 1 : 0;
+  const hipStream_t s = static_cast<hipStream_t>(stream);
+  // The boundary-element list is context state: calls on different streams are ordered behind each other (the
+  // previous call's face kernel has re-armed the counters before this call's volume kernel appends).  Not under
+  // hipGraph capture, where the captured stream alone orders the replays.
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  const bool ordered = a.bnd_list && hipStreamIsCapturing(s, &cap) == hipSuccess && cap == hipStreamCaptureStatusNone;
+  if (ordered) {
+    if (!ctx->rhs_evt && (e = hipEventCreateWithFlags(&ctx->rhs_evt, hipEventDisableTiming)) != hipSuccess)
+      return hip_fail(e, "hdd_swipdg_rhs: list event");
+    if (ctx->rhs_used && ctx->rhs_stream != s && (e = hipStreamWaitEvent(s, ctx->rhs_evt, 0)) != hipSuccess)
+      return hip_fail(e, "hdd_swipdg_rhs: order behind the previous call's stream");
+  }
+  e = launch_rhs(a, s);
+  if (ordered) {
+    const hipError_t er = hipEventRecord(ctx->rhs_evt, s);
+    if (er != hipSuccess && e == hipSuccess) e = er;
+    ctx->rhs_stream = s;
+    ctx->rhs_used = true;
+  }
   return e == hipSuccess ? HDD_OK : hip_fail(e, "hdd_swipdg_rhs: launch");
 }
 

@@ -403,8 +403,10 @@ __global__ __launch_bounds__(256) void rhs2d_kernel(RhsArgs a)
           uint32_t base = 0;
           if (int(__lane_id()) == lead) base = atomicAdd(a.bnd_list, uint32_t(__popcll(m)));
           base = __shfl(base, lead);
-          if (bnd)   // the vertex ids ride along: the face kernel's geometry is one load away from its entry
-            reinterpret_cast<uint4*>(a.bnd_list + RHS_LIST_OFS)[base + __popcll(m & ((1ull << __lane_id()) - 1))] =
+          const uint32_t slot = base + uint32_t(__popcll(m & ((1ull << __lane_id()) - 1)));
+          // (the list holds n_own entries: a count left over from an interrupted call cannot write past it)
+          if (bnd && slot < uint32_t(a.own_end - a.own_begin))   // the vertex ids ride along: the face kernel's
+            reinterpret_cast<uint4*>(a.bnd_list + RHS_LIST_OFS)[slot] =   // geometry is one load from its entry
                 make_uint4(uint32_t(k), uint32_t(vi0), uint32_t(vi1), uint32_t(vi2));
         }
       } else {
@@ -428,7 +430,7 @@ __global__ __launch_bounds__(256) void rhs2d_face_kernel(RhsArgs a)
   const uint32_t n_own = uint32_t(a.own_end - a.own_begin), stride = gridDim.x * blockDim.x;
   uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   uint4 ent = t < n_own ? list[t] : make_uint4(0, 0, 0, 0);   // loaded beside the count (stale beyond it)
-  const uint32_t count = __atomic_load_n(a.bnd_list, __ATOMIC_RELAXED);
+  const uint32_t count = min(__atomic_load_n(a.bnd_list, __ATOMIC_RELAXED), n_own);
   for (; t < count; t += stride) {
     const int64_t k = ent.x;
     const int64_t e = a.own_begin + k;
@@ -744,14 +746,22 @@ hipError_t launch_rhs(const RhsArgs& a, hipStream_t s)
       // a quarter of the CUs (16 K threads: one list entry per thread at C2's 7,680 boundary elements); every
       // workgroup, busy or not, pays the finish atomic
       const dim3 gf(unsigned(std::max(1, a.n_cu / 4)));
-      if (a.ev) {
-        if (tri) hipLaunchKernelGGL((rhs2d_face_kernel<true, true>), gf, b, 0, s, a);
-        else hipLaunchKernelGGL((rhs2d_face_kernel<false, true>), gf, b, 0, s, a);
+      if (a.skip_face) {
+        e = hipErrorLaunchFailure;   // error injection (tests): the face launch did not happen
       } else {
-        if (tri) hipLaunchKernelGGL((rhs2d_face_kernel<true, false>), gf, b, 0, s, a);
-        else hipLaunchKernelGGL((rhs2d_face_kernel<false, false>), gf, b, 0, s, a);
+        if (a.ev) {
+          if (tri) hipLaunchKernelGGL((rhs2d_face_kernel<true, true>), gf, b, 0, s, a);
+          else hipLaunchKernelGGL((rhs2d_face_kernel<false, true>), gf, b, 0, s, a);
+        } else {
+          if (tri) hipLaunchKernelGGL((rhs2d_face_kernel<true, false>), gf, b, 0, s, a);
+          else hipLaunchKernelGGL((rhs2d_face_kernel<false, false>), gf, b, 0, s, a);
+        }
+        e = hipGetLastError();
       }
-      return hipGetLastError();
+      // the volume kernel has filled the list but no face kernel will reset it: re-arm the counters here, so the
+      // next call starts from an empty list (stream-ordered behind the volume kernel)
+      if (e != hipSuccess) (void)hipMemsetAsync(a.bnd_list, 0, 2 * sizeof(uint32_t), s);
+      return e;
     }
     if (a.has_force && a.force.kind == HDD_FN_COS_PRODUCT && a.nqv == (tri ? 6 : 9) && !a.generic) {
       if (tri && a.ev) hipLaunchKernelGGL((rhs2d_kernel<true, true, 6, HDD_FN_COS_PRODUCT>), dim3(unsigned(blocks)), dim3(256), 0, s, a);

@@ -21,8 +21,11 @@
 #include <dlfcn.h>
 
 #include <algorithm>
+#include <chrono>
+#include <condition_variable>
 #include <cstdint>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -174,19 +177,67 @@ hipError_t upload(T** d, const std::vector<T>& h)
 }  // namespace
 
 // ------------------------------------------------------------------------------------------------
+// in-process device transport (hdd_device_hub): several ranks of one process (one thread each, any devices)
+// exchanging device buffers with the stream / event schedule of an RCCL group send/recv.  Per directed pair
+// (src, dst) a channel holds the sender's latest publication -- its message list and its "packed" event (the
+// send buffers are complete) -- and the receiver's "consumed" event (its copies out of them are complete).
+// ------------------------------------------------------------------------------------------------
+struct hdd_device_hub {
+  struct Channel {
+    uint64_t sent = 0, consumed = 0;     // publications by src / publications dst has copied out of
+    std::vector<std::pair<const double*, int64_t>> msgs;
+    hipEvent_t packed = nullptr;         // src's event after its packs
+    hipEvent_t copied = nullptr;         // dst's event after its copies out of publication `consumed`
+  };
+  int32_t nranks = 0;
+  std::mutex m;
+  std::condition_variable cv;
+  std::vector<Channel> ch;               // [src * nranks + dst]
+  std::string failed;                    // first protocol error (every waiting rank returns it)
+  int refs = 1;
+  double timeout_s = 120.0;
+};
+
+static void hub_release(hdd_device_hub* h)
+{
+  if (!h) return;
+  bool last;
+  {
+    std::lock_guard<std::mutex> lk(h->m);
+    last = --h->refs == 0;
+  }
+  if (last) delete h;
+}
+
+extern "C" int hdd_device_hub_create(int32_t nranks, hdd_device_hub** out)
+{
+  if (!out || nranks < 1) return set_error(HDD_ERR_INVALID, "hdd_device_hub_create: invalid argument");
+  auto* h = new hdd_device_hub;
+  h->nranks = nranks;
+  h->ch.resize(size_t(nranks) * size_t(nranks));
+  *out = h;
+  return HDD_OK;
+}
+
+extern "C" void hdd_device_hub_destroy(hdd_device_hub* hub) { hub_release(hub); }
+
+// ------------------------------------------------------------------------------------------------
 // communicators
 // ------------------------------------------------------------------------------------------------
 struct hdd_comm {
-  enum Kind { RCCL_OWNED, RCCL_WRAPPED, HOST } kind = HOST;
+  enum Kind { RCCL_OWNED, RCCL_WRAPPED, HOST, DEVICE } kind = HOST;
   int device = 0;
   ncclComm_t nccl = nullptr;
-  hipStream_t xfer = nullptr;          // RCCL transfer stream
+  hipStream_t xfer = nullptr;          // transfer stream (RCCL, DEVICE)
   hipEvent_t ready = nullptr, done = nullptr;
   bool posted = false;
   hdd_host_exchange_fn fn = nullptr;
   void* user = nullptr;
   double* pinned = nullptr;            // host staging (HOST)
   size_t pinned_doubles = 0;
+  hdd_device_hub* hub = nullptr;       // DEVICE: the hub, this rank, one "copied" event per source rank
+  int32_t rank = 0;
+  std::vector<hipEvent_t> copied;
 };
 
 static int comm_rccl_streams(hdd_comm* c)
@@ -267,6 +318,33 @@ extern "C" int hdd_comm_create_host(hdd_host_exchange_fn fn, void* user, int32_t
   return HDD_OK;
 }
 
+extern "C" int hdd_comm_create_device(hdd_device_hub* hub, int32_t rank, int32_t hip_device, hdd_comm** out)
+{
+  if (!hub || !out || rank < 0 || rank >= hub->nranks)
+    return set_error(HDD_ERR_INVALID, "hdd_comm_create_device: invalid argument");
+  auto* c = new hdd_comm;
+  c->kind = hdd_comm::DEVICE;
+  c->device = hip_device;
+  c->rank = rank;
+  int rc = comm_rccl_streams(c);
+  hipError_t e = hipSuccess;
+  c->copied.assign(size_t(hub->nranks), nullptr);
+  for (auto& ev : c->copied)
+    if (rc == HDD_OK && e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+  if (rc == HDD_OK && e != hipSuccess) rc = hip_fail(e, "hdd_comm_create_device: events");
+  if (rc) {
+    hdd_comm_destroy(c);
+    return rc;
+  }
+  {
+    std::lock_guard<std::mutex> lk(hub->m);
+    ++hub->refs;
+  }
+  c->hub = hub;
+  *out = c;
+  return HDD_OK;
+}
+
 extern "C" void hdd_comm_destroy(hdd_comm* c)
 {
   if (!c) return;
@@ -275,9 +353,100 @@ extern "C" void hdd_comm_destroy(hdd_comm* c)
   if (c->kind == hdd_comm::RCCL_OWNED && c->nccl && rccl().ok) (void)rccl().CommDestroy(c->nccl);
   if (c->ready) (void)hipEventDestroy(c->ready);
   if (c->done) (void)hipEventDestroy(c->done);
+  for (hipEvent_t ev : c->copied)
+    if (ev) (void)hipEventDestroy(ev);
   if (c->xfer) (void)hipStreamDestroy(c->xfer);
   if (c->pinned) (void)hipHostFree(c->pinned);
+  hub_release(c->hub);
   delete c;
+}
+
+// DEVICE transport: the group send/recv of one rank.  On the transfer stream (which already waits for the packs
+// on `stream`): for every source rank, wait for its packed event, copy its messages into the receive buffers,
+// record "copied"; then wait for every destination's "copied" event, so that -- as after ncclGroupEnd -- the
+// completion event covers the sends too and the next pack cannot overwrite a send buffer that is still read.
+// Host side: publish this rank's sends, then block until each source has published (RCCL blocks on the device
+// instead; a thread per rank makes the host rendezvous harmless).  Messages of one directed pair match in order,
+// zero-count messages are skipped on both sides (as RCCL does).
+static int device_post(hdd_comm* c, int32_t n_peers, const int32_t* peers, const double* const* d_send,
+                       const int64_t* send_count, double* const* d_recv, const int64_t* recv_count)
+{
+  hdd_device_hub& H = *c->hub;
+  const int32_t me = c->rank, n = H.nranks;
+  std::map<int32_t, std::vector<std::pair<const double*, int64_t>>> out;
+  std::map<int32_t, std::vector<std::pair<double*, int64_t>>> in;
+  for (int32_t k = 0; k < n_peers; ++k) {
+    if (peers[k] < 0 || peers[k] >= n || send_count[k] < 0 || recv_count[k] < 0)
+      return set_error(HDD_ERR_INVALID, "hdd_comm_post: peer or count out of range (device transport)");
+    if (send_count[k] > 0) out[peers[k]].emplace_back(d_send[k], send_count[k]);
+    if (recv_count[k] > 0) in[peers[k]].emplace_back(d_recv[k], recv_count[k]);
+  }
+  const auto limit = std::chrono::duration<double>(H.timeout_s);
+  auto fail = [&](std::unique_lock<std::mutex>& lk, const std::string& msg) {
+    if (H.failed.empty()) H.failed = msg;
+    lk.unlock();
+    H.cv.notify_all();
+    return set_error(HDD_ERR_INVALID, "hdd_comm_post (device transport): " + msg);
+  };
+  {   // 1. publish (c->ready was recorded on the pack stream by the caller)
+    std::lock_guard<std::mutex> lk(H.m);
+    for (auto& [dst, msgs] : out) {
+      auto& q = H.ch[size_t(me) * n + dst];
+      q.msgs = msgs;
+      q.packed = c->ready;
+      ++q.sent;
+    }
+  }
+  H.cv.notify_all();
+  // 2. receives: wait for each source's publication, copy on the transfer stream, record copied
+  for (auto& [src, msgs] : in) {
+    auto& q = H.ch[size_t(src) * n + me];
+    std::vector<std::pair<const double*, int64_t>> sent;
+    hipEvent_t packed;
+    {
+      std::unique_lock<std::mutex> lk(H.m);
+      if (!H.cv.wait_for(lk, limit, [&] { return q.sent > q.consumed || !H.failed.empty(); }))
+        return fail(lk, "rank " + std::to_string(me) + " timed out waiting for rank " + std::to_string(src));
+      if (!H.failed.empty()) return set_error(HDD_ERR_INVALID, "hdd_comm_post (device transport): " + H.failed);
+      if (q.msgs.size() != msgs.size())
+        return fail(lk, "rank " + std::to_string(src) + " sent " + std::to_string(q.msgs.size()) + " messages to rank " +
+                            std::to_string(me) + ", which receives " + std::to_string(msgs.size()));
+      for (size_t i = 0; i < msgs.size(); ++i)
+        if (q.msgs[i].second != msgs[i].second)
+          return fail(lk, "message size mismatch between rank " + std::to_string(src) + " and rank " + std::to_string(me));
+      sent = q.msgs;
+      packed = q.packed;
+    }
+    hipError_t e = hipStreamWaitEvent(c->xfer, packed, 0);
+    for (size_t i = 0; i < msgs.size() && e == hipSuccess; ++i)
+      e = hipMemcpyAsync(msgs[i].first, sent[i].first, size_t(msgs[i].second) * sizeof(double), hipMemcpyDefault, c->xfer);
+    if (e == hipSuccess) e = hipEventRecord(c->copied[size_t(src)], c->xfer);
+    if (e != hipSuccess) {
+      std::unique_lock<std::mutex> lk(H.m);
+      return fail(lk, std::string("HIP error on rank ") + std::to_string(me) + ": " + hipGetErrorString(e));
+    }
+    {
+      std::lock_guard<std::mutex> lk(H.m);
+      q.copied = c->copied[size_t(src)];
+      ++q.consumed;
+    }
+    H.cv.notify_all();
+  }
+  // 3. sends complete when every destination has copied them
+  for (auto& [dst, msgs] : out) {
+    auto& q = H.ch[size_t(me) * n + dst];
+    hipEvent_t copied;
+    {
+      std::unique_lock<std::mutex> lk(H.m);
+      if (!H.cv.wait_for(lk, limit, [&] { return q.consumed == q.sent || !H.failed.empty(); }))
+        return fail(lk, "rank " + std::to_string(me) + " timed out waiting for rank " + std::to_string(dst) + " to receive");
+      if (!H.failed.empty()) return set_error(HDD_ERR_INVALID, "hdd_comm_post (device transport): " + H.failed);
+      copied = q.copied;
+    }
+    const hipError_t e = hipStreamWaitEvent(c->xfer, copied, 0);
+    if (e != hipSuccess) return hip_fail(e, "hdd_comm_post: wait for the receivers (device transport)");
+  }
+  return HDD_OK;
 }
 
 extern "C" int hdd_comm_post(hdd_comm* c, int32_t n_peers, const int32_t* peers, const double* const* d_send,
@@ -293,6 +462,14 @@ extern "C" int hdd_comm_post(hdd_comm* c, int32_t n_peers, const int32_t* peers,
     e = hipEventRecord(c->ready, s);
     if (e == hipSuccess) e = hipStreamWaitEvent(c->xfer, c->ready, 0);
     if (e != hipSuccess) return hip_fail(e, "hdd_comm_post: order transfer after pack");
+    if (c->kind == hdd_comm::DEVICE) {
+      const int rc = device_post(c, n_peers, peers, d_send, send_count, d_recv, recv_count);
+      if (rc) return rc;
+      e = hipEventRecord(c->done, c->xfer);
+      if (e != hipSuccess) return hip_fail(e, "hdd_comm_post: record completion");
+      c->posted = true;
+      return HDD_OK;
+    }
     const RcclApi& R = rccl();
     ncclResult_t r = R.GroupStart();
     if (r != ncclSuccess) return nccl_fail(r, "ncclGroupStart");

@@ -114,7 +114,8 @@ struct RhsArgs {
   double tc[6];
   const double* tper;
   KappaArg force, kappa, dirichlet, neumann;
-  int32_t has_force, has_dirichlet, has_neumann, pad;
+  int32_t has_force, has_dirichlet, has_neumann;
+  int32_t skip_face;   // 1: error injection (HDD_DEBUG_FLAGS bit 524288): the split path's face launch "fails"
   double sigma_boundary, beta;
   int32_t nqv, nqd, nqn, n_cu;
   int32_t generic;   // 1: the run-time-rule kernel only (HDD_DEBUG_FLAGS bit 32768: A/B of the unrolled path)
@@ -126,8 +127,10 @@ struct RhsArgs {
   const int32_t* ev;   // optional vertex-indexed geometry (2d): element -> vertex ids [nvpe][n_local]
   const double* vxy;   //   and vertex coordinates [n_vertices][2]
   // 2d: boundary-element list of the split path (volume kernel + face kernel); null: one fused kernel.
-  // [0] count, [1] finished face workgroups (both zero between calls), entries from RHS_LIST_OFS (16-byte
-  // aligned): {own index k, the element's three vertex ids (vertex-indexed geometry)}
+  // [0] count, [1] finished face workgroups (both zero between calls: reset by the face kernel's last
+  // workgroup, or by launch_rhs when the face launch fails), entries from RHS_LIST_OFS (16-byte aligned, room
+  // for n_own of them; the volume kernel drops entries beyond it, the face kernel clamps the count to it):
+  // {own index k, the element's three vertex ids (vertex-indexed geometry)}
   uint32_t* bnd_list;
 };
 constexpr int RHS_LIST_OFS = 64;

@@ -152,6 +152,7 @@ def lib():
         "hdd_checkerboard": (_I32, [_I64, _VP, _VP, _VP, _I32, _I32, _VP, _VP]),
         "hdd_indicator": (_I32, [_I64, _VP, _I32, _VP, _VP]),
         "hdd_indicator_sum": (_I32, [_I64, _VP, _I32, _VP, _VP]),
+        "hdd_spe10_model1_read": (_I32, [C.c_char_p, C.c_double, C.c_double, _VP]),
         "hdd_pattern_count": (_I32, [_I32, _I64, _I64, _I64, _VP, C.POINTER(_I64)]),
         "hdd_pattern_fill": (_I32, [_I32, _I64, _I64, _I64, _VP, _VP, _VP, _VP, _VP]),
         "hdd_dg_pattern_count": (_I32, [_I32, _I32, _I64, _I64, _I64, _VP, C.POINTER(_I64)]),
@@ -181,6 +182,10 @@ def lib():
         "hdd_comm_create_rccl": (_I32, [_VP, _I32, _I32, _I32, _VP]),
         "hdd_comm_wrap_rccl": (_I32, [_VP, _I32, _VP]),
         "hdd_comm_create_host": (_I32, [HOST_EXCHANGE_FN, _VP, _I32, _VP]),
+        "hdd_ctx_set_debug_flags": (_I32, [_VP, _I32]),
+        "hdd_device_hub_create": (_I32, [_I32, _VP]),
+        "hdd_device_hub_destroy": (None, [_VP]),
+        "hdd_comm_create_device": (_I32, [_VP, _I32, _I32, _VP]),
         "hdd_comm_destroy": (None, [_VP]),
         "hdd_comm_post": (_I32, [_VP, _I32, _VP, _VP, _VP, _VP, _VP, _VP]),
         "hdd_comm_wait": (_I32, [_VP, _VP]),
@@ -219,6 +224,17 @@ def declared_symbols(header=HEADER):
     import re
     txt = open(header).read()
     return sorted(set(re.findall(r"\b(hdd_[a-z0-9_]+)\s*\(", txt)))
+
+
+SPE10_MODEL1_MIN, SPE10_MODEL1_MAX = 0.001, 998.915
+
+
+def spe10_model1_read(filename, min_value=SPE10_MODEL1_MIN, max_value=SPE10_MODEL1_MAX):
+    """The SPE10 Model1 permeability data file (hdd_spe10_model1_read; problems/spe10.hh:151-156): the 100 x 20
+    checkerboard cells (x fastest) as a float64 array [2000]."""
+    out = np.empty(2000)
+    _check(lib().hdd_spe10_model1_read(os.fsencode(filename), min_value, max_value, _p(out)), "hdd_spe10_model1_read")
+    return out
 
 
 def indicator(centers, boxes, summed=False):
@@ -431,6 +447,10 @@ class Context:
         h = C.c_void_p()
         _check(lib().hdd_ctx_create(device, C.byref(h)), "hdd_ctx_create")
         self.h = h
+
+    def set_debug_flags(self, flags):
+        """profiling ablations / error injection (hdd_ctx_set_debug_flags; 0 in production)"""
+        _check(lib().hdd_ctx_set_debug_flags(self.h, int(flags)), "hdd_ctx_set_debug_flags")
 
     def __del__(self):
         if getattr(self, "h", None):
@@ -825,6 +845,14 @@ class Comm:
         _check(lib().hdd_comm_create_host(fn, None, device, C.byref(h)), "hdd_comm_create_host")
         return cls(h, keep=fn)
 
+    @classmethod
+    def device(cls, hub, rank, device=0):
+        """In-process device transport (hdd_comm_create_device): rank `rank` of hub.nranks thread ranks of this
+        process; the exchange runs on the communicator's transfer stream exactly as over RCCL."""
+        h = C.c_void_p()
+        _check(lib().hdd_comm_create_device(hub.h, rank, device, C.byref(h)), "hdd_comm_create_device")
+        return cls(h, keep=hub)
+
     def post(self, peers, sends, recvs, stream=None):
         """hdd_comm_post of device tensors (float64), then the caller calls wait()."""
         torch = _torch()
@@ -846,6 +874,23 @@ class Comm:
         if getattr(self, "h", None):
             try:
                 lib().hdd_comm_destroy(self.h)
+            except Exception:   # interpreter shutdown
+                pass
+            self.h = None
+
+
+class DeviceHub:
+    """Rendezvous of the in-process device transport (hdd_device_hub): nranks thread ranks of one process."""
+
+    def __init__(self, nranks):
+        h = C.c_void_p()
+        _check(lib().hdd_device_hub_create(nranks, C.byref(h)), "hdd_device_hub_create")
+        self.h, self.nranks = h, nranks
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            try:
+                lib().hdd_device_hub_destroy(self.h)
             except Exception:   # interpreter shutdown
                 pass
             self.h = None

@@ -7,6 +7,10 @@
 //   sharded_main threads <n> [outdir]
 //       n ranks as threads on GPU 0 with an in-process mailbox as the host transport (RCCL refuses two ranks
 //       on one device); every rank's rows must equal, bit for bit, the rows of the single-GPU BlockSWIPDG.
+//   sharded_main device <n> [outdir]
+//       the same n thread ranks with the in-process device transport (hdd_comm_create_device): the halo moves by
+//       device copies on each rank's transfer stream with RCCL's event schedule, so the step takes its RCCL branch
+//       (pack, exchange and ghost-adjacent elements on the transfer stream, joined by an event).
 //   sharded_main rccl <id_file> <rank> <nranks> <hip_device> [outdir]
 //       one process per GPU over RCCL: rank 0 writes its ncclUniqueId to id_file, the others read it; the
 //       rows are written to outdir/rank<r>.bin for the caller to compare.
@@ -119,7 +123,7 @@ Problems::Problem mixed_orders()
   return p;
 }
 
-int run_threads(int n, const std::string& outdir)
+int run_threads(int n, const std::string& outdir, bool device)
 {
   int fails = 0;
   for (int pi = 0; pi < 2; ++pi)
@@ -136,6 +140,7 @@ int run_threads(int n, const std::string& outdir)
     const auto& gcol = gp.col();
 
     Mailbox mb;
+    const auto hub = Parallel::Communicator::device_hub(n);   // (device transport)
     std::vector<std::vector<double>> vals(static_cast<size_t>(n)), rhs(static_cast<size_t>(n));
     std::vector<std::vector<int32_t>> cols(static_cast<size_t>(n));
     std::vector<int64_t> first(static_cast<size_t>(n)), rows(static_cast<size_t>(n));
@@ -145,10 +150,12 @@ int run_threads(int n, const std::string& outdir)
       th.emplace_back([&, r] {
         try {
           Endpoint ep{&mb, r};
-          auto comm = Parallel::Communicator::host(mailbox_exchange, &ep, 0);
+          auto comm = device ? Parallel::Communicator::device(hub, r, 0)
+                             : Parallel::Communicator::host(mailbox_exchange, &ep, 0);
           D::ShardedBlockSWIPDG sh(ms, Dune::Stuff::Common::Configuration(), problem, comm, r, n, 0);
           sh.init();
-          sh.assemble();   // a second step: the halo again, through the same mailbox
+          sh.assemble();   // more steps: the halo again, through the same transport
+          if (device) sh.assemble();
           (void)hipDeviceSynchronize();
           const auto& A = sh.system_matrix();
           vals[size_t(r)] = A.affine_part();
@@ -188,7 +195,7 @@ int run_threads(int n, const std::string& outdir)
                 (long long)gp.nnz, (long long)mismatches);
     fails += mismatches != 0;
   }
-  if (!fails) std::printf("sharded threads ok\n");
+  if (!fails) std::printf("sharded %s ok\n", device ? "device-transport threads" : "threads");
   return fails ? 1 : 0;
 }
 
@@ -231,10 +238,11 @@ int main(int argc, char** argv)
 {
   try {
     const std::string mode = argc > 1 ? argv[1] : "threads";
-    if (mode == "threads") return run_threads(argc > 2 ? std::atoi(argv[2]) : 3, argc > 3 ? argv[3] : "");
+    if (mode == "threads" || mode == "device")
+      return run_threads(argc > 2 ? std::atoi(argv[2]) : 3, argc > 3 ? argv[3] : "", mode == "device");
     if (mode == "rccl" && argc >= 6)
       return run_rccl(argv[2], std::atoi(argv[3]), std::atoi(argv[4]), std::atoi(argv[5]), argc > 6 ? argv[6] : "");
-    std::fprintf(stderr, "usage: sharded_main threads <n> [outdir] | rccl <id_file> <rank> <nranks> <device> [outdir]\n");
+    std::fprintf(stderr, "usage: sharded_main threads|device <n> [outdir] | rccl <id_file> <rank> <nranks> <device> [outdir]\n");
     return 2;
   } catch (const std::exception& e) {
     std::fprintf(stderr, "error: %s\n", e.what());

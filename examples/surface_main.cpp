@@ -335,6 +335,80 @@ int main(int argc, char** argv)
     } catch (const S::Exceptions::wrong_input_given& e) {
       std::printf("oversampled robin rejected\n");
     }
+    // the caller-owned variants of the reference's Python bindings (block-swipdg.hh:602-690, 770-831): each `new`
+    // object equals its by-value getter, owns its values (zeroing them changes nothing else) and is deleted here
+    {
+      int ok = 1;
+      using M = Discretizations::AffinelyDecomposedMatrix;
+      auto same = [](const M& a, const M& b) {
+        return a.pattern->row_ptr() == b.pattern->row_ptr() && a.pattern->col() == b.pattern->col() &&
+               a.affine_part() == b.affine_part() && a.num_components() == b.num_components();
+      };
+      auto zero = [](const M& a) {
+        (void)hipMemset(a.affine->get(), 0, size_t(a.pattern->nnz) * sizeof(double));
+        (void)hipDeviceSynchronize();
+      };
+      std::vector<double> x(size_t(block.num_dofs()));
+      for (size_t i = 0; i < x.size(); ++i) x[i] = 0.5 * double(i);
+      std::vector<std::vector<double>> locals;
+      for (int ss = 0; ss < block.num_subdomains(); ++ss) {
+        std::vector<double>* lv = block.localize_vector_and_return_ptr(x, ss);
+        ok &= *lv == block.localize_vector(x, ss);
+        locals.push_back(*lv);
+        delete lv;
+      }
+      std::vector<double>* gv = block.globalize_vectors_and_return_ptr(locals);
+      ok &= *gv == x;
+      delete gv;
+      const int nb0 = block.neighbouring_subdomains(0).at(0);
+      for (int pass = 0; pass < 2; ++pass) {   // extraction one by one, then from the batched views
+        if (pass == 1) block.extract_operators();
+        const M lo_ref = block.get_local_operator(0), co_ref = block.get_coupling_operator(0, nb0);
+        M* lo = block.get_local_operator_and_return_ptr(0);
+        M* co = block.get_coupling_operator_and_return_ptr(0, nb0);
+        ok &= same(*lo, lo_ref) && same(*co, co_ref);
+        zero(*lo);
+        zero(*co);
+        ok &= same(block.get_local_operator(0), lo_ref) && same(block.get_coupling_operator(0, nb0), co_ref);
+        if (pass == 1)   // the batched view itself is untouched too
+          ok &= block.extract_operators().at({0, nb0}).affine_part() == co_ref.affine_part();
+        delete lo;
+        delete co;
+      }
+      M* lp = block.get_local_product_and_return_ptr(0, "l2");
+      const M lp_ref = block.get_local_product(0, "l2");
+      const auto lp_vals = lp_ref.affine_part();
+      ok &= same(*lp, lp_ref);
+      zero(*lp);
+      ok &= block.get_local_product(0, "l2").affine_part() == lp_vals;
+      delete lp;
+      Discretizations::AffinelyDecomposedVector* lf = block.get_local_functional_and_return_ptr(0);
+      ok &= lf->affine_part() == block.get_local_functional(0).affine_part() && lf->size == block.get_local_functional(0).size;
+      delete lf;
+      Discretizations::SWIPDG* ld = block.pb_get_local_discretization(0);
+      ok &= ld->system_matrix().affine_part() == L0.system_matrix().affine_part() &&
+            ld->rhs().affine_part() == L0.rhs().affine_part() && ld->pattern().col() == L0.pattern().col() &&
+            ld->available_products() == L0.available_products() && ld != &L0;
+      delete ld;
+      for (const char* bt : {"dirichlet", "neumann"}) {
+        Discretizations::SWIPDG* od = block.pb_get_oversampled_discretization(0, bt);
+        const auto& O = block.get_oversampled_discretization(0, bt);
+        ok &= od->system_matrix().affine_part() == O.system_matrix().affine_part() &&
+              od->rhs().affine_part() == O.rhs().affine_part() && od->num_dofs() == O.num_dofs();
+        delete od;
+      }
+      try {
+        delete block.pb_get_local_discretization(-1);
+        ok = 0;
+      } catch (const S::Exceptions::index_out_of_range&) {
+      }
+      try {
+        delete block.pb_get_oversampled_discretization(0, "robin");
+        ok = 0;
+      } catch (const S::Exceptions::wrong_input_given&) {
+      }
+      std::printf("caller-owned copies %d\n", ok);
+    }
   }
 
   // 6b. the same in 3d (block-swipdg.hh:783-817 is dimension-generic): ESV2007 3d on 4 x 3 x 3 hexahedra, Q2,

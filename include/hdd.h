@@ -36,10 +36,11 @@
 extern "C" {
 #endif
 
-#define HDD_ABI_VERSION 6   /* 3: hdd_mesh vertex-indexed geometry, hdd_local_vertices;
+#define HDD_ABI_VERSION 7   /* 3: hdd_mesh vertex-indexed geometry, hdd_local_vertices;
                                4: HDD_FN_FLATTOP (hdd_scalar_fn.table / n_table), hdd_indicator_sum;
                                5: hdd_shard_info.halo_elements, hdd_swipdg_assemble_elements;
-                               6: hdd_grid_create_hex_from_connectivity */
+                               6: hdd_grid_create_hex_from_connectivity;
+                               7: in-process device transport (hdd_device_hub, hdd_comm_create_device) */
 #define HDD_MAX_COMP 8
 
 typedef enum {
@@ -70,6 +71,10 @@ int hdd_abi_version(void);
 /* binds `hip_device`; replaces nothing in the reference (DUNE is host-only) */
 int hdd_ctx_create(int hip_device, hdd_ctx** out);
 void hdd_ctx_destroy(hdd_ctx* ctx);
+/* profiling ablations / error injection of the tests (the HDD_DEBUG_FLAGS value a context reads at creation;
+ * 0 in production).  Bit 524288: hdd_swipdg_rhs's face launch is treated as failed (the call returns
+ * HDD_ERR_HIP after its volume kernel; the next call must still be correct). */
+int hdd_ctx_set_debug_flags(hdd_ctx* ctx, int32_t flags);
 /* message of the last failure on this thread (ctx may be NULL); never NULL */
 const char* hdd_last_error(const hdd_ctx* ctx);
 
@@ -177,6 +182,19 @@ int hdd_indicator(int64_t n, const double* centers /*[2][n]*/, int32_t n_boxes, 
 /* the sum of one-box Indicators (make_sum of the channel's per-box functions, problems/spe10.hh:139-148 with
  * channel_boundary_layer == 0): sum of the values of every closed box containing the barycentre */
 int hdd_indicator_sum(int64_t n, const double* centers /*[2][n]*/, int32_t n_boxes, const double* boxes, double* out);
+/* The SPE10 Model1 permeability data file (problems/spe10.hh:151-156: Spe10FunctionType(filename, lower_left,
+ * upper_right, model1_min_value, model1_max_value)).  dune-stuff's reader is not in the reference tree; restated
+ * (parity unpinned): whitespace-separated numbers, of which the first HDD_SPE10_MODEL1_CELLS (100 x 20, x
+ * fastest -- the file holds 6000) are the cells of the 100 x 20 checkerboard, mapped affinely so that
+ * [HDD_SPE10_MODEL1_MIN, HDD_SPE10_MODEL1_MAX] goes onto [min_value, max_value] (the identity for the values the
+ * reference passes).  cells: [HDD_SPE10_MODEL1_CELLS].  Missing / short file or max_value <= min_value:
+ * HDD_ERR_INVALID. */
+#define HDD_SPE10_MODEL1_NX 100
+#define HDD_SPE10_MODEL1_NZ 20
+#define HDD_SPE10_MODEL1_CELLS 2000
+#define HDD_SPE10_MODEL1_MIN 0.001
+#define HDD_SPE10_MODEL1_MAX 998.915
+int hdd_spe10_model1_read(const char* filename, double min_value, double max_value, double* cells);
 
 /* ---------------------------------------------------------------------------------------------- */
 /* sparsity pattern (host) -- replaces EllipticSWIPDG::pattern(test, ansatz) (swipdg.hh:169) and the */
@@ -415,6 +433,18 @@ int hdd_comm_create_rccl(const void* id, int32_t nranks, int32_t rank, int32_t h
 int hdd_comm_wrap_rccl(void* nccl_comm, int32_t hip_device, hdd_comm** out);
 /* host-staged transport: device -> pinned host -> fn -> device (synchronous; rehearsal / tests / MPI) */
 int hdd_comm_create_host(hdd_host_exchange_fn fn, void* user, int32_t hip_device, hdd_comm** out);
+/* In-process device transport (ABI 7): nranks ranks of ONE process, one thread each (any devices, one device
+ * allowed), exchanging device buffers with RCCL's stream schedule -- the exchange runs on the communicator's
+ * transfer stream: it waits for each source's packed event, copies its messages (hipMemcpyAsync) into the
+ * receive buffers, records a "copied" event, and completes (the event hdd_comm_wait joins) once every
+ * destination has copied this rank's sends; so the sharded step takes exactly the branch it takes over RCCL.
+ * hdd_comm_post blocks the calling thread until every source rank has posted (a host rendezvous; 120 s
+ * timeout, then every waiting rank returns HDD_ERR_INVALID).  The hub is reference counted: destroying it
+ * while communicators still use it is allowed. */
+typedef struct hdd_device_hub hdd_device_hub;
+int hdd_device_hub_create(int32_t nranks, hdd_device_hub** out);
+void hdd_device_hub_destroy(hdd_device_hub* hub);
+int hdd_comm_create_device(hdd_device_hub* hub, int32_t rank, int32_t hip_device, hdd_comm** out);
 void hdd_comm_destroy(hdd_comm* comm);
 /* Post one exchange of device buffers: it starts after the work enqueued on `stream` so far; RCCL runs
  * it on the communicator's own transfer stream (ncclGroupStart / ncclSend / ncclRecv / ncclGroupEnd), so

@@ -257,6 +257,14 @@ class DeviceArray {
   size_t n_ = 0;
   std::shared_ptr<const void> owner_;   // set for views: the allocation is the owner's
 };
+// a device-to-device copy into an allocation of its own
+template <class T>
+std::shared_ptr<DeviceArray<T>> device_copy(const DeviceArray<T>& a)
+{
+  auto o = std::make_shared<DeviceArray<T>>(a.size());
+  if (a.size()) hip_check(hipMemcpy(o->get(), a.get(), a.size() * sizeof(T), hipMemcpyDeviceToDevice), "D2D");
+  return o;
+}
 using Timer = std::chrono::steady_clock;
 inline double seconds_since(Timer::time_point t0)
 {
@@ -472,10 +480,11 @@ inline std::array<double, 2> flattop_default_boundary_layer() { return {{0.1, 0.
 inline Problem Spe10Model1(std::vector<double> permeability, std::vector<std::array<double, 5>> channel,
                            std::vector<std::array<double, 5>> forces, bool parametric_channel,
                            std::array<double, 2> channel_boundary_layer = flattop_default_boundary_layer(),
-                           int flattop_order = 3)
+                           int flattop_order = 3, std::array<double, 2> lower_left = {{0.0, 0.0}},
+                           std::array<double, 2> upper_right = {{5.0, 1.0}})
 {
   Problem p;
-  p.diffusion_tensor = TensorFunction::spe10_model1(std::move(permeability));
+  p.diffusion_tensor = TensorFunction::spe10_model1(std::move(permeability), lower_left, upper_right);
   p.force = ScalarFunction::indicator(std::move(forces));
   if (channel.empty()) return p;   // no channel: diffusion factor 1 + 0.9 * 0 (problems/spe10.hh:141-142)
   const bool indicator = channel_boundary_layer[0] == 0.0 && channel_boundary_layer[1] == 0.0;
@@ -491,11 +500,28 @@ inline Problem Spe10Model1(std::vector<double> permeability, std::vector<std::ar
     p.diffusion_factor.register_component(channel_fn(0.0, 1.0), Pymor::ParameterFunctional("mu", "-1.0*mu", -1.0));
   return p;
 }
+
+// Spe10::Model1 from its data file, with the reference ctor's arguments in its order (problems/spe10.hh:111-125):
+// the permeability checkerboard on [lower_left, upper_right] read by hdd_spe10_model1_read with the Model1
+// min / max values (151-156; dune-stuff's reader restated, parity unpinned); the rest as the vector form above
+inline Problem Spe10Model1(const std::string& filename, std::array<double, 2> lower_left,
+                           std::array<double, 2> upper_right, std::vector<std::array<double, 5>> channel_values,
+                           std::vector<std::array<double, 5>> force_values,
+                           std::array<double, 2> channel_boundary_layer = flattop_default_boundary_layer(),
+                           bool parametric_channel = false, int flattop_order = 3)
+{
+  std::vector<double> perm(HDD_SPE10_MODEL1_CELLS);
+  internal::check(hdd_spe10_model1_read(filename.c_str(), HDD_SPE10_MODEL1_MIN, HDD_SPE10_MODEL1_MAX, perm.data()),
+                  "hdd_spe10_model1_read");
+  return Spe10Model1(std::move(perm), std::move(channel_values), std::move(force_values), parametric_channel,
+                     channel_boundary_layer, flattop_order, lower_left, upper_right);
+}
 }  // namespace Problems
 
 namespace Parallel {
 // the face-halo transport of a ShardedBlockSWIPDG (hdd_comm): RCCL between one process per GPU, an existing
-// ncclComm_t, or a host callback (MPI, an in-process mailbox, ...)
+// ncclComm_t, a host callback (MPI, an in-process mailbox, ...), or the in-process device transport (thread
+// ranks, RCCL's stream schedule with device copies)
 class Communicator {
  public:
   Communicator() = default;   // no peers (a single rank)
@@ -523,6 +549,19 @@ class Communicator {
     hdd_comm* c = nullptr;
     internal::check(hdd_comm_create_host(fn, user, hip_device, &c), "hdd_comm_create_host");
     return Communicator(c);
+  }
+  // in-process device transport: rank `rank` of the hub's thread ranks (the RCCL stream schedule, device copies)
+  static Communicator device(const std::shared_ptr<hdd_device_hub>& hub, int rank, int hip_device)
+  {
+    hdd_comm* c = nullptr;
+    internal::check(hdd_comm_create_device(hub.get(), rank, hip_device, &c), "hdd_comm_create_device");
+    return Communicator(c);
+  }
+  static std::shared_ptr<hdd_device_hub> device_hub(int nranks)
+  {
+    hdd_device_hub* h = nullptr;
+    internal::check(hdd_device_hub_create(nranks, &h), "hdd_device_hub_create");
+    return std::shared_ptr<hdd_device_hub>(h, hdd_device_hub_destroy);
   }
   hdd_comm* get() const { return c_.get(); }
 
@@ -583,6 +622,15 @@ class AffinelyDecomposedMatrix {
   std::vector<double> affine_part() const { return trimmed(*affine); }
   std::vector<double> component(int q) const { return trimmed(*comps.at(size_t(q))); }
   const Pymor::ParameterFunctional& coefficient(int q) const { return coefficients.at(size_t(q)); }
+  // A copy whose value arrays are its own (device-to-device copies; the immutable pattern is shared).  A plain
+  // copy of this class shares the value arrays, as the reference's containers share their backend until a write.
+  AffinelyDecomposedMatrix clone() const
+  {
+    AffinelyDecomposedMatrix c = *this;
+    if (affine) c.affine = internal::device_copy(*affine);
+    for (auto& q : c.comps) q = internal::device_copy(*q);
+    return c;
+  }
   // A(mu) = A_aff + sum_q theta_q(mu) A_q on the shared pattern (hdd_affine_lincomb)
   std::vector<double> freeze_parameter(double mu) const
   {
@@ -621,6 +669,13 @@ class AffinelyDecomposedVector {
   std::vector<double> affine_part() const { auto h = affine->download(); h.resize(size_t(size)); return h; }
   std::vector<double> component(int q) const { auto h = comps.at(size_t(q))->download(); h.resize(size_t(size)); return h; }
   const Pymor::ParameterFunctional& coefficient(int q) const { return coefficients.at(size_t(q)); }
+  AffinelyDecomposedVector clone() const   // (as AffinelyDecomposedMatrix::clone)
+  {
+    AffinelyDecomposedVector c = *this;
+    if (affine) c.affine = internal::device_copy(*affine);
+    for (auto& q : c.comps) q = internal::device_copy(*q);
+    return c;
+  }
   // b(mu) = b_aff + sum_q theta_q(mu) b_q (host)
   std::vector<double> freeze_parameter(double mu) const
   {
@@ -1232,9 +1287,10 @@ class BlockSWIPDG : public SWIPDG {
   // Every local and coupling operator at once (hdd_block_operators_map_device / _values_device: five
   // launches whatever their number, asynchronous -- the counts come from the face pairs counted at
   // construction).  Their patterns and values are views into one row-pointer, one column and one value array
-  // per component (together the size of the system matrix); afterwards get_local_operator /
-  // get_coupling_operator return these instead of extracting one by one.  The LRBMS consumer
-  // (pyMOR's BlockSWIPDG wrapper) asks for all of them.
+  // per component (together the size of the system matrix): writing through one of these views changes the
+  // shared arrays.  Afterwards get_local_operator / get_coupling_operator hand out clones of them (values of
+  // their own, one device copy each) instead of extracting one by one.  The LRBMS consumer (pyMOR's
+  // BlockSWIPDG wrapper) asks for all of them.
   const std::map<std::pair<int, int>, AffinelyDecomposedMatrix>& extract_operators() const
   {
     if (!operators_.empty()) return operators_;
@@ -1343,17 +1399,8 @@ class BlockSWIPDG : public SWIPDG {
   // AllNeumann, ZeroBoundary(problem), the requested products; created and initialised on first use
   const SWIPDG& get_local_discretization(int ss) const
   {
-    if (ss < 0 || ss >= num_subdomains())
-      throw Stuff::Exceptions::index_out_of_range("Given subdomain " + std::to_string(ss) +
-                                                  " too large (has to be smaller than " +
-                                                  std::to_string(num_subdomains()) + "!");
-    auto& d = local_discretizations_[size_t(ss)];
-    if (!d) {
-      d = std::make_shared<SWIPDG>(grid_, Stuff::Grid::BoundaryInfos::AllNeumann::default_config(),
-                                   Problems::ZeroBoundary(original_problem_), Layer::local, ss, only_these_products_,
-                                   device_);
-      d->init();
-    }
+    auto& d = local_discretizations_[size_t(subdomain_check(ss))];
+    if (!d) d = make_local_discretization(ss);
     return *d;
   }
 
@@ -1362,24 +1409,61 @@ class BlockSWIPDG : public SWIPDG {
   // that grid part, ZeroBoundary(problem), the requested products; created and initialised on first use
   const SWIPDG& get_oversampled_discretization(int ss, const std::string& boundary_value_type) const
   {
-    if (ss < 0 || ss >= num_subdomains())
-      throw Stuff::Exceptions::index_out_of_range("Given subdomain " + std::to_string(ss) +
-                                                  " too large (has to be smaller than " +
-                                                  std::to_string(num_subdomains()) + "!");
-    Stuff::Common::Configuration cfg;
-    if (boundary_value_type == "dirichlet") cfg = Stuff::Grid::BoundaryInfos::AllDirichlet::default_config();
-    else if (boundary_value_type == "neumann") cfg = Stuff::Grid::BoundaryInfos::AllNeumann::default_config();
-    else
-      throw Stuff::Exceptions::wrong_input_given(
-          "Unknown boundary_value_type given (has to be dirichlet or neumann): " + boundary_value_type);
+    subdomain_check(ss);
+    boundary_config(boundary_value_type);
     auto& d = oversampled_[{ss, boundary_value_type}];
-    if (!d) {
-      std::vector<int64_t> ids = oversampled_elements(ss);
-      d = std::make_shared<SWIPDG>(subset_grid(ids), ids, info_.n_elements, cfg, Problems::ZeroBoundary(original_problem_),
-                                   only_these_products_, device_);
-      d->init();
-    }
+    if (!d) d = make_oversampled_discretization(ss, boundary_value_type);
     return *d;
+  }
+
+  // The caller-owned variants the reference's Python bindings use (pybindgen caller_owns_return,
+  // examples/linearelliptic/cg_bindings_generator.py:57-60): block-swipdg.hh:602-610, 620-623, 634-637, 672-676,
+  // 687-690 return `new` copies of the by-value getters; the caller deletes them.  The operator / product /
+  // functional copies own their values (clone()), so writing through one changes nothing else.
+  std::vector<double>* globalize_vectors_and_return_ptr(const std::vector<std::vector<double>>& locals) const
+  {
+    return new std::vector<double>(globalize_vectors(locals));
+  }
+  std::vector<double>* localize_vector_and_return_ptr(const std::vector<double>& global, int ss) const
+  {
+    return new std::vector<double>(localize_vector(global, ss));
+  }
+  AffinelyDecomposedMatrix* get_local_product_and_return_ptr(int ss, const std::string& id) const
+  {
+    return new AffinelyDecomposedMatrix(get_local_product(ss, id).clone());
+  }
+  AffinelyDecomposedMatrix* get_local_operator_and_return_ptr(int ss) const
+  {
+    return new AffinelyDecomposedMatrix(get_local_operator(ss));
+  }
+  AffinelyDecomposedMatrix* get_coupling_operator_and_return_ptr(int ss, int nn) const
+  {
+    return new AffinelyDecomposedMatrix(get_coupling_operator(ss, nn));
+  }
+  AffinelyDecomposedVector* get_local_functional_and_return_ptr(int ss) const
+  {
+    return new AffinelyDecomposedVector(get_local_functional(ss));
+  }
+  // block-swipdg.hh:770-781 / 819-831: `new` discretizations equal to the cached ones (built and initialised the
+  // same way; the reference copy-constructs its discretization, which shares the containers -- SWIPDG owns a
+  // context and is not copyable, so this one is built anew).  (The three-argument pb_get_oversampled_discretization
+  // of block-swipdg.hh:833-846 calls an overload the reference never defines: not provided.)
+  SWIPDG* pb_get_local_discretization(int64_t subdomain) const
+  {
+    if (subdomain < 0 || subdomain > int64_t(std::numeric_limits<int>::max()))
+      throw Stuff::Exceptions::index_out_of_range("There was an error converting " + std::to_string(subdomain) +
+                                                  " to size_t");
+    const int ss = subdomain_check(int(subdomain));
+    return make_local_discretization(ss).release();
+  }
+  SWIPDG* pb_get_oversampled_discretization(int64_t subdomain, const std::string& boundary_value_type) const
+  {
+    if (subdomain < 0 || subdomain > int64_t(std::numeric_limits<int>::max()))
+      throw Stuff::Exceptions::index_out_of_range("There was an error converting " + std::to_string(subdomain) +
+                                                  " to size_t");
+    const int ss = subdomain_check(int(subdomain));
+    boundary_config(boundary_value_type);
+    return make_oversampled_discretization(ss, boundary_value_type).release();
   }
   int oversampling_layers() const { return oversampling_layers_; }
   void set_oversampling_layers(int layers)
@@ -1450,6 +1534,38 @@ class BlockSWIPDG : public SWIPDG {
     local_discretizations_.resize(size_t(info_.n_subdomains));
   }
 
+  int subdomain_check(int ss) const   // (the messages of block-swipdg.hh:763-766, 786-789)
+  {
+    if (ss < 0 || ss >= num_subdomains())
+      throw Stuff::Exceptions::index_out_of_range("Given subdomain " + std::to_string(ss) +
+                                                  " too large (has to be smaller than " +
+                                                  std::to_string(num_subdomains()) + "!");
+    return ss;
+  }
+  static Stuff::Common::Configuration boundary_config(const std::string& boundary_value_type)
+  {
+    if (boundary_value_type == "dirichlet") return Stuff::Grid::BoundaryInfos::AllDirichlet::default_config();
+    if (boundary_value_type == "neumann") return Stuff::Grid::BoundaryInfos::AllNeumann::default_config();
+    throw Stuff::Exceptions::wrong_input_given(
+        "Unknown boundary_value_type given (has to be dirichlet or neumann): " + boundary_value_type);
+  }
+  std::unique_ptr<SWIPDG> make_local_discretization(int ss) const
+  {
+    auto d = std::make_unique<SWIPDG>(grid_, Stuff::Grid::BoundaryInfos::AllNeumann::default_config(),
+                                      Problems::ZeroBoundary(original_problem_), Layer::local, ss, only_these_products_,
+                                      device_);
+    d->init();
+    return d;
+  }
+  std::unique_ptr<SWIPDG> make_oversampled_discretization(int ss, const std::string& boundary_value_type) const
+  {
+    std::vector<int64_t> ids = oversampled_elements(ss);
+    auto d = std::make_unique<SWIPDG>(subset_grid(ids), ids, info_.n_elements, boundary_config(boundary_value_type),
+                                      Problems::ZeroBoundary(original_problem_), only_these_products_, device_);
+    d->init();
+    return d;
+  }
+
   void range_check(int ss) const
   {
     if (ss < 0 || ss >= num_subdomains())
@@ -1465,7 +1581,7 @@ class BlockSWIPDG : public SWIPDG {
     range_check(ss);
     range_check(nn);
     const auto it = operators_.find({ss, nn});
-    if (it != operators_.end()) return it->second;   // extract_operators() ran
+    if (it != operators_.end()) return it->second.clone();   // extract_operators() ran: a copy of its view
     const auto& M = system_matrix();
     int64_t a, b, c, d;
     internal::check(hdd_grid_subdomain_range(grid_, ss, ss + 1, &a, &b), "range");

@@ -171,3 +171,53 @@ def test_rhs_split_equals_fused(et):
         # generic (run-time rule) variant of the split path: per-element force
         kw.update(force=H.scalar_fn(H.FN_PER_ELEM, per_elem=torch.from_numpy(rng.uniform(-1, 1, loc.n_local)).cuda()))
         assert torch.equal(H.rhs(ctxs[0], dm, **kw), H.rhs(ctxs[1], dm, **kw)), n
+
+
+def _rhs_split_case():
+    """a 2d problem whose RHS takes the split path (volume kernel + boundary-element list + face kernel)"""
+    torch = _torch()
+    grid = H.Grid.structured(H.SIMPLEX, 64, 16, (0.0, 0.0), (5.0, 1.0))
+    dm = H.DeviceMesh(grid.local())
+    T = torch.from_numpy(np.random.default_rng(4).uniform(0.5, 2.0, grid.ne)).cuda()
+    kw = dict(force=H.esv2007_force(), kappa=H.scalar_fn(H.FN_CONST, 1.0),
+              tensor=H.tensor_fn(H.TENSOR_ISO_PER_ELEM, per_elem=T),
+              dirichlet=H.scalar_fn(H.FN_SINUSOID, 1.0, b=0.5, kx=1.3, ky=0.7, order=3), prm=H.params())
+    return dm, kw, T
+
+
+def test_rhs_list_survives_failed_face_launch():
+    """The boundary-element list of the split RHS is context state.  If the face launch fails after the volume
+    kernel has filled the list (error injection: hdd_ctx_set_debug_flags bit 524288), the call returns an error
+    and re-arms the list's counters, so the next call on the same context is exact again (bit for bit equal to a
+    fresh context), instead of adding the stale entries' faces a second time."""
+    torch = _torch()
+    dm, kw, _ = _rhs_split_case()
+    ref = H.rhs(H.Context(0), dm, **kw).cpu().numpy()
+    c = H.Context(0)
+    first = H.rhs(c, dm, **kw).cpu().numpy()
+    c.set_debug_flags(524288)
+    with pytest.raises(H.HddError):
+        H.rhs(c, dm, **kw)
+    c.set_debug_flags(0)
+    for _ in range(2):
+        got = H.rhs(c, dm, **kw)
+        torch.cuda.synchronize()
+        assert np.array_equal(got.cpu().numpy(), ref)
+    assert np.array_equal(first, ref)
+
+
+def test_rhs_one_context_two_streams():
+    """Split RHS calls with one context on two streams, back to back without host synchronisation: the context
+    orders a call on a new stream behind the previous call (the list is shared), so every result is exact."""
+    torch = _torch()
+    dm, kw, _ = _rhs_split_case()
+    ref = H.rhs(H.Context(0), dm, **kw).cpu().numpy()
+    c = H.Context(0)
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    outs = [torch.full((ref.size,), float("nan"), dtype=torch.float64, device="cuda") for _ in range(8)]
+    torch.cuda.synchronize()
+    for i, o in enumerate(outs):
+        H.rhs(c, dm, out=o, stream=streams[i % 2].cuda_stream, **kw)
+    torch.cuda.synchronize()
+    for i, o in enumerate(outs):
+        assert np.array_equal(o.cpu().numpy(), ref), i

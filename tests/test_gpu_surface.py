@@ -42,6 +42,8 @@ def test_cpp_surface_against_oracle(surface_run):
     if True:
         assert "roundtrip 1" in r.stdout and "coupling(0,3) rejected" in r.stdout
         assert "batched operators 12 same 1" in r.stdout, r.stdout
+        # the *_and_return_ptr / pb_get_* variants (block-swipdg.hh:602-690, 770-831): equal, own values, deletable
+        assert "caller-owned copies 1" in r.stdout, r.stdout
         assert "rejected: The diffusion tensor must not be parametric!" in r.stdout
         assert "os2014 parametric 1 components 1" in r.stdout
         ld = lambda n, t: np.fromfile(os.path.join(d, n + ".bin"), dtype=t)

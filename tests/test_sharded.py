@@ -210,6 +210,17 @@ def test_cpp_example_thread_ranks():
 
 
 @pytest.mark.gpu
+def test_cpp_example_device_transport_threads():
+    """examples/sharded_main device 3: the same thread ranks through Parallel::Communicator::device (the
+    in-process device transport), i.e. the step's RCCL branch -- transfer stream, fixup on it, event join --
+    with a middle rank, three steps each, bit for bit == single-GPU BlockSWIPDG."""
+    r = subprocess.run([EXAMPLE, "device", "3"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "sharded device-transport threads ok" in r.stdout, r.stdout
+    assert r.stdout.count("mismatches vs single-GPU BlockSWIPDG: 0") == 4, r.stdout
+
+
+@pytest.mark.gpu
 def test_cpp_example_rccl_one_rank():
     """examples/sharded_main rccl: the RCCL communicator created from C++ (unique id through a file)."""
     with tempfile.TemporaryDirectory() as d:
