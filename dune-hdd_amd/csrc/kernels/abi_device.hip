@@ -273,8 +273,13 @@ static int assemble_impl(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_fn* k
     return set_error(HDD_ERR_RANGE, "hdd_swipdg_assemble: 0 <= own_begin <= own_end <= n_local violated");
   if (m->n_local >= int64_t(INT32_MAX))
     return set_error(HDD_ERR_RANGE, "hdd_swipdg_assemble: n_local must fit int32 neighbour ids");
+  // The sharded step (shard.hip) runs this function on two streams at once with one context: the element-list
+  // pass on the transfer stream beside the SKIP launch on the caller's stream.  That is safe only because the
+  // 2d paths below (tiles, element lists, skip_ghost) use no context workspace (ws / scan_ws / rhs_ws); the
+  // one path that does (HDD_HEX, p = 3) takes no lists, and the sharded step runs it exchange-then-assemble.
   if (m->elem_type == HDD_HEX) {
-    if (d_tiles) return set_error(HDD_ERR_UNSUPPORTED, "hdd_swipdg_assemble_tiles: no tile / element lists for HDD_HEX");
+    if (d_tiles || skip_ghost)
+      return set_error(HDD_ERR_UNSUPPORTED, "hdd_swipdg_assemble_tiles: no tile / element lists for HDD_HEX");
     return assemble_hex(ctx, m, kappa, n_comp, tensor, p, pattern, d_vals, stream);
   }
   if (m->degree > 1)

@@ -1151,11 +1151,16 @@ struct GenericPolicy {
 // maximum).  Neighbour quantities are in role coordinates (A = my face vertex a, B = b, C = the
 // neighbour vertex next to A), as in GenericPolicy.
 // ------------------------------------------------------------------------------------------------
-template <int TK, int KK, bool PEN = false, bool VX = false>   // PEN: penalty terms only (the SWIPDG penalty product)
+// PEN: penalty terms only (the SWIPDG penalty product).  H2: half images (see the persistent kernel): the tile's
+// two 32-element halves are computed and streamed in turn through a 20 KB image, so 8 tiles fit per CU and the
+// kernel runs two waves per SIMD (<= 256 registers) instead of one.
+template <int TK, int KK, bool PEN = false, bool VX = false, bool H2 = false>
 struct Q1PwcPolicy : GenericPolicy<Cube, 1, 2, TK, KK, VX> {
   using Base = GenericPolicy<Cube, 1, 2, TK, KK, VX>;
   using E = Cube;
   static constexpr int NB = 4, NF = 4;
+  static constexpr bool HALF = H2;
+  static constexpr int WGCU = H2 ? 8 : 4, MINW = H2 ? 2 : 1;
   using Own = typename Base::Own;
   using Gat = typename Base::Gat;
 
@@ -1738,6 +1743,13 @@ template <class P>
 struct fused_of<P, std::void_t<decltype(P::FUSED)>> : std::bool_constant<P::FUSED> {
   using Shared = typename P::Shared;
 };
+// HALF policies (Q1PwcPolicy<.., H2>) stage a tile through an image of 32 row blocks, one half after the other
+template <class P, class = void>
+struct half_of : std::false_type {};
+template <class P>
+struct half_of<P, std::void_t<decltype(P::HALF)>> : std::bool_constant<P::HALF> {};
+template <class P>
+constexpr int image_blocks() { return half_of<P>::value ? 32 : 64; }
 
 // TL: tiles come from a.tile_list, else 0..n_tiles-1; SKIP: the sharded step's full-range launch, which leaves
 // the row blocks of elements with a ghost face neighbour to the concurrent element pass (a.skip_ghost)
@@ -1746,9 +1758,11 @@ __global__ void __launch_bounds__(64, P::MINW)
 swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
 {
   constexpr bool FUSED = fused_of<P>::value;
+  constexpr bool HALF = half_of<P>::value;
   constexpr int RB = P::RB;
-  constexpr int IMG = 64 * RB;
+  constexpr int IMG = image_blocks<P>() * RB;
   constexpr int STORES = (IMG / 2 + 63) / 64;
+  static_assert(!HALF || (P::PAD && !FUSED && (P::NB * P::NB) % 2 == 0), "half images: padded even-block policies");
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const int lane = threadIdx.x;
   const int64_t G = gridDim.x, b = blockIdx.x;
@@ -1841,6 +1855,85 @@ swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
       gmask = __ballot(active && g);
     }
     const bool uni = P::PAD && tlen == RB * int(a.own_end - t0 < 64 ? a.own_end - t0 : 64);   // wave-uniform
+    typename P::Gat gat_n;
+    if constexpr (HALF) {
+      // Half images: lanes 0-31 build their row blocks in the 20 KB image and the wave streams that CSR range
+      // [base, base + len0) out, then lanes 32-63 theirs, [base + len0, tile_end).  Each half is the row blocks
+      // of 32 consecutive elements, so both ranges are contiguous; with even row blocks (Q1: multiples of 16
+      // values, base even) every range starts and ends on a 16-byte boundary.  The LDS writes of the second
+      // half follow the first half's LDS reads in the wave's in-order LDS queue.
+      constexpr int STH = IMG / 128;   // 16-byte chunks per lane per half
+      const int nact = int(a.own_end - t0 < 64 ? a.own_end - t0 : 64);
+      const int len0 = nact > 32 ? __builtin_amdgcn_readlane(off, 32) : tlen;
+      // sharded step: image ranges of the skipped elements, tile coordinates (as in stores_skip below)
+      constexpr int NR = 4;
+      int rb[NR], re[NR];
+      uint64_t mrest = gmask;
+      const int bo = off, be = off + P::NB * P::NB * (P::n_interior(own) + 1);
+#pragma unroll
+      for (int i = 0; i < NR; ++i) {
+        rb[i] = re[i] = 0;
+        if (SKIP && mrest) {
+          const int l = __builtin_ctzll(mrest);
+          mrest &= mrest - 1;
+          rb[i] = __builtin_amdgcn_readlane(bo, l);
+          re[i] = __builtin_amdgcn_readlane(be, l);
+        }
+      }
+      auto skipped = [&](int d) {
+        bool r = false;
+#pragma unroll
+        for (int i = 0; i < NR; ++i) r |= d >= rb[i] && d < re[i];
+        for (uint64_t mm = mrest; mm; mm &= mm - 1) {
+          const int l = __builtin_ctzll(mm);
+          r |= d >= __builtin_amdgcn_readlane(bo, l) && d < __builtin_amdgcn_readlane(be, l);
+        }
+        return r;
+      };
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int hb = h ? len0 : 0, hl = (h ? tlen : len0) - hb;   // wave-uniform
+        if ((lane >> 5) == h && !HDD_ABL(a, 1)) {
+          const RotImg<RB> img{uni ? lds + (lane & 31) * RB : (active ? lds + (off - hb) : scratch),
+                               uni ? 2 * ((lane >> 1) & 15) : 0};
+          // the two halves' computations are identical code on identical registers: without an opaque copy of
+          // the geometry the compiler evaluates them once and keeps all 80 values live across the first
+          // half's stores (spills)
+          typename P::Own oh = own;
+#pragma unroll
+          for (int k = 0; k < P::NB; ++k) asm volatile("" : "+v"(oh.X[k]), "+v"(oh.Y[k]));
+          P::compute(a, e, oh, gat, img);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (h == 1 && !HDD_ABL(a, 4)) P::load_gat(a, en, own_n, gat_n);   // first gather stage of tile t+1
+        if (hl <= 0) continue;
+        const int nb = HDD_ABL(a, 2) ? 0 : hl * 8;
+        const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc(out + base + hb, (short)0, nb, 0x00020000);
+        if (uni) {
+          const int dmax = hl - 2;
+#pragma unroll
+          for (int k = 0; k < STH; ++k) {
+            const int d = 2 * (lane + 64 * k);
+            const int dd = d <= dmax ? d : 0;
+            const int l = dd / RB, j = dd - l * RB;
+            const int q = j + 2 * ((l >> 1) & 15);
+            const dvec2 v = *reinterpret_cast<const dvec2*>(lds + l * RB + (q < RB ? q : q - RB));
+            const int o8 = SKIP && ((gmask >> (32 * h + l)) & 1) ? nb : d * 8;
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ivec4, v), rh, o8, 0, 2);
+          }
+        } else {
+#pragma unroll
+          for (int k = 0; k < STH; ++k) {
+            const int d = 2 * (lane + 64 * k);
+            const dvec2 v = *reinterpret_cast<const dvec2*>(lds + d);
+            const int o8 = SKIP && gmask && skipped(hb + d) ? nb : d * 8;
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ivec4, v), rh, o8, 0, 2);
+          }
+        }
+      }
+    } else {
     if constexpr (P::PAD) {
       const RotImg<RB> img{uni ? lds + lane * RB : (active ? lds + off : scratch), uni ? 2 * ((lane >> 1) & 15) : 0};
       if (!HDD_ABL(a, 1)) P::compute(a, e, own, gat, img);
@@ -1987,7 +2080,6 @@ swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
       }
     };
     if (ksplit > 0) stores(true);
-    typename P::Gat gat_n;
     if (!HDD_ABL(a, 4)) P::load_gat(a, en, own_n, gat_n);
     stores(false);
     if constexpr (FUSED) {   // the other components: same image slots, their own value arrays
@@ -2003,6 +2095,7 @@ swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
       }
       out = a.vals[0];
     }
+    }   // !HALF
     // second gather stage of tile t+1 (vertex-indexed geometry: the neighbours' off-face vertices by the
     // ids the first stage brought): its wait covers the first stage only, which was issued before the
     // stores of tile t (vmcnt is in order), so it never waits for those stores
@@ -2125,7 +2218,7 @@ static hipError_t launch_persistent(const AssembleArgs& a, hipStream_t s)
   if (n_own <= 0) return hipSuccess;
   const int64_t tiles = a.tile_list ? a.n_tile_list : (n_own + 63) / 64;
   if (tiles <= 0) return hipSuccess;
-  const size_t lds = (P::PAD ? size_t(64) * P::RB : size_t(64) * P::RB + 2 + P::RB) * sizeof(double);
+  const size_t lds = (P::PAD ? size_t(image_blocks<P>()) * P::RB : size_t(64) * P::RB + 2 + P::RB) * sizeof(double);
   const int cus = a.n_cu;
   // tiles per CU measured per policy (profiles/r01/sweep_wg_per_cu.log, profiles/r01/s2/); a.wgcu > 0 is the
   // HDD_P1_WGCU sweep override, read once per context
@@ -2237,6 +2330,7 @@ static hipError_t dispatch_kinds(const AssembleArgs& a, hipStream_t s, bool smoo
 
 template <int TK, int KK, bool VX> using P1Pwc = P1PwcPolicy<TK, KK, false, VX>;
 template <int TK, int KK, bool VX> using Q1Pwc = Q1PwcPolicy<TK, KK, false, VX>;
+template <int TK, int KK, bool VX> using Q1PwcH2 = Q1PwcPolicy<TK, KK, false, VX, true>;
 template <int TK, int KK, bool VX> using Q1Smooth3 = GenericPolicy<Cube, 4, 3, TK, KK, VX>;
 template <int TK, int KK, bool VX> using P1Smooth3 = GenericPolicy<Simplex, 6, 3, TK, KK, VX>;
 

@@ -6,7 +6,11 @@
 namespace hdd {
 namespace dev {
 
-hipError_t launch_q1_pwc(const AssembleArgs& a, hipStream_t s) { return dispatch_kinds<Q1Pwc>(a, s, false); }
+// HDD_DEBUG_FLAGS bit 1048576: the half-image kernel (two waves per SIMD) instead of the whole-tile image
+hipError_t launch_q1_pwc(const AssembleArgs& a, hipStream_t s)
+{
+  return (a.debug_flags & 1048576) ? dispatch_kinds<Q1PwcH2>(a, s, false) : dispatch_kinds<Q1Pwc>(a, s, false);
+}
 hipError_t launch_q1_smooth(const AssembleArgs& a, hipStream_t s) { return dispatch_kinds<Q1Smooth3>(a, s, true); }
 
 template <int TK, int KK> using Q1Pen = Q1PwcPolicy<TK, KK, true>;
