@@ -6,10 +6,13 @@
 namespace hdd {
 namespace dev {
 
-// HDD_DEBUG_FLAGS bit 1048576: the half-image kernel (two waves per SIMD) instead of the whole-tile image
+// HDD_DEBUG_FLAGS bit 1048576: the half-image kernel (two waves per SIMD) instead of the whole-tile image;
+// + bit 2097152: with the vertex-indexed geometry (mesh elem_vertices / vertex_coords)
 hipError_t launch_q1_pwc(const AssembleArgs& a, hipStream_t s)
 {
-  return (a.debug_flags & 1048576) ? dispatch_kinds<Q1PwcH2>(a, s, false) : dispatch_kinds<Q1Pwc>(a, s, false);
+  if (!(a.debug_flags & 1048576)) return dispatch_kinds<Q1Pwc>(a, s, false);
+  if ((a.debug_flags & 2097152) && a.ev) return dispatch_kinds_vx<Q1PwcH2, true>(a, s, false);
+  return dispatch_kinds_vx<Q1PwcH2, false>(a, s, false);
 }
 hipError_t launch_q1_smooth(const AssembleArgs& a, hipStream_t s) { return dispatch_kinds<Q1Smooth3>(a, s, true); }
 

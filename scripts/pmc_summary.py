@@ -30,6 +30,24 @@ def main():
         for c in sorted(vals[k]):
             v = vals[k][c]
             print("| %s | %s | %d | %.4g |" % (short, c, len(v), sum(v) / len(v)))
+    # wave-cycle accounting (MI355X_MICROARCH.md: WAIT_ANY + WAIT_INST_ANY + ACTIVE_INST_ANY ~= WAVE_CYCLES, disjoint;
+    # ACTIVE_INST_* by instruction class may overlap each other)
+    for k in sorted(vals):
+        if want and not any(w in k for w in want):
+            continue
+        m = {c: sum(v) / len(v) for c, v in vals[k].items()}
+        wc = m.get("SQ_WAVE_CYCLES")
+        if not wc or not all(c in m for c in ("SQ_ACTIVE_INST_ANY", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY")):
+            continue
+        print("\nwave-cycle accounting, %s (SQ_WAVE_CYCLES %.4g per dispatch):" % (k.split("(")[0], wc))
+        parts = ("SQ_ACTIVE_INST_ANY", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY")
+        for c in parts:
+            print("  %-22s %6.1f %%" % (c, 100 * m[c] / wc))
+        print("  %-22s %6.1f %%" % ("sum", 100 * sum(m[c] for c in parts) / wc))
+        for c in ("SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_LDS", "SQ_ACTIVE_INST_VMEM", "SQ_ACTIVE_INST_SCA",
+                  "SQ_ACTIVE_INST_MISC", "SQ_ACTIVE_INST_FLAT", "SQ_WAIT_INST_LDS"):
+            if c in m:
+                print("    %-20s %6.1f %%" % (c, 100 * m[c] / wc))
     for path in sorted(glob.glob(os.path.join(root, "**", "*kernel_stats.csv"), recursive=True)):
         print("\nkernel stats: %s" % os.path.relpath(path, root))
         with open(path) as f:

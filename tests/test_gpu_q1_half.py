@@ -18,13 +18,15 @@ H = pytest.importorskip("hdd_amd")
 pytestmark = pytest.mark.gpu
 
 HALF = 1048576   # HDD_DEBUG_FLAGS bit selecting the half-image kernel (swipdg_q1.hip)
+VXQ = 2097152    # + the vertex-indexed geometry for quads
 
 
-def _both(ctx, fn):
-    """fn() under the whole-tile and the half-image kernel -> (whole, half) numpy arrays"""
+def _all(ctx, fn):
+    """fn() under the whole-tile kernel, the half-image kernel and the half-image kernel on vertex-indexed
+    geometry -> [whole, half, half_vx]"""
     import torch
     out = []
-    for flags in (0, HALF):
+    for flags in (0, HALF, HALF | VXQ):
         ctx.set_debug_flags(flags)
         try:
             r = fn()
@@ -59,8 +61,9 @@ def test_half_image_equals_whole_tile(ctx, tk, bnd, kpe):
     kf = [H.scalar_fn(H.FN_PER_ELEM, per_elem=torch.from_numpy(np.ascontiguousarray(kap[idx])).cuda())
           if kpe else H.scalar_fn(H.FN_CONST, 1.7)]
     dm, dp = H.DeviceMesh(loc), H.DevicePattern(loc)
-    whole, half = _both(ctx, lambda: H.assemble(ctx, dm, dp, kf, ten)[0].cpu().numpy())
+    whole, half, half_vx = _all(ctx, lambda: H.assemble(ctx, dm, dp, kf, ten)[0].cpu().numpy())
     assert np.array_equal(_bits(whole), _bits(half))
+    assert np.array_equal(_bits(whole), _bits(half_vx))
     pc, pev, _ = grid.connectivity()
     og = O.Grid(O.cube_grid(1, 1, (0, 0), (1, 1))[0], pc, pev)
     okind = O.TENSOR_SYM_PER_ELEM if tk == "sym" else O.TENSOR_ISO_PER_ELEM
@@ -82,9 +85,10 @@ def test_half_image_edge_meshes(ctx, nx, ny):
     k = torch.from_numpy(loc.checkerboard(SPE10_LOWER, SPE10_UPPER, 100, 20, perm)).cuda()
     dm, dp = H.DeviceMesh(loc), H.DevicePattern(loc)
     kf, ten = [H.scalar_fn(H.FN_CONST, 1.0)], H.tensor_fn(H.TENSOR_ISO_PER_ELEM, per_elem=k)
-    whole, half = _both(ctx, lambda: H.assemble(ctx, dm, dp, kf, ten)[0].cpu().numpy())
+    whole, half, half_vx = _all(ctx, lambda: H.assemble(ctx, dm, dp, kf, ten)[0].cpu().numpy())
     assert np.isfinite(half).all()
     assert np.array_equal(_bits(whole), _bits(half))
+    assert np.array_equal(_bits(whole), _bits(half_vx))
 
 
 @pytest.mark.parametrize("kind", ["parallelogram", "scrambled"])
@@ -101,8 +105,9 @@ def test_half_image_general_quads(ctx, kind):
     k = torch.from_numpy(np.ascontiguousarray(10.0 ** np.sin(7 * x + 3 * y))).cuda()
     dm, dp = H.DeviceMesh(loc), H.DevicePattern(loc)
     kf, ten = [H.scalar_fn(H.FN_CONST, 1.0)], H.tensor_fn(H.TENSOR_ISO_PER_ELEM, per_elem=k)
-    whole, half = _both(ctx, lambda: H.assemble(ctx, dm, dp, kf, ten)[0].cpu().numpy())
+    whole, half, half_vx = _all(ctx, lambda: H.assemble(ctx, dm, dp, kf, ten)[0].cpu().numpy())
     assert np.array_equal(_bits(whole), _bits(half))
+    assert np.array_equal(_bits(whole), _bits(half_vx))
 
 
 def test_half_image_tile_lists_and_element_fixup(ctx):
@@ -117,18 +122,23 @@ def test_half_image_tile_lists_and_element_fixup(ctx):
     ref = H.assemble(ctx, dm, dp, kf, ten)[0]
     t_in, t_bd = H.halo_tiles(local)
     fix = np.random.default_rng(4).permutation(H.halo_elements(local)).astype(np.int32)
-    ctx.set_debug_flags(HALF)
+    ctx.set_debug_flags(HALF | VXQ)
     try:
         v = torch.full_like(ref, float("nan"))
         for tl in (t_in, t_bd):
             H.assemble_tiles(ctx, dm, dp, kf, ten, torch.from_numpy(tl).cuda(), [v])
         w = torch.full_like(ref, float("nan"))
-        saved = dm.coords.clone()
+        saved, saved_v = dm.coords.clone(), dm.vertex_coords.clone()
         ghosts = torch.ones(local.n_local, dtype=torch.bool, device="cuda")
         ghosts[local.own_begin:local.own_end] = False
         dm.coords[:, ghosts] = float("nan")
+        ev = dm.elem_vertices.cpu().numpy()
+        own_v = np.zeros(dm.vertex_coords.shape[0], bool)
+        own_v[ev[:, local.own_begin:local.own_end].ravel()] = True
+        dm.vertex_coords[torch.from_numpy(~own_v).cuda()] = float("nan")
         H.assemble(ctx, dm, dp, kf, ten, vals=[w])
         dm.coords.copy_(saved)
+        dm.vertex_coords.copy_(saved_v)
         H.assemble_tiles(ctx, dm, dp, kf, ten, torch.from_numpy(fix).cuda(), [w], elements=True)
         torch.cuda.synchronize()
     finally:
