@@ -25,6 +25,8 @@ int hdd_scatter_fix(hdd_ctx* ctx, const hdd_csr* pattern, int32_t rb, double* co
 int hdd_assemble_elements_inplace(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_fn* kappa, int32_t n_comp,
                                   const hdd_tensor_fn* tensor, const hdd_swipdg_params* p, const hdd_csr* pattern,
                                   double* const* d_vals, const int32_t* d_elems, int64_t n_elems, void* stream);
+// reserve_wg: workgroups of the concurrent element pass (in-place fixup) -- the persistent launch leaves that many
+// slots free when its own tiles would fill the CUs (launch_persistent)
 int hdd_assemble_skip_ghost(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_fn* kappa, int32_t n_comp,
                             const hdd_tensor_fn* tensor, const hdd_swipdg_params* p, const hdd_csr* pattern,
-                            double* const* d_vals, void* stream);
+                            double* const* d_vals, void* stream, int32_t reserve_wg = 0);

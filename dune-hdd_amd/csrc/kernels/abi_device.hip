@@ -258,7 +258,7 @@ static int assemble_hex(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_fn* ka
 static int assemble_impl(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_fn* kappa, int32_t n_comp,
                          const hdd_tensor_fn* tensor, const hdd_swipdg_params* p, const hdd_csr* pattern,
                          double* const* d_vals, const int32_t* d_tiles, int64_t n_tiles, void* stream,
-                         int list_elements = 0, bool skip_ghost = false)
+                         int list_elements = 0, bool skip_ghost = false, int32_t reserve_wg = 0)
 {
   using namespace hdd::dev;
   if (!ctx || !m || !kappa || !tensor || !p || !pattern || !d_vals)
@@ -316,6 +316,7 @@ static int assemble_impl(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_fn* k
   a.n_tile_list = n_tiles;
   a.list_elements = list_elements;
   a.skip_ghost = skip_ghost ? 1 : 0;
+  a.reserve_wg = skip_ghost ? reserve_wg : 0;
   a.fix_rb = (m->elem_type == HDD_SIMPLEX ? 3 * 3 * 4 : 4 * 4 * 5);
   if (!m->elem_vertices != !m->vertex_coords)
     return set_error(HDD_ERR_INVALID, "hdd_swipdg_assemble: mesh elem_vertices / vertex_coords: both or neither");
@@ -423,9 +424,9 @@ int hdd_assemble_elements_inplace(hdd_ctx* ctx, const hdd_mesh* m, const hdd_sca
 
 int hdd_assemble_skip_ghost(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_fn* kappa, int32_t n_comp,
                             const hdd_tensor_fn* tensor, const hdd_swipdg_params* p, const hdd_csr* pattern,
-                            double* const* d_vals, void* stream)
+                            double* const* d_vals, void* stream, int32_t reserve_wg)
 {
-  return assemble_impl(ctx, m, kappa, n_comp, tensor, p, pattern, d_vals, nullptr, 0, stream, 0, true);
+  return assemble_impl(ctx, m, kappa, n_comp, tensor, p, pattern, d_vals, nullptr, 0, stream, 0, true, reserve_wg);
 }
 
 int hdd_scatter_fix(hdd_ctx* ctx, const hdd_csr* pattern, int32_t rb, double* const* d_bufs, int32_t n_comp,

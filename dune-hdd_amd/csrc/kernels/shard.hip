@@ -1043,7 +1043,8 @@ extern "C" int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm*
     const bool skip = fix_pending && !scatter && !fix_unsupported;
     rc = split ? hdd_swipdg_assemble_tiles(ctx, &m, kappa, n_comp, tensor, params, pattern, d_vals, sh->d_tiles_in,
                                            sh->n_in, stream)
-         : skip ? hdd_assemble_skip_ghost(ctx, &m, kappa, n_comp, tensor, params, pattern, d_vals, stream)
+         : skip ? hdd_assemble_skip_ghost(ctx, &m, kappa, n_comp, tensor, params, pattern, d_vals, stream,
+                                          int32_t(std::min<int64_t>((sh->n_fix + 63) / 64, 256)))
                 : hdd_swipdg_assemble(ctx, &m, kappa, n_comp, tensor, params, pattern, d_vals, stream);
     if (rc == HDD_ERR_UNSUPPORTED && split) overlap = false;   // no tile-list kernel: everything after the halo
     else if (rc) {

@@ -37,7 +37,8 @@ struct AssembleArgs {
                                // 2: the same, row blocks into side buffers vals[c] of fix_rb doubles per element;
                                // 3: the same, in place without LDS (beside a skip_ghost assembly)
   int32_t fix_rb;
-  int32_t skip_ghost, pad_sg;  // 1: tiles do not store the row blocks of elements with a ghost face neighbour
+  int32_t skip_ghost;          // 1: tiles do not store the row blocks of elements with a ghost face neighbour
+  int32_t reserve_wg;          // skip_ghost launches: workgroup slots left free for the concurrent element pass
   const int32_t* ev;           // optional vertex-indexed geometry: element -> local vertex ids [nvpe][n_local]
   const double* vxy;           //   and the vertex coordinates [n_vertices][2] (hdd_mesh elem_vertices / vertex_coords)
   KappaArg kappa[HDD_MAX_COMP];

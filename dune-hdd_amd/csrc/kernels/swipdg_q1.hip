@@ -6,13 +6,18 @@
 namespace hdd {
 namespace dev {
 
-// HDD_DEBUG_FLAGS bit 1048576: the half-image kernel (two waves per SIMD) instead of the whole-tile image;
-// + bit 2097152: with the vertex-indexed geometry (mesh elem_vertices / vertex_coords)
+// The C1 / C4 kernel.  With the mesh's vertex-indexed geometry: the half-image kernel (two waves per SIMD, 20 KB
+// image) -- C4 0.547-0.555 ms against 0.595-0.599 for the whole-tile image on element-major coords, same box
+// (profiles/r04/b_sweep/).  The two waves per SIMD hide the second gather stage that made vertex-indexed
+// geometry lose at one wave per SIMD (0.600 -> 0.690 ms, round 2).  Element-major meshes keep the whole-tile
+// kernel (the half-image kernel on element-major coords measured 0.630 ms).
+// A/B switches (HDD_DEBUG_FLAGS): 1048576 = the whole-tile kernel always, 2097152 = the half-image kernel on
+// element-major coords.
 hipError_t launch_q1_pwc(const AssembleArgs& a, hipStream_t s)
 {
-  if (!(a.debug_flags & 1048576)) return dispatch_kinds<Q1Pwc>(a, s, false);
-  if ((a.debug_flags & 2097152) && a.ev) return dispatch_kinds_vx<Q1PwcH2, true>(a, s, false);
-  return dispatch_kinds_vx<Q1PwcH2, false>(a, s, false);
+  if (a.debug_flags & 2097152) return dispatch_kinds_vx<Q1PwcH2, false>(a, s, false);
+  if (a.ev && !(a.debug_flags & 1048576)) return dispatch_kinds_vx<Q1PwcH2, true>(a, s, false);
+  return dispatch_kinds_vx<Q1Pwc, false>(a, s, false);
 }
 hipError_t launch_q1_smooth(const AssembleArgs& a, hipStream_t s) { return dispatch_kinds<Q1Smooth3>(a, s, true); }
 

@@ -1,5 +1,6 @@
 """Q1 half-image kernel (Q1PwcPolicy<.., H2>: the tile's two 32-element halves staged in turn through a 20 KB
-LDS image, two waves per SIMD) == the whole-tile image kernel, bit for bit.
+LDS image, two waves per SIMD; the default on vertex-indexed meshes) == the whole-tile image kernel, bit for bit,
+on vertex-indexed and on element-major geometry.
 
 The two kernels run the same closed-form arithmetic (swipdg_device.hh, Q1PwcPolicy::compute) and differ only in
 how a tile's row blocks reach HBM, so every value must be identical -- uniform, non-uniform and ragged tiles,
@@ -17,8 +18,9 @@ from mesh_tools import affine_quad_mesh, scrambled_quad_mesh
 H = pytest.importorskip("hdd_amd")
 pytestmark = pytest.mark.gpu
 
-HALF = 1048576   # HDD_DEBUG_FLAGS bit selecting the half-image kernel (swipdg_q1.hip)
-VXQ = 2097152    # + the vertex-indexed geometry for quads
+# HDD_DEBUG_FLAGS (swipdg_q1.hip): the default on vertex-indexed meshes is the half-image kernel
+WHOLE = 1048576     # the whole-tile image kernel (round 3's default)
+HALF_EM = 2097152   # the half-image kernel on element-major coordinates
 
 
 def _all(ctx, fn):
@@ -26,7 +28,7 @@ def _all(ctx, fn):
     geometry -> [whole, half, half_vx]"""
     import torch
     out = []
-    for flags in (0, HALF, HALF | VXQ):
+    for flags in (WHOLE, HALF_EM, 0):
         ctx.set_debug_flags(flags)
         try:
             r = fn()
@@ -119,10 +121,11 @@ def test_half_image_tile_lists_and_element_fixup(ctx):
     dm, dp = H.DeviceMesh(local), H.DevicePattern(local)
     k = torch.from_numpy(local.checkerboard((0, 0), (4, 1), 100, 20, O.spe10_synthetic_permeability())).cuda()
     kf, ten = [H.scalar_fn(H.FN_CONST, 1.0)], H.tensor_fn(H.TENSOR_ISO_PER_ELEM, per_elem=k)
+    ctx.set_debug_flags(WHOLE)
     ref = H.assemble(ctx, dm, dp, kf, ten)[0]
     t_in, t_bd = H.halo_tiles(local)
     fix = np.random.default_rng(4).permutation(H.halo_elements(local)).astype(np.int32)
-    ctx.set_debug_flags(HALF | VXQ)
+    ctx.set_debug_flags(0)
     try:
         v = torch.full_like(ref, float("nan"))
         for tl in (t_in, t_bd):
