@@ -2224,13 +2224,12 @@ static hipError_t launch_persistent(const AssembleArgs& a, hipStream_t s)
   // HDD_P1_WGCU sweep override, read once per context
   int wgcu = a.wgcu > 0 ? a.wgcu : P::WGCU;
   wgcu = std::max(1, std::min<int>(wgcu, int((160 * 1024) / lds)));   // resident by LDS (Q1 tiles: 3 per CU)
-  // The sharded step's full-range launch (skip_ghost) runs beside the in-place element pass.  A policy that fills
-  // every SIMD (HALF: 2 x 256 registers) would leave that pass no slot until its own waves retire, so the grid is
-  // shortened by the pass's workgroups, a multiple of 8 to keep the XCD eighths even (HDD_DEBUG_FLAGS 4194304:
-  // never; 8388608: for every policy).
+  // The sharded step's full-range launch (skip_ghost) runs beside the in-place element pass: the grid is shortened
+  // by the pass's workgroups (a multiple of 8 keeps the XCD eighths even), so the pass gets SIMDs of its own
+  // instead of slowing the persistent waves it would share them with.  C4 N = 8 middle rank +9.2 -> +7.8 %, C2 N = 8
+  // end rank +4.9 -> +2.0 % over one launch (profiles/r04/e_reserve/; HDD_DEBUG_FLAGS 4194304: no reserve).
   int64_t slots = int64_t(cus) * wgcu;
-  const bool reserve = a.skip_ghost && a.reserve_wg > 0 && !(a.debug_flags & 4194304) &&
-                       (half_of<P>::value || (a.debug_flags & 8388608));
+  const bool reserve = a.skip_ghost && a.reserve_wg > 0 && !(a.debug_flags & 4194304);
   if (reserve) slots = std::max<int64_t>(8, (slots - a.reserve_wg) & ~int64_t(7));
   const int64_t G = std::min<int64_t>(tiles, slots);
   const int n_launch = fused_of<P>::value ? 1 : a.n_comp;   // a FUSED policy emits every component per tile

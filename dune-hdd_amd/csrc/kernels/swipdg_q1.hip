@@ -13,10 +13,14 @@ namespace dev {
 // kernel (the half-image kernel on element-major coords measured 0.630 ms).
 // A/B switches (HDD_DEBUG_FLAGS): 1048576 = the whole-tile kernel always, 2097152 = the half-image kernel on
 // element-major coords.
+// The sharded step's full-range launch (skip_ghost) keeps the whole-tile kernel: beside the in-place element pass
+// it costs +10 % over one launch at C4 N = 8 against +22 % for the half-image kernel, whose waves fill every SIMD
+// (profiles/r04/c_shard/; bit 16777216 selects the half-image kernel there too).
 hipError_t launch_q1_pwc(const AssembleArgs& a, hipStream_t s)
 {
   if (a.debug_flags & 2097152) return dispatch_kinds_vx<Q1PwcH2, false>(a, s, false);
-  if (a.ev && !(a.debug_flags & 1048576)) return dispatch_kinds_vx<Q1PwcH2, true>(a, s, false);
+  const bool half = a.ev && !(a.debug_flags & 1048576) && (!a.skip_ghost || (a.debug_flags & 16777216));
+  if (half) return dispatch_kinds_vx<Q1PwcH2, true>(a, s, false);
   return dispatch_kinds_vx<Q1Pwc, false>(a, s, false);
 }
 hipError_t launch_q1_smooth(const AssembleArgs& a, hipStream_t s) { return dispatch_kinds<Q1Smooth3>(a, s, true); }
