@@ -47,7 +47,7 @@ def parse():
     ap.add_argument("--ny", type=int, default=0, help="c2: 640; c4: 1200")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU work of the baseline sample")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r03", "traffic.json"),
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r04", "traffic.json"),
                     help="PMC traffic summary (scripts/traffic_summary.py); used only when its build_id matches the "
                          "timed libhdd_amd.so")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
