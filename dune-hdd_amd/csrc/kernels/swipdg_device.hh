@@ -1767,6 +1767,7 @@ swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
   const int lane = threadIdx.x;
   const int64_t G = gridDim.x, b = blockIdx.x;
   int64_t t, t_end, t_step;
+  int64_t rs0 = 0, rlen = 0, rot = 0;   // (study: rotated XCD sweeps)
   if (G >= n_tiles) {
     t = b; t_end = b + 1; t_step = 1;
   } else {   // XCD-aware: the 8 XCDs sweep contiguous eighths of the tile range
@@ -1782,6 +1783,11 @@ swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
       t = s0 + w;
       t_end = s1;
       t_step = gx;
+      if (a.debug_flags & 67108864) {   // study: XCD x starts its sweep x/8 into its eighth (and wraps)
+        rs0 = s0;
+        rlen = s1 - s0;
+        rot = (rlen * x) / 8;
+      }
     }
   }
   if (t >= t_end) return;
@@ -1794,6 +1800,10 @@ swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
   // Tile list (interior / halo-boundary split of a sharded assembly): position -> tile.
   auto tile_raw = [&](int64_t pos) -> int64_t {
     if constexpr (TL) return int64_t(a.tile_list[pos]);
+    if (rot) {
+      const int64_t q = pos - rs0 + rot;
+      return rs0 + (q < rlen ? q : q - rlen);
+    }
     return pos;
   };
   auto uni64 = [](int64_t v) -> int64_t { return __builtin_amdgcn_readfirstlane(v); };

@@ -1,7 +1,7 @@
 """C4-type Q1 assemblies (SPE10 checkerboard, 8 x 8 subdomains, one launch) of growing size under several
 HDD_DEBUG_FLAGS kernel selections, interleaved rounds in one process -- where the half-image kernel on vertex-indexed
 geometry (default) and the whole-tile kernel on element-major coords (1048576) cross over.
-usage: python scripts/study/q1_size_sweep.py [flags ...]     (default: 0 1048576 2097152)"""
+usage: python scripts/study/q1_size_sweep.py [--sizes NXxNY,...] [flags ...]     (default flags: 0 1048576 2097152)"""
 import os
 import sys
 
@@ -14,14 +14,19 @@ import hdd_amd as H  # noqa: E402
 
 
 def main():
-    flags = [int(f) for f in sys.argv[1:]] or [0, 1048576, 2097152]
+    args = sys.argv[1:]
+    sizes = [(440, 1200), (880, 1200), (1760, 1200), (3520, 1200), (3520, 2400)]
+    if args and args[0] == "--sizes":
+        sizes = [tuple(int(v) for v in z.split("x")) for z in args[1].split(",")]
+        args = args[2:]
+    flags = [int(f) for f in args] or [0, 1048576, 2097152]
     ctxs = {}
     for f in flags:
         os.environ["HDD_DEBUG_FLAGS"] = str(f)
         ctxs[f] = H.Context(0)
     os.environ["HDD_DEBUG_FLAGS"] = "0"
     perm = 10.0 ** np.random.default_rng(10).uniform(-3, 3, 2000)
-    for nx, ny in [(440, 1200), (880, 1200), (1760, 1200), (3520, 1200), (3520, 2400)]:
+    for nx, ny in sizes:
         grid = H.Grid.structured(H.CUBE, nx, ny, (0, 0), (5.0 * nx / 3520, 1.0 * ny / 1200), px=8, py=8)
         loc = grid.local()
         dm, dp = H.DeviceMesh(loc), H.DevicePattern(loc)
