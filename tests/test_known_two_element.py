@@ -85,7 +85,8 @@ def expected_rows(basis, vx0, vx1, face, a0, a1, k0, k1, sigma=8.0, beta=1.0, we
     c0 = np.mean(np.asarray(vx0, float), axis=0)
     if np.dot(n, (A + B) / 2 - c0) < 0:
         n = -n   # from element 0 outwards
-    dm, dp = a0, a1   # n^T A n for isotropic tensors
+    A0, A1 = (np.asarray(a, float) * (np.eye(2) if np.ndim(a) == 0 else 1.0) for a in (a0, a1))
+    dm, dp = n @ A0 @ n, n @ A1 @ n
     if weights == "swip":
         wm, wp, gam = dp / (dp + dm), dm / (dp + dm), dp * dm / (dp + dm)
     elif weights == "swapped":
@@ -95,7 +96,7 @@ def expected_rows(basis, vx0, vx1, face, a0, a1, k0, k1, sigma=8.0, beta=1.0, we
     elif weights == "arith_gamma":
         wm, wp, gam = dp / (dp + dm), dm / (dp + dm), 0.5 * (dp + dm)
     elif weights == "kappa_in_weights":
-        dm, dp = k0 * a0, k1 * a1
+        dm, dp = k0 * dm, k1 * dp
         wm, wp, gam = dp / (dp + dm), dm / (dp + dm), dp * dm / (dp + dm) / (k0 * k1)
     pen = sigma * k0 * k1 * gam / L ** beta
     S = np.zeros((nb, nb))
@@ -103,17 +104,17 @@ def expected_rows(basis, vx0, vx1, face, a0, a1, k0, k1, sigma=8.0, beta=1.0, we
     for x, w in zip(vq, vw):
         for i in range(nb):
             for j in range(nb):
-                S[i, j] += w * area0 * k0 * a0 * np.dot(grad0(j, x), grad0(i, x))
+                S[i, j] += w * area0 * k0 * np.dot(A0 @ grad0(j, x), grad0(i, x))
     for s, w in G2:
         x = A + s * t
         for i in range(nb):
-            vi, fi = phi0(i, x), k0 * a0 * np.dot(grad0(i, x), n)   # v-, kappa A grad v- . n
+            vi, fi = phi0(i, x), k0 * np.dot(A0 @ grad0(i, x), n)   # v-, kappa A grad v- . n
             for j in range(nb):
                 # u = phi0_j (element 0): [u] = u-, {kAgrad u}_w.n = w- k0 a0 grad u- . n
-                uj, fj = phi0(j, x), k0 * a0 * np.dot(grad0(j, x), n)
+                uj, fj = phi0(j, x), k0 * np.dot(A0 @ grad0(j, x), n)
                 S[i, j] += w * L * (-wm * fj * vi - uj * wm * fi + pen * uj * vi)
                 # u = phi1_j (element 1): [u] = -u+, {kAgrad u}_w.n = w+ k1 a1 grad u+ . n
-                uj1, fj1 = phi1(j, x), k1 * a1 * np.dot(grad1(j, x), n)
+                uj1, fj1 = phi1(j, x), k1 * np.dot(A1 @ grad1(j, x), n)
                 C[i, j] += w * L * (-wp * fj1 * vi - (-uj1) * wm * fi + pen * (-uj1) * vi)
     return S, C
 
@@ -127,6 +128,12 @@ CASES = {
                             ((1, 0), (1, 0.5)), 3.0, 0.2, 2.0, 7.0),
     # P1: the unit square cut along its diagonal, tensor jump 0.01 : 50
     "p1_tensor_jump": ("p1", [(0, 0), (1, 0), (0, 1)], [(1, 0), (1, 1), (0, 1)], ((1, 0), (0, 1)), 0.01, 50.0, 1.0, 1.0),
+    # sheared Q1 parallelograms (face not axis-aligned), anisotropic symmetric tensors, kappa jump
+    "q1_sym_sheared": ("q1", [(0, 0), (1, 0.2), (0.3, 0.7), (1.3, 0.9)], [(1, 0.2), (2, 0.4), (1.3, 0.9), (2.3, 1.1)],
+                       ((1, 0.2), (1.3, 0.9)), [[2.0, 0.7], [0.7, 1.5]], [[0.05, -0.02], [-0.02, 0.3]], 1.5, 0.4),
+    # P1 with anisotropic symmetric tensors on a skewed pair
+    "p1_sym": ("p1", [(0, 0), (1.1, 0.1), (0.2, 0.9)], [(1.1, 0.1), (1.4, 1.2), (0.2, 0.9)], ((1.1, 0.1), (0.2, 0.9)),
+               [[4.0, 1.0], [1.0, 0.8]], [[0.3, 0.1], [0.1, 0.09]], 1.0, 3.0),
 }
 
 
@@ -141,10 +148,19 @@ def _case(name):
     return et, basis, vx0, vx1, face, a0, a1, k0, k1, uniq, ev
 
 
+def _sym(a):
+    """per-element symmetric tensor rows (a00, a01, a11) of the two elements, or None for isotropic ones"""
+    if np.ndim(a[0]) == 0:
+        return None
+    return np.array([[m[0][0], m[0][1], m[1][1]] for m in a], float)   # [element][3]
+
+
 def _oracle_rows(et, coords, ev, a, k):
     g = O.Grid(O.SIMPLEX if et == "p1" else O.CUBE, np.ascontiguousarray(coords), np.ascontiguousarray(ev))
-    rp, col, val = O.assemble(g, O.scalar(O.FN_PER_ELEM, per_elem=np.asarray(k, float)),
-                              O.tensor(O.TENSOR_ISO_PER_ELEM, per_elem=np.asarray(a, float)),
+    sym = _sym(a)
+    ten = (O.tensor(O.TENSOR_ISO_PER_ELEM, per_elem=np.asarray(a, float)) if sym is None
+           else O.tensor(O.TENSOR_SYM_PER_ELEM, per_elem=np.ascontiguousarray(sym)))
+    rp, col, val = O.assemble(g, O.scalar(O.FN_PER_ELEM, per_elem=np.asarray(k, float)), ten,
                               O.params(O.BOUNDARY_NEUMANN))
     return rp, col, val
 
@@ -187,11 +203,15 @@ def test_gpu_equals_published_form(ctx, name):
                                     boundary=H.BOUNDARY_ALL_NEUMANN)
     loc = grid.local()
     gid = loc.global_id
-    a = torch.from_numpy(np.ascontiguousarray(np.array([a0, a1])[gid])).cuda()
+    sym = _sym([a0, a1])
+    if sym is None:
+        ten = H.tensor_fn(H.TENSOR_ISO_PER_ELEM,
+                          per_elem=torch.from_numpy(np.ascontiguousarray(np.array([a0, a1])[gid])).cuda())
+    else:   # the device layout is [3][n]
+        ten = H.tensor_fn(H.TENSOR_SYM_PER_ELEM, per_elem=torch.from_numpy(np.ascontiguousarray(sym[gid].T)).cuda())
     k = torch.from_numpy(np.ascontiguousarray(np.array([k0, k1])[gid])).cuda()
     dm, dp = H.DeviceMesh(loc), H.DevicePattern(loc)
-    (val,) = H.assemble(ctx, dm, dp, [H.scalar_fn(H.FN_PER_ELEM, per_elem=k)],
-                        H.tensor_fn(H.TENSOR_ISO_PER_ELEM, per_elem=a))
+    (val,) = H.assemble(ctx, dm, dp, [H.scalar_fn(H.FN_PER_ELEM, per_elem=k)], ten)
     torch.cuda.synchronize()
     rp, col, _ = dp.host
     nb = 4 if et == "q1" else 3
