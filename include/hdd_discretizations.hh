@@ -1322,8 +1322,21 @@ class BlockSWIPDG : public SWIPDG {
     auto rp = std::make_shared<internal::DeviceArray<int64_t>>(size_t(roff.back()));
     auto col = std::make_shared<internal::DeviceArray<int32_t>>(size_t(noff.back()) + 1);
     const hdd_csr pat = pattern_->csr();
+#ifdef NDEBUG
+    // release builds stay asynchronous: the counts from the face pairs are trusted (the tests below check them)
     internal::check(hdd_block_operators_map_device(ctx_, &pat, n_ops, rng.data(), rp->get(), col->get(), nullptr,
                                                    nullptr, nullptr), "hdd_block_operators_map_device");
+#else
+    // debug builds (and the test programs, built without NDEBUG): the device returns the operators' offsets from
+    // the pattern itself, which must equal the face-pair counts the arrays above were sized with
+    std::vector<int64_t> dev_off(size_t(n_ops) + 1);
+    internal::check(hdd_block_operators_map_device(ctx_, &pat, n_ops, rng.data(), rp->get(), col->get(), nullptr,
+                                                   dev_off.data(), nullptr), "hdd_block_operators_map_device");
+    for (int32_t k = 0; k <= n_ops; ++k)
+      if (dev_off[size_t(k)] != noff[size_t(k)])
+        throw std::runtime_error("BlockSWIPDG::extract_operators: the pattern's operator sizes differ from the face-pair "
+                                 "counts (operator " + std::to_string(k) + ")");
+#endif
     std::vector<std::shared_ptr<internal::DeviceArray<double>>> all;   // affine first, then the components
     std::vector<const double*> in;
     std::vector<double*> res;
