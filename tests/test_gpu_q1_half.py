@@ -21,7 +21,7 @@ pytestmark = pytest.mark.gpu
 # HDD_DEBUG_FLAGS (swipdg_q1.hip): the default on vertex-indexed meshes is the half-image kernel
 WHOLE = 1048576     # the whole-tile image kernel (round 3's default)
 HALF_EM = 2097152   # the half-image kernel on element-major coordinates
-PAIRS = 134217728   # the half-image kernel's pair-lane compute (study)
+PAIRS = 134217728   # the half-image kernel's pair-lane compute (study; equal up to rounding)
 
 
 def _all(ctx, fn):
@@ -67,7 +67,9 @@ def test_half_image_equals_whole_tile(ctx, tk, bnd, kpe):
     whole, half, half_vx, pairs = _all(ctx, lambda: H.assemble(ctx, dm, dp, kf, ten)[0].cpu().numpy())
     assert np.array_equal(_bits(whole), _bits(half))
     assert np.array_equal(_bits(whole), _bits(half_vx))
-    assert np.array_equal(_bits(whole), _bits(pairs))
+    # the pair-lane compute evaluates the row-dependent constants at run time, so its fused multiply-adds contract
+    # differently: equal up to rounding, not bit for bit
+    assert np.abs(pairs - whole).max() <= 1e-13 * np.abs(whole).max()
     pc, pev, _ = grid.connectivity()
     og = O.Grid(O.cube_grid(1, 1, (0, 0), (1, 1))[0], pc, pev)
     okind = O.TENSOR_SYM_PER_ELEM if tk == "sym" else O.TENSOR_ISO_PER_ELEM
@@ -93,7 +95,9 @@ def test_half_image_edge_meshes(ctx, nx, ny):
     assert np.isfinite(half).all()
     assert np.array_equal(_bits(whole), _bits(half))
     assert np.array_equal(_bits(whole), _bits(half_vx))
-    assert np.array_equal(_bits(whole), _bits(pairs))
+    # the pair-lane compute evaluates the row-dependent constants at run time, so its fused multiply-adds contract
+    # differently: equal up to rounding, not bit for bit
+    assert np.abs(pairs - whole).max() <= 1e-13 * np.abs(whole).max()
 
 
 @pytest.mark.parametrize("kind", ["parallelogram", "scrambled"])
@@ -113,7 +117,9 @@ def test_half_image_general_quads(ctx, kind):
     whole, half, half_vx, pairs = _all(ctx, lambda: H.assemble(ctx, dm, dp, kf, ten)[0].cpu().numpy())
     assert np.array_equal(_bits(whole), _bits(half))
     assert np.array_equal(_bits(whole), _bits(half_vx))
-    assert np.array_equal(_bits(whole), _bits(pairs))
+    # the pair-lane compute evaluates the row-dependent constants at run time, so its fused multiply-adds contract
+    # differently: equal up to rounding, not bit for bit
+    assert np.abs(pairs - whole).max() <= 1e-13 * np.abs(whole).max()
 
 
 def test_half_image_tile_lists_and_element_fixup(ctx):
