@@ -1290,169 +1290,6 @@ struct Q1PwcPolicy : GenericPolicy<Cube, 1, 2, TK, KK, VX> {
 #pragma unroll
       for (int j = 0; j < NB; ++j) img[i * rowlen + pos_self * NB + j] = S[i][j];
   }
-
-  // the pair-lane mode's data movement: this lane takes element `src`'s own / gathered data from lane src
-  // (ds_bpermute); only what compute() reads, and per-element coefficient rows only when they vary per element
-  __device__ static void shuffle_from(const Own& o, const Gat& g, int src, Own& os, Gat& gs)
-  {
-    auto tens = [&](const Tensor& t) {
-      Tensor r = t;
-      if constexpr (TK == HDD_TENSOR_ISO_PER_ELEM) {
-        r.a00 = r.a11 = __shfl(t.a00, src);
-      } else if constexpr (TK == HDD_TENSOR_SYM_PER_ELEM) {
-        r.a00 = __shfl(t.a00, src);
-        r.a01 = __shfl(t.a01, src);
-        r.a11 = __shfl(t.a11, src);
-      }
-      return r;
-    };
-#pragma unroll
-    for (int k = 0; k < NB; ++k) {
-      os.X[k] = __shfl(o.X[k], src);
-      os.Y[k] = __shfl(o.Y[k], src);
-    }
-#pragma unroll
-    for (int f = 0; f < NF; ++f) {
-      os.nbr[f] = __shfl(o.nbr[f], src);
-      gs.Cx[f] = __shfl(g.Cx[f], src);
-      gs.Cy[f] = __shfl(g.Cy[f], src);
-      gs.Ap[f] = tens(g.Ap[f]);
-      gs.kn[f] = KK == HDD_FN_PER_ELEM ? __shfl(g.kn[f], src) : g.kn[f];
-    }
-    os.finfo = uint32_t(__shfl(int(o.finfo), src));
-    os.A = tens(o.A);
-    os.ke = KK == HDD_FN_PER_ELEM ? __shfl(o.ke, src) : o.ke;
-  }
-
-  // Rows 2 rp, 2 rp + 1 only, rp a run-time 0 / 1 (the two lanes of a pair share an element and run this same code
-  // on its two row pairs: the half-image kernel's pair-lane mode).  Same arithmetic per entry as compute().
-  template <class IMG>
-  __device__ static void compute_pair(const AssembleArgs& a, int64_t e, const Own& o, const Gat& gt, IMG img, int rp)
-  {
-    const double j00 = o.X[1] - o.X[0], j01 = o.X[2] - o.X[0], j10 = o.Y[1] - o.Y[0], j11 = o.Y[2] - o.Y[0];
-    const double det = j00 * j11 - j01 * j10;
-    const double id = rcp_nr(det);
-    const double i00 = j11 * id, i01 = -j01 * id, i10 = -j10 * id, i11 = j00 * id;   // J^{-1}
-    const double adet = fabs(det);
-    const double osgn = det > 0.0 ? 1.0 : -1.0;
-    int pos_self = 0, pos[NF];
-#pragma unroll
-    for (int f = 0; f < NF; ++f) pos_self += (o.nbr[f] >= 0 && o.nbr[f] < e);
-#pragma unroll
-    for (int f = 0; f < NF; ++f) {
-      int p = (e < o.nbr[f]) ? 1 : 0;
-#pragma unroll
-      for (int q = 0; q < NF; ++q) p += (o.nbr[q] >= 0 && o.nbr[q] < o.nbr[f]);
-      pos[f] = p;
-    }
-    const int rowlen = (Base::n_interior(o) + 1) * NB;
-    const Tensor A = o.A;
-    const double ke = o.ke;
-    double S[2][NB];
-    {   // LocalEvaluation::Elliptic, 1-point rule: K = J^{-1} A J^{-T}
-      const double p00 = i00 * A.a00 + i01 * A.a01, p01 = i00 * A.a01 + i01 * A.a11;
-      const double p10 = i10 * A.a00 + i11 * A.a01, p11 = i10 * A.a01 + i11 * A.a11;
-      const double k00 = p00 * i00 + p01 * i01, k01 = p00 * i10 + p01 * i11, k11 = p10 * i10 + p11 * i11;
-      const double fac = PEN ? 0.0 : adet * ke;
-#pragma unroll
-      for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-        for (int j = 0; j < NB; ++j) {
-          const int i = 2 * rp + ii;
-          const double gix = gh(i, 0, 0.5, 0.5), giy = gh(i, 1, 0.5, 0.5);
-          const double gjx = gh(j, 0, 0.5, 0.5), gjy = gh(j, 1, 0.5, 0.5);
-          S[ii][j] = fac * (gix * (k00 * gjx + k01 * gjy) + giy * (k01 * gjx + k11 * gjy));
-        }
-    }
-#pragma unroll
-    for (int f = 0; f < NF; ++f) {
-      const int32_t n = o.nbr[f];
-      if (n <= HDD_NBR_NEUMANN) continue;
-      const int fa = E::fv(f, 0), fb = E::fv(f, 1);
-      const double ax = E::rv(fa, 0), ay = E::rv(fa, 1), bx = E::rv(fb, 0), by = E::rv(fb, 1);
-      const double Ax = o.X[fa], Ay = o.Y[fa], Bx = o.X[fb], By = o.Y[fb];
-      const double tx = Bx - Ax, ty = By - Ay;
-      const double il = rsq_nr(tx * tx + ty * ty);
-      const double len = (tx * tx + ty * ty) * il;
-      const double nsc = E::face_sign(f) * osgn * il;
-      const double nx = ty * nsc, ny = -tx * nsc;
-      const double anx = A.a00 * nx + A.a01 * ny, any = A.a01 * nx + A.a11 * ny;
-      const double dm = anx * nx + any * ny;
-      const double ihp = a.beta == 1.0 ? il : inv_pow(len, a.beta);
-      const double mx = i00 * anx + i01 * any, my = i10 * anx + i11 * any;   // J^{-1} A n
-      double al[NB], be[NB];   // (A grad phi_k . n) at my face vertices a, b
-#pragma unroll
-      for (int k = 0; k < NB; ++k) {
-        al[k] = gh(k, 0, ax, ay) * mx + gh(k, 1, ax, ay) * my;
-        be[k] = gh(k, 0, bx, by) * mx + gh(k, 1, bx, by) * my;
-      }
-      const double L3 = len * (1.0 / 3.0), L6 = len * (1.0 / 6.0);
-      // int (A grad phi_j . n) phi_i  and  int phi_i phi_j
-      auto I1 = [&](int j, int i) { return i == fa ? L3 * al[j] + L6 * be[j] : (i == fb ? L6 * al[j] + L3 * be[j] : 0.0); };
-      auto MM = [&](int i, int j) {
-        return (i == fa || i == fb) && (j == fa || j == fb) ? (i == j ? L3 : L6) : 0.0;
-      };
-      if (n >= 0) {
-        const double Cx = gt.Cx[f], Cy = gt.Cy[f];
-        const Tensor Ap = gt.Ap[f];
-        const double kn = gt.kn[f];
-        // neighbour in role coordinates: A = (0,0), B = (1,0), C = (0,1)
-        const double h00 = Bx - Ax, h01 = Cx - Ax, h10 = By - Ay, h11 = Cy - Ay;
-        const double hid = rcp_nr(h00 * h11 - h01 * h10);
-        const double anpx = Ap.a00 * nx + Ap.a01 * ny, anpy = Ap.a01 * nx + Ap.a11 * ny;
-        const double dp = anpx * nx + anpy * ny;
-        const double mpx = (h11 * anpx - h01 * anpy) * hid, mpy = (-h10 * anpx + h00 * anpy) * hid;
-        double alp[NB], bep[NB];   // (A+ grad phi+_r . n) at A (0,0) and B (1,0)
-#pragma unroll
-        for (int r = 0; r < NB; ++r) {
-          alp[r] = gh(r, 0, 0.0, 0.0) * mpx + gh(r, 1, 0.0, 0.0) * mpy;
-          bep[r] = gh(r, 0, 1.0, 0.0) * mpx + gh(r, 1, 1.0, 0.0) * mpy;
-        }
-        const double rs = rcp_nr(dp + dm);
-        const double gamma = (dp * dm) * rs;
-        const double w_plus = dm * rs, w_minus = dp * rs;
-        const double pen = (ke * kn * a.sigma_inner * gamma) * ihp;
-        constexpr double CS = PEN ? 0.0 : 1.0;
-        const double cs = -w_minus * ke * CS, cp = -w_plus * kn * CS, cm = w_minus * ke * CS;
-#pragma unroll
-        for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-          for (int j = 0; j < NB; ++j) {
-            const int i = 2 * rp + ii;
-            S[ii][j] += cs * (I1(j, i) + I1(i, j)) + pen * MM(i, j);
-          }
-        int slot[NB];
-#pragma unroll
-        for (int r = 0; r < NB; ++r) slot[r] = role_slot<E>(o.finfo, f, r);
-#pragma unroll
-        for (int ii = 0; ii < 2; ++ii) {
-          const int i = 2 * rp + ii;
-          // int phi+_r phi_i: phi+_A = 1 - s, phi+_B = s (roles 0, 1); int phi+_r (A grad phi_i . n) likewise
-          const double pi = i == fa ? L3 : (i == fb ? L6 : 0.0), qi = i == fa ? L6 : (i == fb ? L3 : 0.0);
-#pragma unroll
-          for (int r = 0; r < NB; ++r) {
-            const double anr = pi * alp[r] + qi * bep[r];
-            const double ai = r == 0 ? L3 * al[i] + L6 * be[i] : (r == 1 ? L6 * al[i] + L3 * be[i] : 0.0);
-            const double mr = r == 0 ? pi : (r == 1 ? qi : 0.0);
-            img[i * rowlen + pos[f] * NB + slot[r]] = cp * anr + cm * ai - pen * mr;
-          }
-        }
-      } else {   // Dirichlet: SWIPDG::BoundaryLHS
-        const double pen = (a.sigma_boundary * ke * dm) * ihp;
-#pragma unroll
-        for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-          for (int j = 0; j < NB; ++j) {
-            const int i = 2 * rp + ii;
-            S[ii][j] += -ke * (PEN ? 0.0 : 1.0) * (I1(j, i) + I1(i, j)) + pen * MM(i, j);
-          }
-      }
-    }
-#pragma unroll
-    for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-      for (int j = 0; j < NB; ++j) img[(2 * rp + ii) * rowlen + pos_self * NB + j] = S[ii][j];
-  }
 };
 
 // P1 simplex, piecewise-constant coefficients: the closed-form policy (p1_compute above)
@@ -1913,8 +1750,6 @@ template <class P>
 struct half_of<P, std::void_t<decltype(P::HALF)>> : std::bool_constant<P::HALF> {};
 template <class P>
 constexpr int image_blocks() { return half_of<P>::value ? 32 : 64; }
-template <class P>
-constexpr bool requires_pairs() { return half_of<P>::value; }   // HALF policies provide compute_pair / shuffle_from
 
 // TL: tiles come from a.tile_list, else 0..n_tiles-1; SKIP: the sharded step's full-range launch, which leaves
 // the row blocks of elements with a ghost face neighbour to the concurrent element pass (a.skip_ghost)
@@ -2040,7 +1875,6 @@ swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
       constexpr int STH = IMG / 128;   // 16-byte chunks per lane per half
       const int nact = int(a.own_end - t0 < 64 ? a.own_end - t0 : 64);
       const int len0 = nact > 32 ? __builtin_amdgcn_readlane(off, 32) : tlen;
-      const bool pairs = requires_pairs<P>() && (a.debug_flags & 134217728);   // study: pair-lane compute
       // sharded step: image ranges of the skipped elements, tile coordinates (as in stores_skip below)
       constexpr int NR = 4;
       int rb[NR], re[NR];
@@ -2069,23 +1903,7 @@ swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int hb = h ? len0 : 0, hl = (h ? tlen : len0) - hb;   // wave-uniform
-        if constexpr (requires_pairs<P>()) {
-          if (pairs) {
-            // pair-lane mode: lanes 2m, 2m + 1 build rows 0-1 / 2-3 of element 32 h + m (its data by ds_bpermute)
-            const int src = 32 * h + (lane >> 1);
-            typename P::Own os;
-            typename P::Gat gs;
-            P::shuffle_from(own, gat, src, os, gs);
-            const int off_s = __shfl(off, src);
-            const bool act_s = t0 + src < a.own_end;
-            if (!HDD_ABL(a, 1)) {
-              const RotImg<RB> img{uni ? lds + (src & 31) * RB : (act_s ? lds + (off_s - hb) : scratch),
-                                   uni ? 2 * ((src >> 1) & 15) : 0};
-              P::compute_pair(a, act_s ? t0 + src : t0, os, gs, img, lane & 1);
-            }
-          }
-        }
-        if (!pairs && (lane >> 5) == h && !HDD_ABL(a, 1)) {
+        if ((lane >> 5) == h && !HDD_ABL(a, 1)) {
           const RotImg<RB> img{uni ? lds + (lane & 31) * RB : (active ? lds + (off - hb) : scratch),
                                uni ? 2 * ((lane >> 1) & 15) : 0};
           // the two halves' computations are identical code on identical registers: without an opaque copy of

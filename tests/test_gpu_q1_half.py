@@ -21,15 +21,14 @@ pytestmark = pytest.mark.gpu
 # HDD_DEBUG_FLAGS (swipdg_q1.hip): the default on vertex-indexed meshes is the half-image kernel
 WHOLE = 1048576     # the whole-tile image kernel (round 3's default)
 HALF_EM = 2097152   # the half-image kernel on element-major coordinates
-PAIRS = 134217728   # the half-image kernel's pair-lane compute (study; equal up to rounding)
 
 
 def _all(ctx, fn):
     """fn() under the whole-tile kernel, the half-image kernel and the half-image kernel on vertex-indexed
-    geometry, and its pair-lane compute -> [whole, half, half_vx, pairs]"""
+    geometry -> [whole, half, half_vx]"""
     import torch
     out = []
-    for flags in (WHOLE, HALF_EM, 0, PAIRS):
+    for flags in (WHOLE, HALF_EM, 0):
         ctx.set_debug_flags(flags)
         try:
             r = fn()
@@ -64,12 +63,9 @@ def test_half_image_equals_whole_tile(ctx, tk, bnd, kpe):
     kf = [H.scalar_fn(H.FN_PER_ELEM, per_elem=torch.from_numpy(np.ascontiguousarray(kap[idx])).cuda())
           if kpe else H.scalar_fn(H.FN_CONST, 1.7)]
     dm, dp = H.DeviceMesh(loc), H.DevicePattern(loc)
-    whole, half, half_vx, pairs = _all(ctx, lambda: H.assemble(ctx, dm, dp, kf, ten)[0].cpu().numpy())
+    whole, half, half_vx = _all(ctx, lambda: H.assemble(ctx, dm, dp, kf, ten)[0].cpu().numpy())
     assert np.array_equal(_bits(whole), _bits(half))
     assert np.array_equal(_bits(whole), _bits(half_vx))
-    # the pair-lane compute evaluates the row-dependent constants at run time, so its fused multiply-adds contract
-    # differently: equal up to rounding, not bit for bit
-    assert np.abs(pairs - whole).max() <= 1e-13 * np.abs(whole).max()
     pc, pev, _ = grid.connectivity()
     og = O.Grid(O.cube_grid(1, 1, (0, 0), (1, 1))[0], pc, pev)
     okind = O.TENSOR_SYM_PER_ELEM if tk == "sym" else O.TENSOR_ISO_PER_ELEM
@@ -91,13 +87,10 @@ def test_half_image_edge_meshes(ctx, nx, ny):
     k = torch.from_numpy(loc.checkerboard(SPE10_LOWER, SPE10_UPPER, 100, 20, perm)).cuda()
     dm, dp = H.DeviceMesh(loc), H.DevicePattern(loc)
     kf, ten = [H.scalar_fn(H.FN_CONST, 1.0)], H.tensor_fn(H.TENSOR_ISO_PER_ELEM, per_elem=k)
-    whole, half, half_vx, pairs = _all(ctx, lambda: H.assemble(ctx, dm, dp, kf, ten)[0].cpu().numpy())
+    whole, half, half_vx = _all(ctx, lambda: H.assemble(ctx, dm, dp, kf, ten)[0].cpu().numpy())
     assert np.isfinite(half).all()
     assert np.array_equal(_bits(whole), _bits(half))
     assert np.array_equal(_bits(whole), _bits(half_vx))
-    # the pair-lane compute evaluates the row-dependent constants at run time, so its fused multiply-adds contract
-    # differently: equal up to rounding, not bit for bit
-    assert np.abs(pairs - whole).max() <= 1e-13 * np.abs(whole).max()
 
 
 @pytest.mark.parametrize("kind", ["parallelogram", "scrambled"])
@@ -114,12 +107,9 @@ def test_half_image_general_quads(ctx, kind):
     k = torch.from_numpy(np.ascontiguousarray(10.0 ** np.sin(7 * x + 3 * y))).cuda()
     dm, dp = H.DeviceMesh(loc), H.DevicePattern(loc)
     kf, ten = [H.scalar_fn(H.FN_CONST, 1.0)], H.tensor_fn(H.TENSOR_ISO_PER_ELEM, per_elem=k)
-    whole, half, half_vx, pairs = _all(ctx, lambda: H.assemble(ctx, dm, dp, kf, ten)[0].cpu().numpy())
+    whole, half, half_vx = _all(ctx, lambda: H.assemble(ctx, dm, dp, kf, ten)[0].cpu().numpy())
     assert np.array_equal(_bits(whole), _bits(half))
     assert np.array_equal(_bits(whole), _bits(half_vx))
-    # the pair-lane compute evaluates the row-dependent constants at run time, so its fused multiply-adds contract
-    # differently: equal up to rounding, not bit for bit
-    assert np.abs(pairs - whole).max() <= 1e-13 * np.abs(whole).max()
 
 
 def test_half_image_tile_lists_and_element_fixup(ctx):
