@@ -325,8 +325,15 @@ def main():
                          "traffic_frac": (traffic / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if traffic else None,
                          "traffic_gbs": (traffic / (kernel_ms * 1e-3) / 1e9) if traffic else None,
                          "traffic_source": traffic_src, "build_id": bid,
-                         "kernel": "swipdg_persistent_kernel<%s<1, 0, false>, %s>"
-                                   % ("Q1PwcPolicy" if c4 else "P1PwcPolicy", "true" if per_step else "false"),
+                         # the dominant kernel (swipdg_q1.hip / swipdg_p1.hip dispatch): C4 at one launch per step the
+                         # half-image Q1 kernel on vertex-indexed geometry; the sharded step's full-range launch skips the
+                         # ghost-adjacent row blocks (whole-tile Q1 kernel; P1: skip instantiation on in-place ranks)
+                         "kernel": ("swipdg_persistent_kernel<Q1PwcPolicy<1, 0, false, false, false>, false, true>"
+                                    if c4 and per_step else
+                                    "swipdg_persistent_kernel<Q1PwcPolicy<1, 0, false, true, true>, false, false>"
+                                    if c4 else
+                                    "swipdg_persistent_kernel<P1PwcPolicy<1, 0, false, true>, false, %s>"
+                                    % ("true" if per_step else "false")),
                          "kernel_ms_avg": kernel_ms, "kernel_ms_avg_max_rank": kernel_ms_max,
                          "algorithmic_bytes_per_launch": alg_bytes,
                          # measured on this box in this run: device copy (read + write) and fill (write)
