@@ -901,7 +901,14 @@ extern "C" int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm*
 
   hipError_t e = hipSetDevice(sh->device);
   if (e != hipSuccess) return hip_fail(e, "hdd_block_assemble_sharded: hipSetDevice");
-  const bool split = (flags & HDD_SHARD_SPLIT_TILES) != 0;
+  // Default schedule by element type and peer count (one-card step study, profiles/r04/e_reserve/): P1 ranks with
+  // two peers split the tiles -- interior tiles during the exchange, the 2 % of tiles with a ghost-adjacent element
+  // after it (C2 N = 8 middle rank +0.8 / +4.0 % over one launch, against +10.1 % for the side-buffer fixup and
+  // +26.5 % in place, whose row blocks share cache lines with the tiles' stores: P1 blocks are 288 B); every other
+  // shard keeps the off-stream element fixup in place (Q1: its split costs +18 %).
+  const bool default_schedule = !(flags & (HDD_SHARD_FIX_INLINE | HDD_SHARD_FIX_SCATTER | HDD_SHARD_FIX_INPLACE));
+  const bool split = (flags & HDD_SHARD_SPLIT_TILES) != 0 ||
+                     (default_schedule && sh->gi.elem_type == HDD_SIMPLEX && sh->peers.size() >= 2 && sh->n_in > 0);
   bool overlap = !(flags & HDD_SHARD_NO_OVERLAP) && sh->gi.elem_type != HDD_HEX && (split ? sh->n_in > 0 : true);
   // The pack and the transfer leave the assembly stream when the assembly overlaps them: the RCCL transfer
   // stream (or, in the loopback study, the shard's side stream) waits for the inputs, packs and sends while
@@ -939,8 +946,7 @@ extern "C" int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm*
   // 8): in place, except P1 ranks with two peers (C2 middle ranks: +10 % with the side buffer vs +14 % in place,
   // the P1 tiles' two waves per SIMD leaving the element pass no registers beside them; end ranks +4 % in place
   // vs +8 %); Q1 in place everywhere (+9 % middle / +15 % end rank at N = 8 vs +20 / +13 %)
-  const bool scatter = offfix && !(flags & HDD_SHARD_FIX_INPLACE) &&
-                       ((flags & HDD_SHARD_FIX_SCATTER) || (sh->gi.elem_type == HDD_SIMPLEX && sh->peers.size() >= 2));
+  const bool scatter = offfix && !(flags & HDD_SHARD_FIX_INPLACE) && (flags & HDD_SHARD_FIX_SCATTER);
   const int32_t rb = hdd_fix_rb(sh->gi.elem_type);
   std::vector<double*> fbufs;
   if (scatter) {

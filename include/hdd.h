@@ -502,17 +502,17 @@ enum {
                                    loopback copy + unpack kernel instead of the transfer (comm may be NULL; the
                                    ghost columns receive the rank's own send buffers, i.e. wrong values) -- an
                                    upper bound of the GPU-side cost of the sharded step */
-  HDD_SHARD_SPLIT_TILES = 16,   /* overlap by tiles (round 2): interior tiles during the exchange, the tiles with a
-                                   ghost-adjacent element after it (default: every tile during the exchange, then
-                                   the ghost-adjacent ELEMENTS again, hdd_swipdg_assemble_elements) */
+  HDD_SHARD_SPLIT_TILES = 16,   /* overlap by tiles: interior tiles during the exchange, the tiles with a
+                                   ghost-adjacent element after it -- the default for P1 shards with two peers;
+                                   otherwise the default is every tile during the exchange and the ghost-adjacent
+                                   ELEMENTS again, off-stream, in place (HDD_SHARD_FIX_INPLACE) */
   HDD_SHARD_FIX_INLINE = 32,    /* study (round 3 A/B): the ghost-adjacent elements recomputed on `stream` after
                                    the wait (default: on the transfer stream right after the receives, beside the
                                    assembly) */
-  HDD_SHARD_FIX_SCATTER = 64,   /* the off-stream fixup into a side buffer, copied into place by one kernel after
-                                   the join (the assembly's tiles store every row block): default for P1 shards
-                                   with two or more peers */
+  HDD_SHARD_FIX_SCATTER = 64,   /* study: the off-stream fixup into a side buffer, copied into place by one kernel
+                                   after the join (the assembly's tiles store every row block) */
   HDD_SHARD_FIX_INPLACE = 128   /* the off-stream fixup in place, the assembly's tiles skip those row blocks:
-                                   default otherwise */
+                                   default except on P1 shards with two peers (HDD_SHARD_SPLIT_TILES) */
 };
 /* One sharded assembly step -- the LHS of BlockSWIPDG::init() for the owned subdomains: pack the halo
  * records (per-element tensor / kappa rows, [+ coordinates]) of the elements the peers need -> post the
