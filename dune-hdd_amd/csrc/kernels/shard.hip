@@ -961,6 +961,17 @@ extern "C" int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm*
     }
     for (int32_t c = 0; c < n_comp; ++c) fbufs.push_back(sh->d_fixbuf + size_t(c) * slot);
   }
+  // 0. HDD_SHARD_LAUNCH_FIRST: the full-range skip launch is enqueued before the halo work.  It needs nothing the
+  // exchange delivers (the row blocks that read a ghost column are the element pass's), and its inputs event was
+  // recorded above, so the pack does not wait for it; enqueued first, it starts while the host is still issuing the
+  // pack / exchange / element-pass launches instead of after them.
+  const int32_t reserve = int32_t(std::min<int64_t>((sh->n_fix + 63) / 64, 256));
+  bool first = false;
+  if (offfix && !scatter && (flags & HDD_SHARD_LAUNCH_FIRST)) {
+    const int rc0 = hdd_assemble_skip_ghost(ctx, &m, kappa, n_comp, tensor, params, pattern, d_vals, stream, reserve);
+    if (rc0 == HDD_OK) first = true;
+    else if (rc0 != HDD_ERR_UNSUPPORTED) return rc0;   // (unsupported rules: the order below, whole range again)
+  }
   // 1. pack the records the peers need (one launch for every peer)
   for (int k = 0; k <= h.n_peers; ++k) h.prefix[k] = sh->send_prefix[k];
   h.idx = sh->d_send_idx;
@@ -1044,13 +1055,12 @@ extern "C" int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm*
   // blocks of the ghost-adjacent elements read ghost columns the receives are still writing and are recomputed
   // in 5).  HDD_SHARD_SPLIT_TILES: the interior tiles only (the kernels that take lists: P1 / Q1 persistent
   // policies) -- a second launch of whole boundary tiles later, which on thin strips is a large fraction.
-  if (overlap) {
+  if (overlap && !first) {
     // in-place fixup running: the tiles leave the ghost-adjacent elements' row blocks to it
     const bool skip = fix_pending && !scatter && !fix_unsupported;
     rc = split ? hdd_swipdg_assemble_tiles(ctx, &m, kappa, n_comp, tensor, params, pattern, d_vals, sh->d_tiles_in,
                                            sh->n_in, stream)
-         : skip ? hdd_assemble_skip_ghost(ctx, &m, kappa, n_comp, tensor, params, pattern, d_vals, stream,
-                                          int32_t(std::min<int64_t>((sh->n_fix + 63) / 64, 256)))
+         : skip ? hdd_assemble_skip_ghost(ctx, &m, kappa, n_comp, tensor, params, pattern, d_vals, stream, reserve)
                 : hdd_swipdg_assemble(ctx, &m, kappa, n_comp, tensor, params, pattern, d_vals, stream);
     if (rc == HDD_ERR_UNSUPPORTED && split) overlap = false;   // no tile-list kernel: everything after the halo
     else if (rc) {

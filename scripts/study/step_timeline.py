@@ -43,6 +43,7 @@ def main():
     import hdd_amd as H
     wl, n, rank = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
     reps = int(sys.argv[4]) if len(sys.argv) > 4 else 20
+    flags = H.SHARD_NO_TRANSFER | (int(sys.argv[5]) if len(sys.argv) > 5 else 0)
     if wl == "c4":
         grid = H.Grid.structured(H.CUBE, 3520, 1200, (0.0, 0.0), (5.0, 1.0), px=8, py=8)
         up, ncx, ncell = (5.0, 1.0), 100, 2000
@@ -58,12 +59,12 @@ def main():
     kap, ten = [H.scalar_fn(H.FN_CONST, 1.0)], H.tensor_fn(H.TENSOR_ISO_PER_ELEM, per_elem=k)
     marker = torch.empty(64, dtype=torch.float64, device="cuda")
     for _ in range(10):
-        H.assemble_sharded(ctx, sh, None, kap, ten, pat, vals, flags=H.SHARD_NO_TRANSFER)
+        H.assemble_sharded(ctx, sh, None, kap, ten, pat, vals, flags=flags)
     torch.cuda.synchronize()
     for _ in range(reps):
         marker.fill_(0.0)
         torch.cuda.synchronize()
-        H.assemble_sharded(ctx, sh, None, kap, ten, pat, vals, flags=H.SHARD_NO_TRANSFER)
+        H.assemble_sharded(ctx, sh, None, kap, ten, pat, vals, flags=flags)
         torch.cuda.synchronize()
     marker.fill_(1.0)
     torch.cuda.synchronize()

@@ -38,6 +38,7 @@ SCHEDULES = {
     "inline": H.SHARD_FIX_INLINE,
     "split": H.SHARD_SPLIT_TILES,
     "serial": H.SHARD_NO_OVERLAP,
+    "first": H.SHARD_FIX_INPLACE | H.SHARD_LAUNCH_FIRST,
 }
 
 
