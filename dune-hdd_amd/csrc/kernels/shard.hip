@@ -915,7 +915,13 @@ extern "C" int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm*
   // `stream` starts the assembly at once -- the pack launch is off the critical path.  (The host transport
   // stages through the host on `stream` anyway.)
   hipStream_t ps = s;
-  const bool side = overlap && !split;
+  // The assembly's own launch (the full-range skip launch, or the interior tiles of a split) is enqueued BEFORE the
+  // halo work by default, so it starts at once instead of after the host has issued pack, exchange and element pass
+  // (one-card kernel timeline, profiles/r04/n_first/: C4 N = 8 step 113-120 -> 77-79 us when steps do not overlap;
+  // back-to-back steps, where the host runs ahead, are unchanged).  The split then packs on the side stream too.
+  // HDD_SHARD_LAUNCH_LAST: round 3's order.
+  const bool last = (flags & HDD_SHARD_LAUNCH_LAST) != 0;
+  const bool side = overlap && (!split || !last);
   if (side) {
     if (transfer && comm->kind != hdd_comm::HOST) {
       ps = comm->xfer;
@@ -940,7 +946,7 @@ extern "C" int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm*
     if (e == hipSuccess) e = hipStreamWaitEvent(ps, sh->ev_in, 0);
     if (e != hipSuccess) return hip_fail(e, "hdd_block_assemble_sharded: order pack after inputs");
   }
-  const bool offfix = side && !(flags & HDD_SHARD_FIX_INLINE) && sh->n_fix > 0;
+  const bool offfix = side && !split && !(flags & HDD_SHARD_FIX_INLINE) && sh->n_fix > 0;
   // where the fixup writes: in place beside a tile launch that skips those row blocks, or a side buffer + one
   // copy kernel after the join.  Default from the one-card step study (profiles/r03/shard_step/final/, N = 2 and
   // 8): in place, except P1 ranks with two peers (C2 middle ranks: +10 % with the side buffer vs +14 % in place,
@@ -961,16 +967,18 @@ extern "C" int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm*
     }
     for (int32_t c = 0; c < n_comp; ++c) fbufs.push_back(sh->d_fixbuf + size_t(c) * slot);
   }
-  // 0. HDD_SHARD_LAUNCH_FIRST: the full-range skip launch is enqueued before the halo work.  It needs nothing the
-  // exchange delivers (the row blocks that read a ghost column are the element pass's), and its inputs event was
-  // recorded above, so the pack does not wait for it; enqueued first, it starts while the host is still issuing the
-  // pack / exchange / element-pass launches instead of after them.
+  // 0. The assembly's launch first (see above): the full-range skip launch needs nothing the exchange delivers (the
+  // row blocks that read a ghost column are the element pass's), the interior tiles of a split read no ghost column,
+  // and the inputs event was recorded above, so the pack does not wait for either.
   const int32_t reserve = int32_t(std::min<int64_t>((sh->n_fix + 63) / 64, 256));
   bool first = false;
-  if (offfix && !scatter && (flags & HDD_SHARD_LAUNCH_FIRST)) {
-    const int rc0 = hdd_assemble_skip_ghost(ctx, &m, kappa, n_comp, tensor, params, pattern, d_vals, stream, reserve);
+  if (!last && ((offfix && !scatter) || (overlap && split))) {
+    const int rc0 = split ? hdd_swipdg_assemble_tiles(ctx, &m, kappa, n_comp, tensor, params, pattern, d_vals,
+                                                      sh->d_tiles_in, sh->n_in, stream)
+                          : hdd_assemble_skip_ghost(ctx, &m, kappa, n_comp, tensor, params, pattern, d_vals, stream,
+                                                    reserve);
     if (rc0 == HDD_OK) first = true;
-    else if (rc0 != HDD_ERR_UNSUPPORTED) return rc0;   // (unsupported rules: the order below, whole range again)
+    else if (rc0 != HDD_ERR_UNSUPPORTED) return rc0;   // (unsupported rules: the order below)
   }
   // 1. pack the records the peers need (one launch for every peer)
   for (int k = 0; k <= h.n_peers; ++k) h.prefix[k] = sh->send_prefix[k];

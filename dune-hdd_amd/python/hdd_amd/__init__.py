@@ -108,7 +108,7 @@ HOST_EXCHANGE_FN = C.CFUNCTYPE(C.c_int32, C.c_void_p, C.c_int32, C.POINTER(C.c_i
                                C.POINTER(C.c_int64), C.POINTER(C.c_void_p), C.POINTER(C.c_int64))
 RCCL_ID_BYTES = 128
 (SHARD_NO_OVERLAP, SHARD_HALO_GEOMETRY, SHARD_NO_HALO, SHARD_NO_TRANSFER, SHARD_SPLIT_TILES, SHARD_FIX_INLINE,
- SHARD_FIX_SCATTER, SHARD_FIX_INPLACE, SHARD_LAUNCH_FIRST) = 1, 2, 4, 8, 16, 32, 64, 128, 256
+ SHARD_FIX_SCATTER, SHARD_FIX_INPLACE, SHARD_LAUNCH_LAST) = 1, 2, 4, 8, 16, 32, 64, 128, 256
 
 
 _LIB = None

@@ -87,7 +87,7 @@ def main():
             "NO_HALO, all ranks (one launch each)": (H.SHARD_NO_HALO, True),
             "step, default": (0, False),
             "step, fixup in place": (H.SHARD_FIX_INPLACE, False),
-            "step, in place, tiles launched first": (H.SHARD_FIX_INPLACE | H.SHARD_LAUNCH_FIRST, False),
+            "step, default, launch after the halo work (r3)": (H.SHARD_LAUNCH_LAST, False),
             "step, fixup inline (round 2)": (H.SHARD_FIX_INLINE, False),
             "step, serial": (H.SHARD_NO_OVERLAP, False),
         }

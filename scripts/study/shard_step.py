@@ -65,7 +65,7 @@ def main():
                 "b' step, fixup inline (round 2)": H.SHARD_NO_TRANSFER | H.SHARD_FIX_INLINE,
                 "b'' step, fixup + copy kernel": H.SHARD_NO_TRANSFER | H.SHARD_FIX_SCATTER,
                 "b''' step, fixup in place": H.SHARD_NO_TRANSFER | H.SHARD_FIX_INPLACE,
-                "b'''' in place, tiles launched first": H.SHARD_NO_TRANSFER | H.SHARD_FIX_INPLACE | H.SHARD_LAUNCH_FIRST,
+                "b'''' step, launch after halo work (r3)": H.SHARD_NO_TRANSFER | H.SHARD_LAUNCH_LAST,
                 "c serial step, no transfer": H.SHARD_NO_TRANSFER | H.SHARD_NO_OVERLAP,
                 "e split tiles, no transfer": H.SHARD_NO_TRANSFER | H.SHARD_SPLIT_TILES,
             }
