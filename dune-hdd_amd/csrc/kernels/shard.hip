@@ -915,13 +915,14 @@ extern "C" int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm*
   // `stream` starts the assembly at once -- the pack launch is off the critical path.  (The host transport
   // stages through the host on `stream` anyway.)
   hipStream_t ps = s;
-  // The assembly's own launch (the full-range skip launch, or the interior tiles of a split) is enqueued BEFORE the
-  // halo work by default, so it starts at once instead of after the host has issued pack, exchange and element pass
-  // (one-card kernel timeline, profiles/r04/n_first/: C4 N = 8 step 113-120 -> 77-79 us when steps do not overlap;
-  // back-to-back steps, where the host runs ahead, are unchanged).  The split then packs on the side stream too.
-  // HDD_SHARD_LAUNCH_LAST: round 3's order.
+  // With the in-place fixup the full-range skip launch is enqueued BEFORE the halo work by default, so it starts at
+  // once instead of after the host has issued pack, exchange and element pass (one-card kernel timeline,
+  // profiles/r04/n_first/: C4 N = 8 step 113-120 -> 77-79 us when steps do not overlap; back-to-back steps, where the
+  // host runs ahead, are unchanged).  HDD_SHARD_LAUNCH_LAST: round 3's order.  The split keeps its pack on `stream`
+  // before the interior tiles: packing on the side stream beside them measured +10.0 % against +5.3 % (C2 N = 8
+  // middle rank, back-to-back, profiles/r04/o_final/).
   const bool last = (flags & HDD_SHARD_LAUNCH_LAST) != 0;
-  const bool side = overlap && (!split || !last);
+  const bool side = overlap && !split;
   if (side) {
     if (transfer && comm->kind != hdd_comm::HOST) {
       ps = comm->xfer;
@@ -967,16 +968,12 @@ extern "C" int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm*
     }
     for (int32_t c = 0; c < n_comp; ++c) fbufs.push_back(sh->d_fixbuf + size_t(c) * slot);
   }
-  // 0. The assembly's launch first (see above): the full-range skip launch needs nothing the exchange delivers (the
-  // row blocks that read a ghost column are the element pass's), the interior tiles of a split read no ghost column,
-  // and the inputs event was recorded above, so the pack does not wait for either.
+  // 0. The skip launch first (see above): it needs nothing the exchange delivers (the row blocks that read a ghost
+  // column are the element pass's), and the inputs event was recorded above, so the pack does not wait for it.
   const int32_t reserve = int32_t(std::min<int64_t>((sh->n_fix + 63) / 64, 256));
   bool first = false;
-  if (!last && ((offfix && !scatter) || (overlap && split))) {
-    const int rc0 = split ? hdd_swipdg_assemble_tiles(ctx, &m, kappa, n_comp, tensor, params, pattern, d_vals,
-                                                      sh->d_tiles_in, sh->n_in, stream)
-                          : hdd_assemble_skip_ghost(ctx, &m, kappa, n_comp, tensor, params, pattern, d_vals, stream,
-                                                    reserve);
+  if (!last && offfix && !scatter) {
+    const int rc0 = hdd_assemble_skip_ghost(ctx, &m, kappa, n_comp, tensor, params, pattern, d_vals, stream, reserve);
     if (rc0 == HDD_OK) first = true;
     else if (rc0 != HDD_ERR_UNSUPPORTED) return rc0;   // (unsupported rules: the order below)
   }

@@ -513,8 +513,8 @@ enum {
                                    after the join (the assembly's tiles store every row block) */
   HDD_SHARD_FIX_INPLACE = 128,  /* the off-stream fixup in place, the assembly's tiles skip those row blocks:
                                    default except on P1 shards with two peers (HDD_SHARD_SPLIT_TILES) */
-  HDD_SHARD_LAUNCH_LAST = 256   /* study (round 3's order): enqueue the assembly's launch after the halo work (pack,
-                                   exchange, element pass) instead of before it */
+  HDD_SHARD_LAUNCH_LAST = 256   /* study (round 3's order): with the in-place fixup, enqueue the full-range launch
+                                   after the halo work (pack, exchange, element pass) instead of before it */
 };
 /* One sharded assembly step -- the LHS of BlockSWIPDG::init() for the owned subdomains: pack the halo
  * records (per-element tensor / kappa rows, [+ coordinates]) of the elements the peers need -> post the
