@@ -42,6 +42,19 @@ int hip_fail(hipError_t e, const char* where)
   return set_error(HDD_ERR_HIP, std::string(where) + ": " + hipGetErrorString(e));
 }
 
+// Events that only order two streams of ONE device (the step's side stream against `stream`, RCCL's transfer
+// stream back into `stream`): the data both sides touch stays on that device, so a device-scope release /
+// acquire is enough.  A default event's record is a system-scope release -- an L2 write-back of everything the
+// previous tile launch left dirty -- which sits between two launches of back-to-back steps (C4 N = 8 one-card
+// trace, profiles/r04/q_btb/: 12.5 us of 93 us per step with nothing running).  Events another device waits on
+// (the device transport's "packed" = comm->ready, read by peer copies; RCCL may read send buffers from a peer)
+// keep the system fence.  HDD_EVENT_SYSTEM_FENCE=1 restores it everywhere (A/B).
+unsigned local_event_flags()
+{
+  static const bool sys = getenv("HDD_EVENT_SYSTEM_FENCE") != nullptr;
+  return sys ? hipEventDisableTiming : hipEventDisableTiming | hipEventDisableSystemFence;
+}
+
 // ------------------------------------------------------------------------------------------------
 // RCCL, resolved at run time: in a PyTorch process this is torch's own librccl (already loaded, found
 // through the library's rpath), so the process holds one RCCL and one HIP runtime.
@@ -245,7 +258,7 @@ static int comm_rccl_streams(hdd_comm* c)
   hipError_t e = hipSetDevice(c->device);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->xfer, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ready, hipEventDisableTiming);
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->done, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->done, local_event_flags());
   return e == hipSuccess ? HDD_OK : hip_fail(e, "hdd_comm: transfer stream / events");
 }
 
@@ -929,18 +942,18 @@ extern "C" int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm*
     } else {   // loopback study, host transport (which stages through the host on this stream)
       if (!sh->aux) {
         e = hipStreamCreateWithFlags(&sh->aux, hipStreamNonBlocking);
-        if (e == hipSuccess) e = hipEventCreateWithFlags(&sh->ev_in, hipEventDisableTiming);
-        if (e == hipSuccess) e = hipEventCreateWithFlags(&sh->ev_out, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&sh->ev_in, local_event_flags());
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&sh->ev_out, local_event_flags());
         if (e != hipSuccess) return hip_fail(e, "hdd_block_assemble_sharded: side stream");
       }
       ps = sh->aux;
     }
     if (!sh->ev_in) {
-      e = hipEventCreateWithFlags(&sh->ev_in, hipEventDisableTiming);
+      e = hipEventCreateWithFlags(&sh->ev_in, local_event_flags());
       if (e != hipSuccess) return hip_fail(e, "hdd_block_assemble_sharded: event");
     }
     if (!sh->ev_out) {
-      e = hipEventCreateWithFlags(&sh->ev_out, hipEventDisableTiming);
+      e = hipEventCreateWithFlags(&sh->ev_out, local_event_flags());
       if (e != hipSuccess) return hip_fail(e, "hdd_block_assemble_sharded: event");
     }
     e = hipEventRecord(sh->ev_in, s);

@@ -1,7 +1,10 @@
 """Timeline of the sharded step's kernels on one card (run under `rocprofv3 --kernel-trace`), for rank r of an
 N-rank C4 / C2 decomposition with the loopback transfer (HDD_SHARD_NO_TRANSFER): `reps` steps after a warmup,
 each step bracketed by a tiny marker fill so the trace can be cut into steps.  Summarise with --summary <csv>.
-usage: python scripts/study/step_timeline.py c4 8 0 [reps]
+With --btb the steps run back to back (no host synchronisation between them, one marker before and one after),
+and the summary lists every kernel of the run with its start relative to the previous persistent launch's start
+and end: the step-to-step period and the gap the join leaves between the launches.
+usage: python scripts/study/step_timeline.py c4 8 0 [reps [flags]] [--btb]
        python scripts/study/step_timeline.py --summary <run_kernel_trace.csv>"""
 import os
 import sys
@@ -27,7 +30,10 @@ def summary(path):
             cur.append((name.split("(")[0].replace("void ", "")[:90], int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
     if cur:
         steps.append(cur)
-    steps = [s for s in steps if s][-5:]
+    steps = [s for s in steps if s]
+    if len(steps) == 1 and sum("persistent" in n for n, _, _ in steps[0]) > 2:   # --btb: one segment
+        return summary_btb(steps[0])
+    steps = steps[-5:]
     for k, s in enumerate(steps):
         t0 = min(b for _, b, _ in s)
         t1 = max(e for _, _, e in s)
@@ -36,7 +42,24 @@ def summary(path):
             print("   %7.1f .. %7.1f us  %s" % ((b - t0) / 1e3, (e - t0) / 1e3, name))
 
 
+def summary_btb(seg):
+    pers = [(b, e) for n, b, e in seg if "persistent" in n]
+    per = [(pers[i + 1][0] - pers[i][0]) / 1e3 for i in range(len(pers) - 1)]
+    gap = [(pers[i + 1][0] - pers[i][1]) / 1e3 for i in range(len(pers) - 1)]
+    dur = [(e - b) / 1e3 for b, e in pers]
+    print("%d persistent launches back to back: period median %.1f us (min %.1f, max %.1f), launch median %.1f us, "
+          "gap end -> next start median %.1f us (min %.1f, max %.1f)"
+          % (len(pers), np.median(per), min(per), max(per), np.median(dur), np.median(gap), min(gap), max(gap)))
+    t0 = pers[len(pers) // 2][0]
+    for name, b, e in seg:   # the middle of the run in detail
+        if -150e3 <= b - t0 <= 250e3:
+            print("   %7.1f .. %7.1f us  %s" % ((b - t0) / 1e3, (e - t0) / 1e3, name))
+
+
 def main():
+    btb = "--btb" in sys.argv
+    if btb:
+        sys.argv.remove("--btb")
     if sys.argv[1] == "--summary":
         return summary(sys.argv[2])
     import torch
@@ -61,7 +84,13 @@ def main():
     for _ in range(10):
         H.assemble_sharded(ctx, sh, None, kap, ten, pat, vals, flags=flags)
     torch.cuda.synchronize()
-    for _ in range(reps):
+    if btb:
+        marker.fill_(0.0)
+        torch.cuda.synchronize()
+        for _ in range(reps):
+            H.assemble_sharded(ctx, sh, None, kap, ten, pat, vals, flags=flags)
+        torch.cuda.synchronize()
+    for _ in range(0 if btb else reps):
         marker.fill_(0.0)
         torch.cuda.synchronize()
         H.assemble_sharded(ctx, sh, None, kap, ten, pat, vals, flags=flags)
