@@ -235,11 +235,12 @@ def main():
         flags = H.SHARD_NO_HALO
     for _ in range(args.warmup):
         step(flags)
-    # Kernel time: with a per-step halo, events bracket each sharded step (pack, exchange, both tile sets,
-    # unpack) on the assembly stream; otherwise one event pair brackets the K back-to-back launches
-    # (per-step event records add ~9 us of queue work per launch on ROCm: scripts/study/gap.py ->
-    # profiles/r01/s2/gap.log), so kernel_ms is the average launch duration including the dispatch gaps.
-    per_step = world > 1 and args.halo == "step"
+    # Kernel time: one event pair brackets the K back-to-back steps on the assembly stream, so kernel_ms is the
+    # average step duration including the dispatch gaps (and, with N > 1, the sharded step's pack / exchange /
+    # element pass).  Per-step event records would add ~9 us of queue work per step on ROCm (scripts/study/gap.py
+    # -> profiles/r01/s2/gap.log) inside the timed region, so they are not used at any N.
+    per_step = False
+    sharded_step = world > 1 and args.halo == "step"   # (the kernel label below: the SKIP / split launches)
     events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
               for _ in range(args.steps if per_step else 1)]
     if world > 1:
@@ -329,11 +330,11 @@ def main():
                          # half-image Q1 kernel on vertex-indexed geometry; the sharded step's full-range launch skips the
                          # ghost-adjacent row blocks (whole-tile Q1 kernel; P1: skip instantiation on in-place ranks)
                          "kernel": ("swipdg_persistent_kernel<Q1PwcPolicy<1, 0, false, false, false>, false, true>"
-                                    if c4 and per_step else
+                                    if c4 and sharded_step else
                                     "swipdg_persistent_kernel<Q1PwcPolicy<1, 0, false, true, true>, false, false>"
                                     if c4 else
                                     "swipdg_persistent_kernel<P1PwcPolicy<1, 0, false, true>, false, %s>"
-                                    % ("true" if per_step else "false")),
+                                    % ("true" if sharded_step else "false")),
                          "kernel_ms_avg": kernel_ms, "kernel_ms_avg_max_rank": kernel_ms_max,
                          "algorithmic_bytes_per_launch": alg_bytes,
                          # measured on this box in this run: device copy (read + write) and fill (write)
