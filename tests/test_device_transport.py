@@ -157,6 +157,36 @@ def test_device_transport_equals_single_gpu(kind, n):
 
 
 @pytest.mark.gpu
+def test_device_transport_c4_full_size_n8():
+    """BASELINE C4 at full size (3520 x 1200 Q1 quads, 8 x 8 subdomains) as 8 thread ranks of one column each on
+    one card: the production schedules at production shard sizes (persistent tile schedule with the grid reserve,
+    the SKIP launch, the in-place element pass of 1,200 / 2,400 ghost-adjacent elements) -- every rank's rows
+    bit-identical to the whole-grid assembly, two steps."""
+    grid = H.Grid.structured(H.CUBE, 3520, 1200, LOWER, UPPER, px=8, py=8)
+    got, infos = run_device_ranks(grid, 8, H.TENSOR_ISO_PER_ELEM, False, {"default": 0}, steps=2)
+    assert [i.n_peers for i in infos] == [1] + [2] * 6 + [1]
+    ref = _single_gpu(grid, H.TENSOR_ISO_PER_ELEM, False)
+    v = got["default"]
+    assert v.shape == ref.shape and np.isfinite(v).all()
+    assert np.array_equal(v.view(np.int64), ref.view(np.int64))
+
+
+@pytest.mark.gpu
+def test_device_transport_c2_full_strips_n4():
+    """bench.py's C2 weak-scaling layout at full per-rank size (3200 x 640 Kuhn strips, 4.1 M triangles per rank),
+    N = 4 thread ranks on one card: the end ranks take the in-place element pass, the middle ranks (two peers) the
+    split-tile default -- every rank's rows bit-identical to the whole-grid assembly, two steps."""
+    n = 4
+    grid = H.Grid.structured(H.SIMPLEX, 3200 * n, 640, LOWER, (5.0 * n, 1.0), px=n, py=1)
+    got, infos = run_device_ranks(grid, n, H.TENSOR_ISO_PER_ELEM, False, {"default": 0}, steps=2)
+    assert [i.n_peers for i in infos] == [1, 2, 2, 1]
+    ref = _single_gpu(grid, H.TENSOR_ISO_PER_ELEM, False)
+    v = got["default"]
+    assert v.shape == ref.shape and np.isfinite(v).all()
+    assert np.array_equal(v.view(np.int64), ref.view(np.int64))
+
+
+@pytest.mark.gpu
 def test_device_transport_halo_geometry():
     """HDD_SHARD_HALO_GEOMETRY: the ghost coordinates travel too (element-major coords, no vertex arrays)."""
     grid, tk, two = _layout("c4_q1", 3)
