@@ -47,9 +47,12 @@ def parse():
     ap.add_argument("--ny", type=int, default=0, help="c2: 640; c4: 1200")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU work of the baseline sample")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r04", "traffic.json"),
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r05", "traffic.json"),
                     help="PMC traffic summary (scripts/traffic_summary.py); used only when its build_id matches the "
                          "timed libhdd_amd.so")
+    ap.add_argument("--kernel-times-json", default=os.path.join(ROOT, "profiles", "r05", "kernel_times.json"),
+                    help="rocprofv3 kernel durations per workload (scripts/kernel_times.py); used only when its build_id "
+                         "matches the timed libhdd_amd.so and its kernel the dispatched one")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo = rehearsal of the N-rank path on one GPU (host-staged halo)")
     ap.add_argument("--no-overlap", action="store_true",
@@ -170,10 +173,14 @@ def main():
         raise SystemExit("--gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
     gpu = local_rank if args.backend == "nccl" else 0
     torch.cuda.set_device(gpu)
+    # N > 1: every device synchronisation runs under this deadline (hdd_amd.watchdog): a lost or stalled peer ends the
+    # rank with a report of the step stage that did not complete instead of a hang
+    deadline = float(os.environ.get("HDD_BENCH_DEADLINE", "60"))
     if world > 1:
+        import datetime
         # control plane only (barriers, the max-over-ranks timing, the RCCL id broadcast); the halo itself is
         # moved by the library (hdd_comm: RCCL send/recv, or the host-staged rehearsal transport)
-        dist.init_process_group("gloo")
+        dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=max(120.0, 2 * deadline)))
 
     c4 = args.workload == "c4"
     if c4:   # strong scaling: one 3520 x 1200 Q1 mesh, 8 x 8 subdomains, rank r owns a subdomain-column range
@@ -205,9 +212,23 @@ def main():
     nnz = shard.info.nnz
     vals = [torch.empty(nnz, dtype=torch.float64, device="cuda")]
     comm = None
+    rccl_init_s = None
     if world > 1:
+        t_init = time.perf_counter()
         comm = rccl_comm(rank, world, gpu) if args.backend == "nccl" else gloo_host_comm(gpu)
+        rccl_init_s = time.perf_counter() - t_init
+        sys.stderr.write("[bench] rank %d/%d on GPU %d: %s communicator in %.3f s, halo peers %s\n"
+                         % (rank, world, gpu, "RCCL (ncclCommInitRank)" if args.backend == "nccl" else "gloo host",
+                            rccl_init_s, [int(p) for p in shard.halo_lists()[0]]))
+        sys.stderr.flush()
     flags = H.SHARD_NO_OVERLAP if args.no_overlap else 0
+
+    def gpu_sync(what):
+        if world > 1:
+            from hdd_amd.watchdog import guarded_sync
+            guarded_sync(torch, shard, rank, what, deadline, stream=stream.cuda_stream)
+        else:
+            torch.cuda.synchronize()
 
     n_own = shard.n_own
     nbf = 4 if c4 else 3
@@ -231,6 +252,7 @@ def main():
     att = None if args.probe_last else attainable_hbm(torch)
     # the first step fills the ghost columns (NaN until then); --halo once keeps them for the timed steps
     step()
+    gpu_sync("the first step")
     if args.halo == "once":
         flags = H.SHARD_NO_HALO
     for _ in range(args.warmup):
@@ -244,6 +266,7 @@ def main():
     events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
               for _ in range(args.steps if per_step else 1)]
     if world > 1:
+        gpu_sync("the warmup steps")
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -257,10 +280,11 @@ def main():
         for k in range(args.steps):
             step(flags)
         events[0][1].record(stream)
-    torch.cuda.synchronize()
+    gpu_sync("the timed steps")
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    kernel_label = H.last_tile_kernel()
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in events])) / (1 if per_step else args.steps)
     t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64)
     if world > 1:
@@ -285,6 +309,16 @@ def main():
                     traffic_src = os.path.relpath(args.traffic_json, ROOT)
             except (OSError, ValueError, KeyError):
                 traffic = None
+        rocprof_ms, rocprof_src = None, None
+        if os.path.exists(args.kernel_times_json) and world == 1:
+            try:
+                kj = json.load(open(args.kernel_times_json))
+                ent = kj.get("workloads", {}).get("c4" if c4 else "c2", {})
+                if kj.get("build_id") == bid and ent.get("kernel") == kernel_label:
+                    rocprof_ms = ent["avg_ns"] * 1e-6
+                    rocprof_src = os.path.relpath(args.kernel_times_json, ROOT)
+            except (OSError, ValueError, KeyError):
+                rocprof_ms = None
         halo_desc = ""
         if world > 1 and args.halo == "once":
             halo_desc = ", face halo exchanged once at setup (static mesh and coefficients)"
@@ -326,16 +360,15 @@ def main():
                          "traffic_frac": (traffic / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if traffic else None,
                          "traffic_gbs": (traffic / (kernel_ms * 1e-3) / 1e9) if traffic else None,
                          "traffic_source": traffic_src, "build_id": bid,
-                         # the dominant kernel (swipdg_q1.hip / swipdg_p1.hip dispatch): C4 at one launch per step the
-                         # half-image Q1 kernel on vertex-indexed geometry; the sharded step's full-range launch skips the
-                         # ghost-adjacent row blocks (whole-tile Q1 kernel; P1: skip instantiation on in-place ranks)
-                         "kernel": ("swipdg_persistent_kernel<Q1PwcPolicy<1, 0, false, false, false>, false, true>"
-                                    if c4 and sharded_step else
-                                    "swipdg_persistent_kernel<Q1PwcPolicy<1, 0, false, true, true>, false, false>"
-                                    if c4 else
-                                    "swipdg_persistent_kernel<P1PwcPolicy<1, 0, false, true>, false, %s>"
-                                    % ("true" if sharded_step else "false")),
-                         "kernel_ms_avg": kernel_ms, "kernel_ms_avg_max_rank": kernel_ms_max,
+                         # the dominant kernel as the library's dispatch picked it in the last timed step
+                         # (hdd_last_tile_kernel, rank 0)
+                         "kernel": kernel_label,
+                         # event-timed average step on the assembly stream (one event pair around the K steps, so
+                         # dispatch gaps -- and at N > 1 the step's pack / exchange / element pass -- are included)
+                         "step_ms_event": kernel_ms, "step_ms_event_max_rank": kernel_ms_max,
+                         # the same kernel's average duration from a rocprofv3 --kernel-trace run of this build
+                         # (profiles/*/kernel_times.json, build-stamped like the traffic), else null
+                         "kernel_ms_rocprof": rocprof_ms, "kernel_ms_rocprof_source": rocprof_src,
                          "algorithmic_bytes_per_launch": alg_bytes,
                          # measured on this box in this run: device copy (read + write) and fill (write)
                          "attainable": dict(att, source="torch copy_ / fill_ of 1 GiB, HIP events"),
@@ -347,6 +380,7 @@ def main():
         }
         out["config"]["entry"] = "hdd_block_assemble_sharded (C ABI)"
         if world > 1:
+            out["config"]["comm_init_s_rank0"] = rccl_init_s
             out["config"]["halo"] = args.halo
             out["config"]["halo_elements_rank0"] = [int(shard.info.halo_send), int(shard.info.halo_recv)]
         print(json.dumps(out), flush=True)

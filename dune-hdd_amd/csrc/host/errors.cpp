@@ -18,3 +18,13 @@ int set_error(int code, const std::string& msg)
 extern "C" int hdd_abi_version(void) { return HDD_ABI_VERSION; }
 
 extern "C" const char* hdd_last_error(const hdd_ctx* /*ctx*/) { return hdd::last_error_slot().c_str(); }
+
+namespace hdd {
+const char*& last_tile_kernel_slot()
+{
+  thread_local const char* name = "";
+  return name;
+}
+}  // namespace hdd
+
+extern "C" const char* hdd_last_tile_kernel(void) { return hdd::last_tile_kernel_slot(); }

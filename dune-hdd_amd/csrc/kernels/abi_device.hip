@@ -24,7 +24,8 @@ struct hdd_ctx {
   size_t ws_bytes = 0;
   // read once at hdd_ctx_create, never per launch
   int n_cu = 256;           // hipDeviceAttributeMultiprocessorCount
-  int debug_flags = 0;      // HDD_DEBUG_FLAGS: profiling ablations only (0 in production)
+  int debug_flags = 0;      // HDD_DEBUG_FLAGS: error injection of the tests; ablation bits (HDD_ABLATION builds only)
+  uint32_t variant = 0;     // HDD_VARIANT / hdd_ctx_set_variant: verification variants (0: the default kernels)
   int wgcu = 0;             // HDD_P1_WGCU: tiles-per-CU sweep override (0: the policy's measured value)
   int q3g_reps = 0;         // HDD_Q3G_REPS: workgroups per (XCD, row quad) of the p=3 GEMM kernel (0: by CU count)
   double* q3g_tab = nullptr;   // p=3 reference matrices [Q3G_K][4096], uploaded on first use
@@ -84,6 +85,7 @@ extern "C" int hdd_ctx_create(int hip_device, hdd_ctx** out)
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, hip_device) == hipSuccess && cus > 0)
     c->n_cu = cus;
   if (const char* df = getenv("HDD_DEBUG_FLAGS")) c->debug_flags = atoi(df);
+  if (const char* v = getenv("HDD_VARIANT")) c->variant = uint32_t(strtoul(v, nullptr, 0));
   if (const char* w = getenv("HDD_P1_WGCU")) c->wgcu = std::max(0, atoi(w));
   if (const char* r = getenv("HDD_Q3G_REPS")) c->q3g_reps = std::max(0, atoi(r));
   *out = c;
@@ -94,6 +96,13 @@ extern "C" int hdd_ctx_set_debug_flags(hdd_ctx* ctx, int32_t flags)
 {
   if (!ctx) return set_error(HDD_ERR_INVALID, "hdd_ctx_set_debug_flags: null context");
   ctx->debug_flags = flags;
+  return HDD_OK;
+}
+
+extern "C" int hdd_ctx_set_variant(hdd_ctx* ctx, uint32_t variant)
+{
+  if (!ctx) return set_error(HDD_ERR_INVALID, "hdd_ctx_set_variant: null context");
+  ctx->variant = variant;
   return HDD_OK;
 }
 
@@ -217,6 +226,7 @@ static int assemble_hex(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_fn* ka
     a.sigma_boundary = p->sigma_boundary;
     a.beta = p->beta;
     a.debug_flags = ctx->debug_flags;   // profiling ablations (HDD_ABLATION builds only)
+    a.variant = ctx->variant;
     gauss_legendre01(nq1v, a.tab.sv, a.tab.wv);
     gauss_legendre01(nq1f, a.tab.sf, a.tab.wf);
     for (int r = 0; r <= deg; ++r) {
@@ -320,13 +330,14 @@ static int assemble_impl(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_fn* k
   a.fix_rb = (m->elem_type == HDD_SIMPLEX ? 3 * 3 * 4 : 4 * 4 * 5);
   if (!m->elem_vertices != !m->vertex_coords)
     return set_error(HDD_ERR_INVALID, "hdd_swipdg_assemble: mesh elem_vertices / vertex_coords: both or neither");
-  // vertex-indexed geometry (bit 16384 of HDD_DEBUG_FLAGS: A/B against the element-major coords)
-  if (m->elem_vertices && !(ctx->debug_flags & 16384)) {
+  // vertex-indexed geometry (HDD_VARIANT_ELEMENT_MAJOR: the element-major coords, cross-check)
+  if (m->elem_vertices && !(ctx->variant & HDD_VARIANT_ELEMENT_MAJOR)) {
     a.ev = m->elem_vertices;
     a.vxy = m->vertex_coords;
   }
   a.n_cu = ctx->n_cu;
   a.debug_flags = ctx->debug_flags;   // profiling ablations only
+  a.variant = ctx->variant;
   a.wgcu = ctx->wgcu;
   // integrand orders of LocalEvaluation::Elliptic / SWIPDG::Inner / BoundaryLHS at p = 1 (piecewise
   // constant tensors): volume ord(kappa); faces ord(kappa) + 2.  One kernel serves components of equal
@@ -683,8 +694,8 @@ extern "C" int hdd_pattern_elem_ptr_device(hdd_ctx* ctx, const hdd_mesh* m, int3
     ctx->scan_ws_bytes = tmp_bytes;
   }
   // nnz reaches the host through a mapped pinned word the elem_ptr kernel writes (no copy launch);
-  // HDD_DEBUG_FLAGS bit 262144: the round-3 scheme (scan launch + device-to-host copy), A/B
-  const bool legacy = (ctx->debug_flags & 262144) != 0;
+  // HDD_VARIANT_PATTERN_SCAN_COPY: the round-3 scheme (scan launch + device-to-host copy), cross-check
+  const bool legacy = (ctx->variant & HDD_VARIANT_PATTERN_SCAN_COPY) != 0;
   if (!legacy && !ctx->nnz_h && n_own > 0) {
     if ((e = hipHostMalloc(reinterpret_cast<void**>(&ctx->nnz_h), sizeof(int64_t), hipHostMallocMapped)) != hipSuccess)
       return hip_fail(e, "hdd_pattern_elem_ptr_device: pinned nnz");
@@ -833,7 +844,7 @@ extern "C" int hdd_swipdg_rhs(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_
   a.coords = m->coords;
   if (!m->elem_vertices != !m->vertex_coords)
     return set_error(HDD_ERR_INVALID, "hdd_swipdg_rhs: mesh elem_vertices / vertex_coords: both or neither");
-  if (m->elem_vertices && m->elem_type != HDD_HEX && !(ctx->debug_flags & 16384)) {
+  if (m->elem_vertices && m->elem_type != HDD_HEX && !(ctx->variant & HDD_VARIANT_ELEMENT_MAJOR)) {
     a.ev = m->elem_vertices;   // vertex-indexed geometry
     a.vxy = m->vertex_coords;
   }
@@ -852,8 +863,8 @@ extern "C" int hdd_swipdg_rhs(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_
   a.beta = p->beta;
   a.out = d_rhs;
   a.n_cu = ctx->n_cu;
-  a.generic = (ctx->debug_flags & 32768) ? 1 : 0;
-  a.no_tiny = (ctx->debug_flags & 131072) ? 1 : 0;
+  a.generic = (ctx->variant & HDD_VARIANT_RHS_GENERIC) ? 1 : 0;
+  a.no_tiny = (ctx->variant & HDD_VARIANT_RHS_NO_TINY) ? 1 : 0;
   if (force) {
     const int order = fn_order(*force) + deg;
     a.nqv = m->elem_type == HDD_SIMPLEX ? simplex_rule(order, a.qv, 64) : tensor_rule(dim, order, a.qv, 64);
@@ -871,10 +882,10 @@ extern "C" int hdd_swipdg_rhs(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_
   hipError_t e = hipSetDevice(ctx->device);
   if (e != hipSuccess) return hip_fail(e, "hdd_swipdg_rhs: hipSetDevice");
   const int64_t n_own = m->own_end - m->own_begin;
-  // split path (HDD_DEBUG_FLAGS bit 65536: the fused kernel, A/B): the list is kept in the context, allocated
+  // split path (HDD_VARIANT_RHS_FUSED: the fused kernel, cross-check): the list is kept in the context, allocated
   // (and its counters zeroed) on the first call of a size class -- warm up before hipGraph capture
   if (m->elem_type != HDD_HEX && (dirichlet || neumann) && n_own > 0 && n_own < (int64_t(1) << 31) &&
-      !(ctx->debug_flags & 65536)) {
+      !(ctx->variant & HDD_VARIANT_RHS_FUSED)) {
     const size_t bytes = hdd::dev::rhs_list_bytes(n_own);
     if (bytes > ctx->rhs_ws_bytes) {
       if (ctx->rhs_ws) {
@@ -1013,10 +1024,11 @@ extern "C" int hdd_product_assemble(hdd_ctx* ctx, const hdd_mesh* m, int32_t pro
     f.vals[0] = d_vals;
     f.n_cu = ctx->n_cu;
     f.debug_flags = ctx->debug_flags;
+    f.variant = ctx->variant;
     f.wgcu = ctx->wgcu;
     if (!m->elem_vertices != !m->vertex_coords)
       return set_error(HDD_ERR_INVALID, "hdd_product_assemble: mesh elem_vertices / vertex_coords: both or neither");
-    if (m->elem_vertices && m->elem_type == HDD_SIMPLEX && !(ctx->debug_flags & 16384)) {
+    if (m->elem_vertices && m->elem_type == HDD_SIMPLEX && !(ctx->variant & HDD_VARIANT_ELEMENT_MAJOR)) {
       f.ev = m->elem_vertices;   // vertex-indexed geometry, as hdd_swipdg_assemble
       f.vxy = m->vertex_coords;
     }

@@ -972,7 +972,7 @@ static hipError_t launch_hex_q3(const HexArgs& a, hipStream_t s)
   const int64_t n_own = a.own_end - a.own_begin;
   if (n_own <= 0) return hipSuccess;
   hipLaunchKernelGGL(hex_q3_setup_kernel, dim3(unsigned((n_own + 255) / 256)), dim3(256), 0, s, a);
-  if (a.debug_flags & 512) {   // A/B: the register-fragment MFMA kernel (operands generated per element)
+  if (a.variant & HDD_VARIANT_HEX_Q3_REGISTER) {   // the register-fragment MFMA kernel (operands generated per element)
     const int64_t grid = std::min<int64_t>(n_own, 1 << 20);
     hipLaunchKernelGGL(hex_q3_kernel, dim3(unsigned(grid)), dim3(256), 0, s, a);
     return hipGetLastError();

@@ -28,6 +28,7 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "hdd.h"
@@ -209,7 +210,22 @@ struct hdd_device_hub {
   std::string failed;                    // first protocol error (every waiting rank returns it)
   int refs = 1;
   double timeout_s = 120.0;
+  // error injection (hdd_device_hub_stall): the next post of rank `stall_rank` gates its sends behind a device-side
+  // wait for a host word (a peer whose sends never complete, bounded by stall_s), released by hdd_device_hub_release
+  int32_t stall_rank = -1;
+  double stall_s = 0.0;
+  uint32_t* gate = nullptr;              // pinned host word (device-visible): 0 = closed
 };
+
+// The injected stall: one wave spins (s_sleep between polls) until the host opens the gate or max_ticks of the
+// 100 MHz real-time counter have passed -- every launch ends by itself.
+__global__ void __launch_bounds__(64) hub_gate_kernel(const uint32_t* gate, uint64_t max_ticks)
+{
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (__hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0u &&
+         __builtin_amdgcn_s_memrealtime() - t0 < max_ticks)
+    __builtin_amdgcn_s_sleep(100);
+}
 
 static void hub_release(hdd_device_hub* h)
 {
@@ -219,7 +235,10 @@ static void hub_release(hdd_device_hub* h)
     std::lock_guard<std::mutex> lk(h->m);
     last = --h->refs == 0;
   }
-  if (last) delete h;
+  if (last) {
+    if (h->gate) (void)hipHostFree(h->gate);
+    delete h;
+  }
 }
 
 extern "C" int hdd_device_hub_create(int32_t nranks, hdd_device_hub** out)
@@ -233,6 +252,33 @@ extern "C" int hdd_device_hub_create(int32_t nranks, hdd_device_hub** out)
 }
 
 extern "C" void hdd_device_hub_destroy(hdd_device_hub* hub) { hub_release(hub); }
+
+extern "C" int hdd_device_hub_stall(hdd_device_hub* hub, int32_t rank, double max_seconds)
+{
+  if (!hub || rank < 0 || rank >= hub->nranks || !(max_seconds > 0.0) || max_seconds > 600.0)
+    return set_error(HDD_ERR_INVALID, "hdd_device_hub_stall: invalid argument");
+  std::lock_guard<std::mutex> lk(hub->m);
+  if (!hub->gate) {
+    const hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&hub->gate), 64, hipHostMallocMapped | hipHostMallocCoherent);
+    if (e != hipSuccess) {
+      hub->gate = nullptr;
+      return hip_fail(e, "hdd_device_hub_stall: gate word");
+    }
+  }
+  __atomic_store_n(hub->gate, 0u, __ATOMIC_SEQ_CST);
+  hub->stall_rank = rank;
+  hub->stall_s = max_seconds;
+  return HDD_OK;
+}
+
+extern "C" int hdd_device_hub_release(hdd_device_hub* hub)
+{
+  if (!hub) return set_error(HDD_ERR_INVALID, "hdd_device_hub_release: null hub");
+  std::lock_guard<std::mutex> lk(hub->m);
+  if (hub->gate) __atomic_store_n(hub->gate, 1u, __ATOMIC_SEQ_CST);
+  hub->stall_rank = -1;
+  return HDD_OK;
+}
 
 // ------------------------------------------------------------------------------------------------
 // communicators
@@ -251,6 +297,8 @@ struct hdd_comm {
   hdd_device_hub* hub = nullptr;       // DEVICE: the hub, this rank, one "copied" event per source rank
   int32_t rank = 0;
   std::vector<hipEvent_t> copied;
+  hipEvent_t gated = nullptr;          // DEVICE, injected stall: the sends' event behind the gate
+  std::vector<int32_t> last_peers;     // the peers of the last post (watchdog messages)
 };
 
 static int comm_rccl_streams(hdd_comm* c)
@@ -368,6 +416,7 @@ extern "C" void hdd_comm_destroy(hdd_comm* c)
   if (c->done) (void)hipEventDestroy(c->done);
   for (hipEvent_t ev : c->copied)
     if (ev) (void)hipEventDestroy(ev);
+  if (c->gated) (void)hipEventDestroy(c->gated);
   if (c->xfer) (void)hipStreamDestroy(c->xfer);
   if (c->pinned) (void)hipHostFree(c->pinned);
   hub_release(c->hub);
@@ -401,12 +450,29 @@ static int device_post(hdd_comm* c, int32_t n_peers, const int32_t* peers, const
     H.cv.notify_all();
     return set_error(HDD_ERR_INVALID, "hdd_comm_post (device transport): " + msg);
   };
-  {   // 1. publish (c->ready was recorded on the pack stream by the caller)
+  hipEvent_t packed_ev = c->ready;   // recorded on the pack stream by the caller; the transfer stream waits for it
+  {
+    std::lock_guard<std::mutex> lk(H.m);
+    if (H.stall_rank == me && H.gate) {   // injected stall: the sends complete only once the gate opens
+      if (!c->gated && hipEventCreateWithFlags(&c->gated, hipEventDisableTiming) != hipSuccess) c->gated = nullptr;
+      uint32_t* dgate = nullptr;
+      hipError_t e = c->gated ? hipHostGetDevicePointer(reinterpret_cast<void**>(&dgate), H.gate, 0) : hipErrorOutOfMemory;
+      if (e == hipSuccess) {
+        hipLaunchKernelGGL(hub_gate_kernel, dim3(1), dim3(64), 0, c->xfer, dgate, uint64_t(H.stall_s * 1.0e8));
+        e = hipGetLastError();
+      }
+      if (e == hipSuccess) e = hipEventRecord(c->gated, c->xfer);
+      if (e != hipSuccess) return hip_fail(e, "hdd_comm_post: injected stall (device transport)");
+      packed_ev = c->gated;
+      H.stall_rank = -1;   // one post
+    }
+  }
+  {   // 1. publish
     std::lock_guard<std::mutex> lk(H.m);
     for (auto& [dst, msgs] : out) {
       auto& q = H.ch[size_t(me) * n + dst];
       q.msgs = msgs;
-      q.packed = c->ready;
+      q.packed = packed_ev;
       ++q.sent;
     }
   }
@@ -470,6 +536,10 @@ extern "C" int hdd_comm_post(hdd_comm* c, int32_t n_peers, const int32_t* peers,
   const hipStream_t s = static_cast<hipStream_t>(stream);
   hipError_t e = hipSetDevice(c->device);
   if (e != hipSuccess) return hip_fail(e, "hdd_comm_post: hipSetDevice");
+  c->last_peers.clear();
+  for (int32_t k = 0; k < n_peers; ++k)
+    if (std::find(c->last_peers.begin(), c->last_peers.end(), peers[k]) == c->last_peers.end())
+      c->last_peers.push_back(peers[k]);
   if (c->kind != hdd_comm::HOST) {
     // the transfer stream starts after the packs already enqueued on `stream`
     e = hipEventRecord(c->ready, s);
@@ -599,6 +669,11 @@ struct hdd_shard {
   hipEvent_t ev_in = nullptr, ev_out = nullptr;
   double* d_fixbuf = nullptr;          // side buffers of the off-stream fixup (n_comp x (n_fix + 1) x fix_rb)
   size_t fixbuf_doubles = 0;
+  // watchdog (hdd_block_step_query / _sync): the stages the last step recorded events for, and a marker event
+  uint32_t stages = 0;                 // bit 0: pack (comm->ready), 1: exchange (comm->done), 2: element pass (ev_out)
+  const hdd_comm* stage_comm = nullptr;
+  hipEvent_t ev_mark = nullptr;
+  bool marked = false;
 };
 
 extern "C" void hdd_shard_destroy(hdd_shard* sh)
@@ -608,6 +683,7 @@ extern "C" void hdd_shard_destroy(hdd_shard* sh)
   if (sh->aux) (void)hipStreamDestroy(sh->aux);
   if (sh->ev_in) (void)hipEventDestroy(sh->ev_in);
   if (sh->ev_out) (void)hipEventDestroy(sh->ev_out);
+  if (sh->ev_mark) (void)hipEventDestroy(sh->ev_mark);
   for (void* p : {static_cast<void*>(sh->d_coords), static_cast<void*>(sh->d_nbrs), static_cast<void*>(sh->d_finfo),
                   static_cast<void*>(sh->d_gid), static_cast<void*>(sh->d_send_idx), static_cast<void*>(sh->d_sbuf),
                   static_cast<void*>(sh->d_rbuf), static_cast<void*>(sh->d_tiles_in),
@@ -914,6 +990,9 @@ extern "C" int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm*
 
   hipError_t e = hipSetDevice(sh->device);
   if (e != hipSuccess) return hip_fail(e, "hdd_block_assemble_sharded: hipSetDevice");
+  sh->stages = 0;
+  sh->stage_comm = comm;
+  sh->marked = false;
   // Default schedule by element type and peer count (one-card step study, profiles/r04/e_reserve/): P1 ranks with
   // two peers split the tiles -- interior tiles during the exchange, the 2 % of tiles with a ghost-adjacent element
   // after it (C2 N = 8 middle rank +0.8 / +4.0 % over one launch, against +10.1 % for the side-buffer fixup and
@@ -934,7 +1013,11 @@ extern "C" int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm*
   // host runs ahead, are unchanged).  HDD_SHARD_LAUNCH_LAST: round 3's order.  The split keeps its pack on `stream`
   // before the interior tiles: packing on the side stream beside them measured +10.0 % against +5.3 % (C2 N = 8
   // middle rank, back-to-back, profiles/r04/o_final/).
+#ifdef HDD_ABLATION
   const bool last = (flags & HDD_SHARD_LAUNCH_LAST) != 0;
+#else
+  const bool last = false;   // (HDD_SHARD_LAUNCH_LAST: ablation builds only)
+#endif
   const bool side = overlap && !split;
   if (side) {
     if (transfer && comm->kind != hdd_comm::HOST) {
@@ -1020,6 +1103,7 @@ extern "C" int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm*
       }
     }
     rc = hdd_comm_post(comm, int32_t(mp.size()), mp.data(), ms.data(), mn.data(), mr.data(), mrn.data(), ps);
+    if (rc == HDD_OK && comm->kind != hdd_comm::HOST) sh->stages |= 3u;
     // host transport on the side stream, fixup on `stream`: the ghost columns were written on ps
     if (rc == HDD_OK && side && !offfix && ps != s && comm->kind == hdd_comm::HOST &&
         hipEventRecord(sh->ev_out, ps) != hipSuccess)
@@ -1068,6 +1152,7 @@ extern "C" int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm*
     e = hipEventRecord(sh->ev_out, ps);
     if (e != hipSuccess) return hip_fail(e, "hdd_block_assemble_sharded: record fixup");
     fix_pending = true;
+    sh->stages |= 4u;
   }
   // 3. the assembly overlaps the transfer.  Default: EVERY tile (one full-size launch at full rate; the row
   // blocks of the ghost-adjacent elements read ghost columns the receives are still writing and are recomputed
@@ -1120,4 +1205,71 @@ extern "C" int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm*
     if (rc != HDD_ERR_UNSUPPORTED) return rc;   // (no list kernel for these rules: the whole range again)
   }
   return hdd_swipdg_assemble(ctx, &m, kappa, n_comp, tensor, params, pattern, d_vals, stream);
+}
+
+// ------------------------------------------------------------------------------------------------
+// watchdog: which stage of the last sharded step has not completed.  A lost peer shows as a step that never
+// completes on the device (RCCL waits inside its kernels), so a caller that would block in a device synchronize
+// can instead poll these events with a deadline and report the rank and stage before exiting.
+// ------------------------------------------------------------------------------------------------
+static const char* const stage_names[] = {"complete", "halo pack", "halo exchange (group send/recv)",
+                                          "ghost-adjacent element pass", "tile assembly and join"};
+
+extern "C" int hdd_block_step_mark(hdd_shard* sh, void* stream)
+{
+  if (!sh || sh->host_only) return set_error(HDD_ERR_INVALID, "hdd_block_step_mark: invalid shard");
+  hipError_t e = hipSetDevice(sh->device);
+  if (e == hipSuccess && !sh->ev_mark) e = hipEventCreateWithFlags(&sh->ev_mark, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventRecord(sh->ev_mark, static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(e, "hdd_block_step_mark");
+  sh->marked = true;
+  return HDD_OK;
+}
+
+extern "C" int hdd_block_step_query(hdd_shard* sh, int32_t* stage)
+{
+  if (!sh || !stage || sh->host_only) return set_error(HDD_ERR_INVALID, "hdd_block_step_query: invalid argument");
+  const hdd_comm* c = sh->stage_comm;
+  const hipEvent_t evs[4] = {(sh->stages & 1u) && c ? c->ready : nullptr, (sh->stages & 2u) && c ? c->done : nullptr,
+                             (sh->stages & 4u) ? sh->ev_out : nullptr, sh->marked ? sh->ev_mark : nullptr};
+  *stage = HDD_STAGE_COMPLETE;
+  for (int i = 0; i < 4; ++i) {
+    if (!evs[i]) continue;
+    const hipError_t e = hipEventQuery(evs[i]);
+    if (e == hipErrorNotReady) {
+      *stage = i + 1;
+      return HDD_OK;
+    }
+    if (e != hipSuccess) return hip_fail(e, "hdd_block_step_query");
+  }
+  return HDD_OK;
+}
+
+extern "C" const char* hdd_block_stage_name(int32_t stage)
+{
+  return stage >= 0 && stage <= HDD_STAGE_ASSEMBLY ? stage_names[stage] : "unknown stage";
+}
+
+extern "C" int hdd_block_step_sync(hdd_shard* sh, void* stream, double timeout_s)
+{
+  int rc = hdd_block_step_mark(sh, stream);
+  if (rc) return rc;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    int32_t st = 0;
+    rc = hdd_block_step_query(sh, &st);
+    if (rc) return rc;
+    if (st == HDD_STAGE_COMPLETE) return HDD_OK;
+    const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (dt > timeout_s) {
+      std::string peers;
+      if (sh->stage_comm)
+        for (int32_t p : sh->stage_comm->last_peers) peers += (peers.empty() ? "" : ", ") + std::to_string(p);
+      return set_error(HDD_ERR_TIMEOUT, "rank " + std::to_string(sh->rank) + " of " + std::to_string(sh->nranks) +
+                                            ": the sharded step's " + stage_names[st] + " did not complete within " +
+                                            std::to_string(timeout_s) + " s (halo peers: " +
+                                            (peers.empty() ? "none" : peers) + ")");
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(dt < 0.01 ? 20 : 1000));
+  }
 }

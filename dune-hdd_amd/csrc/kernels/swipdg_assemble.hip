@@ -10,9 +10,9 @@ namespace dev {
 static hipError_t launch_components(const AssembleArgs& a, int nqv, int nqf, hipStream_t s, bool* supported)
 {
   // C3: sinusoid components sharing one phase (OS2014's affine part and mu-component) -> one fused launch that
-  // evaluates the sines once per element (P1, vertex-indexed geometry; HDD_DEBUG_FLAGS bit 4096: per component)
+  // evaluates the sines once per element (P1, vertex-indexed geometry; HDD_VARIANT_C3_PER_COMPONENT: per component)
   if (a.elem_type == HDD_SIMPLEX && nqv == 6 && nqf == 3 && a.ev && a.n_comp > 1 &&
-      !(a.debug_flags & 4096)) {
+      !(a.variant & HDD_VARIANT_C3_PER_COMPONENT)) {
     bool same = true;
     for (int c = 0; c < a.n_comp; ++c)
       same = same && a.kappa[c].kind == HDD_FN_SINUSOID && a.kappa[c].kx == a.kappa[0].kx &&
@@ -72,7 +72,7 @@ int face_points(int order)
 hipError_t launch_assemble(const AssembleArgs& a, int nqv, int nqf, hipStream_t s, bool* supported)
 {
   *supported = true;
-  if (!(a.debug_flags & 64)) {
+  if (!(a.variant & HDD_VARIANT_WAVE_PER_ROW)) {
     const hipError_t e = launch_components(a, nqv, nqf, s, supported);
     if (*supported || a.tile_list || a.skip_ghost) return e;
     *supported = true;   // fall through to the wave-per-row kernels for the remaining rules

@@ -27,9 +27,11 @@
 #include <cstdint>
 #include <algorithm>
 #include <cstdlib>
+#include <string>
 #include <type_traits>
 
 #include "hdd.h"
+#include "hdd_internal.hh"
 #include "swipdg_kernels.hh"
 #include "flattop.hh"
 #include "trig_phase.hh"
@@ -1171,16 +1173,14 @@ struct Q1PwcPolicy : GenericPolicy<Cube, 1, 2, TK, KK, VX> {
                   : ((k & 2) ? 1.0 : -1.0) * ((k & 1) ? x : 1.0 - x);
   }
 
-  template <class IMG>
-  __device__ static void compute(const AssembleArgs& a, int64_t e, const Own& o, const Gat& gt, IMG img)
+  // Canonical register order of one element's values: V[i * VR + b * NB + c], row i, block b (0: the element
+  // itself, column c = basis j; 1 + f: the neighbour across face f, column c = role r).  VR = 20 values per row.
+  static constexpr int VR = (NF + 1) * NB, NV80 = NB * VR;
+
+  // block positions inside the element's row block (blocks sorted by element id): the element's own, face f's
+  __device__ static void positions(int64_t e, const Own& o, int& pos_self, int* pos)
   {
-    const double j00 = o.X[1] - o.X[0], j01 = o.X[2] - o.X[0], j10 = o.Y[1] - o.Y[0], j11 = o.Y[2] - o.Y[0];
-    const double det = j00 * j11 - j01 * j10;
-    const double id = rcp_nr(det);
-    const double i00 = j11 * id, i01 = -j01 * id, i10 = -j10 * id, i11 = j00 * id;   // J^{-1}
-    const double adet = fabs(det);
-    const double osgn = det > 0.0 ? 1.0 : -1.0;
-    int pos_self = 0, pos[NF];
+    pos_self = 0;
 #pragma unroll
     for (int f = 0; f < NF; ++f) pos_self += (o.nbr[f] >= 0 && o.nbr[f] < e);
 #pragma unroll
@@ -1190,7 +1190,37 @@ struct Q1PwcPolicy : GenericPolicy<Cube, 1, 2, TK, KK, VX> {
       for (int q = 0; q < NF; ++q) p += (o.nbr[q] >= 0 && o.nbr[q] < o.nbr[f]);
       pos[f] = p;
     }
+  }
+
+  // the element's row block into an LDS image (row length (1 + interior faces) * NB, blocks sorted by element id)
+  template <class IMG>
+  __device__ static void compute(const AssembleArgs& a, int64_t e, const Own& o, const Gat& gt, IMG img)
+  {
+    int pos_self, pos[NF];
+    positions(e, o, pos_self, pos);
     const int rowlen = (Base::n_interior(o) + 1) * NB;
+    emit(a, o, gt, [&](int b, const double (&blk)[NB][NB]) {
+      if (b > 0 && o.nbr[b - 1] < 0) return;
+#pragma unroll
+      for (int i = 0; i < NB; ++i)
+#pragma unroll
+        for (int c = 0; c < NB; ++c)
+          img[i * rowlen + (b == 0 ? pos_self * NB + c : pos[b - 1] * NB + role_slot<E>(o.finfo, b - 1, c))] = blk[i][c];
+    });
+  }
+
+  // The closed forms.  sink(b, blk) receives the row block one 4 x 4 block at a time, blk[i][c] = row i, column c: the
+  // neighbour blocks face by face (b = 1 + f, column c = role r; called for every face in uniform control flow,
+  // zeros when face f has no neighbour), the element's own block last (b = 0, column c = basis j).
+  template <class SINK>
+  __device__ static void emit(const AssembleArgs& a, const Own& o, const Gat& gt, SINK&& sink)
+  {
+    const double j00 = o.X[1] - o.X[0], j01 = o.X[2] - o.X[0], j10 = o.Y[1] - o.Y[0], j11 = o.Y[2] - o.Y[0];
+    const double det = j00 * j11 - j01 * j10;
+    const double id = rcp_nr(det);
+    const double i00 = j11 * id, i01 = -j01 * id, i10 = -j10 * id, i11 = j00 * id;   // J^{-1}
+    const double adet = fabs(det);
+    const double osgn = det > 0.0 ? 1.0 : -1.0;
     const Tensor A = o.A;
     const double ke = o.ke;
     double S[NB][NB];
@@ -1211,84 +1241,85 @@ struct Q1PwcPolicy : GenericPolicy<Cube, 1, 2, TK, KK, VX> {
 #pragma unroll
     for (int f = 0; f < NF; ++f) {
       const int32_t n = o.nbr[f];
-      if (n <= HDD_NBR_NEUMANN) continue;
-      const int fa = E::fv(f, 0), fb = E::fv(f, 1);
-      const double ax = E::rv(fa, 0), ay = E::rv(fa, 1), bx = E::rv(fb, 0), by = E::rv(fb, 1);
-      const double Ax = o.X[fa], Ay = o.Y[fa], Bx = o.X[fb], By = o.Y[fb];
-      const double tx = Bx - Ax, ty = By - Ay;
-      const double il = rsq_nr(tx * tx + ty * ty);
-      const double len = (tx * tx + ty * ty) * il;
-      const double nsc = E::face_sign(f) * osgn * il;
-      const double nx = ty * nsc, ny = -tx * nsc;
-      const double anx = A.a00 * nx + A.a01 * ny, any = A.a01 * nx + A.a11 * ny;
-      const double dm = anx * nx + any * ny;
-      const double ihp = a.beta == 1.0 ? il : inv_pow(len, a.beta);
-      const double mx = i00 * anx + i01 * any, my = i10 * anx + i11 * any;   // J^{-1} A n
-      double al[NB], be[NB];   // (A grad phi_k . n) at my face vertices a, b
+      double EN[NB][NB];
 #pragma unroll
-      for (int k = 0; k < NB; ++k) {
-        al[k] = gh(k, 0, ax, ay) * mx + gh(k, 1, ax, ay) * my;
-        be[k] = gh(k, 0, bx, by) * mx + gh(k, 1, bx, by) * my;
-      }
-      const double L3 = len * (1.0 / 3.0), L6 = len * (1.0 / 6.0);
-      // int (A grad phi_j . n) phi_i  and  int phi_i phi_j
-      auto I1 = [&](int j, int i) { return i == fa ? L3 * al[j] + L6 * be[j] : (i == fb ? L6 * al[j] + L3 * be[j] : 0.0); };
-      auto MM = [&](int i, int j) {
-        return (i == fa || i == fb) && (j == fa || j == fb) ? (i == j ? L3 : L6) : 0.0;
-      };
-      if (n >= 0) {
-        const double Cx = gt.Cx[f], Cy = gt.Cy[f];
-        const Tensor Ap = gt.Ap[f];
-        const double kn = gt.kn[f];
-        // neighbour in role coordinates: A = (0,0), B = (1,0), C = (0,1)
-        const double h00 = Bx - Ax, h01 = Cx - Ax, h10 = By - Ay, h11 = Cy - Ay;
-        const double hid = rcp_nr(h00 * h11 - h01 * h10);
-        const double anpx = Ap.a00 * nx + Ap.a01 * ny, anpy = Ap.a01 * nx + Ap.a11 * ny;
-        const double dp = anpx * nx + anpy * ny;
-        const double mpx = (h11 * anpx - h01 * anpy) * hid, mpy = (-h10 * anpx + h00 * anpy) * hid;
-        double alp[NB], bep[NB];   // (A+ grad phi+_r . n) at A (0,0) and B (1,0)
+      for (int i = 0; i < NB; ++i)
 #pragma unroll
-        for (int r = 0; r < NB; ++r) {
-          alp[r] = gh(r, 0, 0.0, 0.0) * mpx + gh(r, 1, 0.0, 0.0) * mpy;
-          bep[r] = gh(r, 0, 1.0, 0.0) * mpx + gh(r, 1, 1.0, 0.0) * mpy;
+        for (int r = 0; r < NB; ++r) EN[i][r] = 0.0;
+      if (n > HDD_NBR_NEUMANN) {
+        const int fa = E::fv(f, 0), fb = E::fv(f, 1);
+        const double ax = E::rv(fa, 0), ay = E::rv(fa, 1), bx = E::rv(fb, 0), by = E::rv(fb, 1);
+        const double Ax = o.X[fa], Ay = o.Y[fa], Bx = o.X[fb], By = o.Y[fb];
+        const double tx = Bx - Ax, ty = By - Ay;
+        const double il = rsq_nr(tx * tx + ty * ty);
+        const double len = (tx * tx + ty * ty) * il;
+        const double nsc = E::face_sign(f) * osgn * il;
+        const double nx = ty * nsc, ny = -tx * nsc;
+        const double anx = A.a00 * nx + A.a01 * ny, any = A.a01 * nx + A.a11 * ny;
+        const double dm = anx * nx + any * ny;
+        const double ihp = a.beta == 1.0 ? il : inv_pow(len, a.beta);
+        const double mx = i00 * anx + i01 * any, my = i10 * anx + i11 * any;   // J^{-1} A n
+        double al[NB], be[NB];   // (A grad phi_k . n) at my face vertices a, b
+#pragma unroll
+        for (int k = 0; k < NB; ++k) {
+          al[k] = gh(k, 0, ax, ay) * mx + gh(k, 1, ax, ay) * my;
+          be[k] = gh(k, 0, bx, by) * mx + gh(k, 1, bx, by) * my;
         }
-        const double rs = rcp_nr(dp + dm);
-        const double gamma = (dp * dm) * rs;
-        const double w_plus = dm * rs, w_minus = dp * rs;
-        const double pen = (ke * kn * a.sigma_inner * gamma) * ihp;
-        constexpr double CS = PEN ? 0.0 : 1.0;
-        const double cs = -w_minus * ke * CS, cp = -w_plus * kn * CS, cm = w_minus * ke * CS;
-#pragma unroll
-        for (int i = 0; i < NB; ++i)
-#pragma unroll
-          for (int j = 0; j < NB; ++j) S[i][j] += cs * (I1(j, i) + I1(i, j)) + pen * MM(i, j);
-        int slot[NB];
-#pragma unroll
-        for (int r = 0; r < NB; ++r) slot[r] = role_slot<E>(o.finfo, f, r);
-#pragma unroll
-        for (int i = 0; i < NB; ++i) {
-          // int phi+_r phi_i: phi+_A = 1 - s, phi+_B = s (roles 0, 1); int phi+_r (A grad phi_i . n) likewise
-          const double pi = i == fa ? L3 : (i == fb ? L6 : 0.0), qi = i == fa ? L6 : (i == fb ? L3 : 0.0);
+        const double L3 = len * (1.0 / 3.0), L6 = len * (1.0 / 6.0);
+        // int (A grad phi_j . n) phi_i  and  int phi_i phi_j
+        auto I1 = [&](int j, int i) { return i == fa ? L3 * al[j] + L6 * be[j] : (i == fb ? L6 * al[j] + L3 * be[j] : 0.0); };
+        auto MM = [&](int i, int j) {
+          return (i == fa || i == fb) && (j == fa || j == fb) ? (i == j ? L3 : L6) : 0.0;
+        };
+        if (n >= 0) {
+          const double Cx = gt.Cx[f], Cy = gt.Cy[f];
+          const Tensor Ap = gt.Ap[f];
+          const double kn = gt.kn[f];
+          // neighbour in role coordinates: A = (0,0), B = (1,0), C = (0,1)
+          const double h00 = Bx - Ax, h01 = Cx - Ax, h10 = By - Ay, h11 = Cy - Ay;
+          const double hid = rcp_nr(h00 * h11 - h01 * h10);
+          const double anpx = Ap.a00 * nx + Ap.a01 * ny, anpy = Ap.a01 * nx + Ap.a11 * ny;
+          const double dp = anpx * nx + anpy * ny;
+          const double mpx = (h11 * anpx - h01 * anpy) * hid, mpy = (-h10 * anpx + h00 * anpy) * hid;
+          double alp[NB], bep[NB];   // (A+ grad phi+_r . n) at A (0,0) and B (1,0)
 #pragma unroll
           for (int r = 0; r < NB; ++r) {
-            const double anr = pi * alp[r] + qi * bep[r];
-            const double ai = r == 0 ? L3 * al[i] + L6 * be[i] : (r == 1 ? L6 * al[i] + L3 * be[i] : 0.0);
-            const double mr = r == 0 ? pi : (r == 1 ? qi : 0.0);
-            img[i * rowlen + pos[f] * NB + slot[r]] = cp * anr + cm * ai - pen * mr;
+            alp[r] = gh(r, 0, 0.0, 0.0) * mpx + gh(r, 1, 0.0, 0.0) * mpy;
+            bep[r] = gh(r, 0, 1.0, 0.0) * mpx + gh(r, 1, 1.0, 0.0) * mpy;
           }
+          const double rs = rcp_nr(dp + dm);
+          const double gamma = (dp * dm) * rs;
+          const double w_plus = dm * rs, w_minus = dp * rs;
+          const double pen = (ke * kn * a.sigma_inner * gamma) * ihp;
+          constexpr double CS = PEN ? 0.0 : 1.0;
+          const double cs = -w_minus * ke * CS, cp = -w_plus * kn * CS, cm = w_minus * ke * CS;
+#pragma unroll
+          for (int i = 0; i < NB; ++i)
+#pragma unroll
+            for (int j = 0; j < NB; ++j) S[i][j] += cs * (I1(j, i) + I1(i, j)) + pen * MM(i, j);
+#pragma unroll
+          for (int i = 0; i < NB; ++i) {
+            // int phi+_r phi_i: phi+_A = 1 - s, phi+_B = s (roles 0, 1); int phi+_r (A grad phi_i . n) likewise
+            const double pi = i == fa ? L3 : (i == fb ? L6 : 0.0), qi = i == fa ? L6 : (i == fb ? L3 : 0.0);
+#pragma unroll
+            for (int r = 0; r < NB; ++r) {
+              const double anr = pi * alp[r] + qi * bep[r];
+              const double ai = r == 0 ? L3 * al[i] + L6 * be[i] : (r == 1 ? L6 * al[i] + L3 * be[i] : 0.0);
+              const double mr = r == 0 ? pi : (r == 1 ? qi : 0.0);
+              EN[i][r] = cp * anr + cm * ai - pen * mr;
+            }
+          }
+        } else {   // Dirichlet: SWIPDG::BoundaryLHS
+          const double pen = (a.sigma_boundary * ke * dm) * ihp;
+#pragma unroll
+          for (int i = 0; i < NB; ++i)
+#pragma unroll
+            for (int j = 0; j < NB; ++j) S[i][j] += -ke * (PEN ? 0.0 : 1.0) * (I1(j, i) + I1(i, j)) + pen * MM(i, j);
         }
-      } else {   // Dirichlet: SWIPDG::BoundaryLHS
-        const double pen = (a.sigma_boundary * ke * dm) * ihp;
-#pragma unroll
-        for (int i = 0; i < NB; ++i)
-#pragma unroll
-          for (int j = 0; j < NB; ++j) S[i][j] += -ke * (PEN ? 0.0 : 1.0) * (I1(j, i) + I1(i, j)) + pen * MM(i, j);
-      }
+      }   // a neighbour or Dirichlet
+      sink(1 + f, EN);
     }
-#pragma unroll
-    for (int i = 0; i < NB; ++i)
-#pragma unroll
-      for (int j = 0; j < NB; ++j) img[i * rowlen + pos_self * NB + j] = S[i][j];
+    sink(0, S);
   }
 };
 
@@ -1762,12 +1793,11 @@ swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
   constexpr int RB = P::RB;
   constexpr int IMG = image_blocks<P>() * RB;
   constexpr int STORES = (IMG / 2 + 63) / 64;
-  static_assert(!HALF || (P::PAD && !FUSED && (P::NB * P::NB) % 2 == 0), "half images: padded even-block policies");
+  static_assert(!HALF || (P::PAD && !FUSED && RB == 80), "half images: the Q1 closed-form policy");
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const int lane = threadIdx.x;
   const int64_t G = gridDim.x, b = blockIdx.x;
   int64_t t, t_end, t_step;
-  int64_t rs0 = 0, rlen = 0, rot = 0;   // (study: rotated XCD sweeps)
   if (G >= n_tiles) {
     t = b; t_end = b + 1; t_step = 1;
   } else {   // XCD-aware: the 8 XCDs sweep contiguous eighths of the tile range
@@ -1783,11 +1813,6 @@ swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
       t = s0 + w;
       t_end = s1;
       t_step = gx;
-      if (a.debug_flags & 67108864) {   // study: XCD x starts its sweep x/8 into its eighth (and wraps)
-        rs0 = s0;
-        rlen = s1 - s0;
-        rot = (rlen * x) / 8;
-      }
     }
   }
   if (t >= t_end) return;
@@ -1800,12 +1825,23 @@ swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
   // Tile list (interior / halo-boundary split of a sharded assembly): position -> tile.
   auto tile_raw = [&](int64_t pos) -> int64_t {
     if constexpr (TL) return int64_t(a.tile_list[pos]);
-    if (rot) {
-      const int64_t q = pos - rs0 + rot;
-      return rs0 + (q < rlen ? q : q - rlen);
-    }
     return pos;
   };
+  // Full uniform tiles of HALF policies (see the HALF branch below): tile-invariant LDS byte addresses of the lane's
+  // two row bases (writer) and of its chunks 0..4 (reader; chunk k + 5 j lies 5120 j bytes further)
+  [[maybe_unused]] uint32_t hrow[2] = {0u, 0u}, hrd[5] = {0u, 0u, 0u, 0u, 0u};
+  if constexpr (HALF) {
+    const int m = lane & 31, hi = lane >> 5;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) hrow[i] = uint32_t(m * RB + 20 * ((i + 2 * hi + ((m & 7) >> 1)) & 3)) * 8u;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      const int c = lane + 64 * k, mc = c / 40, u = c % 40, r = u / 10, x = 2 * (u % 10);
+      const int rot2 = 2 * (mc & 1), rho = (mc & 7) >> 1;
+      const int w = x + rot2;
+      hrd[k] = uint32_t(mc * RB + 20 * ((r + rho) & 3) + (w >= 20 ? w - 20 : w)) * 8u;
+    }
+  }
   auto uni64 = [](int64_t v) -> int64_t { return __builtin_amdgcn_readfirstlane(v); };
   auto elem_of_tile = [&](int64_t tile) {
     const int64_t t0 = a.own_begin + tile * 64;
@@ -1867,14 +1903,112 @@ swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
     const bool uni = P::PAD && tlen == RB * int(a.own_end - t0 < 64 ? a.own_end - t0 : 64);   // wave-uniform
     typename P::Gat gat_n;
     if constexpr (HALF) {
-      // Half images: lanes 0-31 build their row blocks in the 20 KB image and the wave streams that CSR range
-      // [base, base + len0) out, then lanes 32-63 theirs, [base + len0, tile_end).  Each half is the row blocks
-      // of 32 consecutive elements, so both ranges are contiguous; with even row blocks (Q1: multiples of 16
-      // values, base even) every range starts and ends on a 16-byte boundary.  The LDS writes of the second
-      // half follow the first half's LDS reads in the wave's in-order LDS queue.
-      constexpr int STH = IMG / 128;   // 16-byte chunks per lane per half
+      // Half images (Q1): the tile's row blocks reach HBM in two halves, elements 0-31 and then 32-63, each half's
+      // 32 row blocks staged in a 20 KB LDS image and streamed out as one contiguous CSR range ([base, base + len0),
+      // then [base + len0, tile_end); Q1 row blocks are multiples of 16 values and base is even, so both ranges are
+      // 16-byte aligned).  20 KB images fit 8 tiles per CU: two waves per SIMD at <= 256 registers.
+      //
+      // Every lane computes its element's 80 values ONCE, into registers (all 64 lanes busy), and
+      // v_permlane32_swap regroups them by half: afterwards V[0..39] hold, in lanes 0-31, rows 0-1 of elements
+      // 0-31 and, in lanes 32-63, rows 2-3 of elements 0-31 (lane l - 32's); V[40..79] the same for elements 32-63.
+      // So a half's image takes 40 full-width ds_write_b64, and no element is computed twice (round 4 computed each
+      // half under a 32-lane exec mask: +57 % VALU instructions for the same output).  The placement of
+      // a value (row offsets, column offsets, which blocks exist) is computed by the lane that owns the element and
+      // swapped the same way.
+      //
+      // Full uniform tiles (64 elements with four interior faces each: the bulk of a mesh) use a rotated image:
+      // element m of the half, value (row r, column x) of its row block at
+      //   m * 80 + 20 ((r + rho_m) & 3) + ((x + rot_m) mod 20),  rot_m = 2 (m & 1), rho_m = (m & 7) >> 1,
+      // so the 16 lanes of a ds_write_b64 group (elements m and m + 8 share (rot, rho)) hit 8 distinct 8-byte bank
+      // pairs for every (r, x): 2-way, the floor while value pairs stay 16-byte aligned for the reader (an
+      // exhaustive search over per-element (row, column) rotations; rotating columns alone mod 20 gives at most 4
+      // conflict-free elements).  Other tiles (partial, boundary elements, sharded SKIP tiles) use the contiguous
+      // image (CSR order) with per-block predicates.
+      constexpr int STH = IMG / 128;   // 16-byte chunks per lane per half (20)
+      constexpr int NH = P::NV80 / 2;  // values per lane per half (40)
       const int nact = int(a.own_end - t0 < 64 ? a.own_end - t0 : 64);
-      const int len0 = nact > 32 ? __builtin_amdgcn_readlane(off, 32) : tlen;
+      const bool full = uni && nact == 64 && !(SKIP && gmask);   // wave-uniform
+      int ps, pf[P::NF];
+      P::positions(e, own, ps, pf);
+      // column byte offsets of the lane's own element: (x + rot) mod 20 (rotated image) or x (contiguous), x = block
+      // position * 4 + column; 8 bits each, four per register
+      const int rot2 = full ? 2 * (lane & 1) : 0;
+      auto col8 = [&](int x) {
+        const int w = x + rot2;
+        return uint32_t(w >= P::VR ? w - P::VR : w) * 8u;
+      };
+      uint32_t W0[P::VR / 4], W1[P::VR / 4];
+#pragma unroll
+      for (int g = 0; g < P::VR / 4; ++g) {
+        uint32_t w = 0;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int q = 4 * g + s, b = q / P::NB, c = q % P::NB;
+          const int x = b == 0 ? ps * P::NB + c : pf[b - 1] * P::NB + role_slot<Cube>(own.finfo, b - 1, c);
+          w |= col8(x) << (8 * s);
+        }
+        W0[g] = w;
+      }
+      // contiguous image: the element block's byte offset in the tile image, the row length in bytes, and which of
+      // its blocks exist (bit 0: the element is active, bit 1 + f: face f has a neighbour)
+      uint32_t ob0 = uint32_t(off) * 8u, rl0 = uint32_t(P::NB * (P::n_interior(own) + 1)) * 8u, pk0 = active ? 1u : 0u;
+#pragma unroll
+      for (int f = 0; f < P::NF; ++f) pk0 |= (active && own.nbr[f] >= 0 ? 2u : 0u) << f;
+      // the element a lane writes in half h is (lane & 31) + 32 h: after the swaps X0 holds half 0's, X1 half 1's
+      auto swap32 = [](uint32_t& x0, uint32_t& x1) {
+        const auto r = __builtin_amdgcn_permlane32_swap(x0, x1, false, false);
+        x0 = r[0];
+        x1 = r[1];
+      };
+#pragma unroll
+      for (int g = 0; g < P::VR / 4; ++g) {
+        W1[g] = W0[g];
+        swap32(W0[g], W1[g]);
+      }
+      uint32_t ob1 = ob0, rl1 = rl0, pk1 = pk0;
+      swap32(ob0, ob1);
+      swap32(rl0, rl1);
+      swap32(pk0, pk1);
+      const int len0 = full ? 32 * RB : (nact > 32 ? __builtin_amdgcn_readlane(off, 32) : tlen);
+      // LDS byte address of the lane's two rows (rows i + 2 (lane >> 5) of its element) in each half's image
+      uint32_t row0[2], row1[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const uint32_t ri = uint32_t(i + 2 * (lane >> 5));
+        row0[i] = full ? hrow[i] : ob0 + ri * rl0;
+        row1[i] = full ? hrow[i] : ob1 - uint32_t(len0) * 8u + ri * rl1;
+      }
+      char* const ldsb = reinterpret_cast<char*>(lds);
+      auto wcol = [](const uint32_t* Wh, int q) { return (Wh[q / 4] >> (8 * (q % 4))) & 255u; };
+      // The values, one 4 x 4 block at a time as the closed forms complete it: rows (0, 1) and (2, 3) swapped
+      // between the wave's halves, half 0's part straight into the image, half 1's part kept in registers
+      double V1[NH];
+      auto put0 = [&](int b, const double (&blk)[P::NB][P::NB]) {
+        double lo[2][P::NB];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int c = 0; c < P::NB; ++c) {
+            ivec2 x = __builtin_bit_cast(ivec2, blk[i][c]), y = __builtin_bit_cast(ivec2, blk[i + 2][c]);
+#pragma unroll
+            for (int d = 0; d < 2; ++d) {
+              const auto r = __builtin_amdgcn_permlane32_swap(unsigned(x[d]), unsigned(y[d]), false, false);
+              x[d] = int(r[0]);
+              y[d] = int(r[1]);
+            }
+            lo[i][c] = __builtin_bit_cast(double, x);
+            V1[i * P::VR + b * P::NB + c] = __builtin_bit_cast(double, y);
+          }
+        if ((pk0 >> b) & 1u) {
+#pragma unroll
+          for (int c = 0; c < P::NB; ++c) {
+            const uint32_t w = wcol(W0, b * P::NB + c);
+#pragma unroll
+            for (int i = 0; i < 2; ++i) *reinterpret_cast<double*>(ldsb + row0[i] + w) = lo[i][c];
+          }
+        }
+      };
+      if (!HDD_ABL(a, 1)) P::emit(a, own, gat, put0);
       // sharded step: image ranges of the skipped elements, tile coordinates (as in stores_skip below)
       constexpr int NR = 4;
       int rb[NR], re[NR];
@@ -1903,16 +2037,17 @@ swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int hb = h ? len0 : 0, hl = (h ? tlen : len0) - hb;   // wave-uniform
-        if ((lane >> 5) == h && !HDD_ABL(a, 1)) {
-          const RotImg<RB> img{uni ? lds + (lane & 31) * RB : (active ? lds + (off - hb) : scratch),
-                               uni ? 2 * ((lane >> 1) & 15) : 0};
-          // the two halves' computations are identical code on identical registers: without an opaque copy of
-          // the geometry the compiler evaluates them once and keeps all 80 values live across the first
-          // half's stores (spills)
-          typename P::Own oh = own;
+        if (h == 1) {   // half 1's values from registers
 #pragma unroll
-          for (int k = 0; k < P::NB; ++k) asm volatile("" : "+v"(oh.X[k]), "+v"(oh.Y[k]));
-          P::compute(a, e, oh, gat, img);
+          for (int b = 0; b < P::NF + 1; ++b) {
+            if (!((pk1 >> b) & 1u)) continue;
+#pragma unroll
+            for (int c = 0; c < P::NB; ++c) {
+              const uint32_t w = wcol(W1, b * P::NB + c);
+#pragma unroll
+              for (int i = 0; i < 2; ++i) *reinterpret_cast<double*>(ldsb + row1[i] + w) = V1[i * P::VR + b * P::NB + c];
+            }
+          }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -1921,19 +2056,14 @@ swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
         if (hl <= 0) continue;
         const int nb = HDD_ABL(a, 2) ? 0 : hl * 8;
         const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc(out + base + hb, (short)0, nb, 0x00020000);
-        if (uni) {
-          const int dmax = hl - 2;
+        if (full) {   // 2560 values: every chunk in range, the lane part of the offset in voffset
 #pragma unroll
           for (int k = 0; k < STH; ++k) {
-            const int d = 2 * (lane + 64 * k);
-            const int dd = d <= dmax ? d : 0;
-            const int l = dd / RB, j = dd - l * RB;
-            const int q = j + 2 * ((l >> 1) & 15);
-            const dvec2 v = *reinterpret_cast<const dvec2*>(lds + l * RB + (q < RB ? q : q - RB));
-            const int o8 = SKIP && ((gmask >> (32 * h + l)) & 1) ? nb : d * 8;
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ivec4, v), rh, o8, 0, 2);
+            // lane l's chunk k + 5 j (CSR chunk l + 64 (k + 5 j)) sits at hrd[k] + 5120 j in the rotated image
+            const dvec2 v = *reinterpret_cast<const dvec2*>(ldsb + hrd[k % 5] + 5120 * (k / 5));
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ivec4, v), rh, 16 * lane, 1024 * k, 2);
           }
-        } else {
+        } else {      // the range check drops the chunks beyond the half; skipped elements' chunks go out of range
 #pragma unroll
           for (int k = 0; k < STH; ++k) {
             const int d = 2 * (lane + 64 * k);
@@ -2221,6 +2351,17 @@ static hipError_t launch_t(const AssembleArgs& a, hipStream_t s)
   return hipSuccess;
 }
 
+// "swipdg_persistent_kernel<Policy<...>, TL, SKIP>" from the template argument's pretty name (host, once per policy)
+template <class P>
+static std::string kernel_name(const char* flags)
+{
+  const std::string f = __PRETTY_FUNCTION__;   // "... [P = hdd::dev::Q1PwcPolicy<1, 0, false, true, true>]"
+  const size_t a = f.find("P = "), b = f.rfind(']');
+  std::string p = a == std::string::npos ? "?" : f.substr(a + 4, b - a - 4);
+  if (p.rfind("hdd::dev::", 0) == 0) p = p.substr(10);
+  return "swipdg_persistent_kernel<" + p + ", " + flags + ">";
+}
+
 template <class P>
 static hipError_t launch_persistent(const AssembleArgs& a, hipStream_t s)
 {
@@ -2237,9 +2378,9 @@ static hipError_t launch_persistent(const AssembleArgs& a, hipStream_t s)
   // The sharded step's full-range launch (skip_ghost) runs beside the in-place element pass: the grid is shortened
   // by the pass's workgroups (a multiple of 8 keeps the XCD eighths even), so the pass gets SIMDs of its own
   // instead of slowing the persistent waves it would share them with.  C4 N = 8 middle rank +9.2 -> +7.8 %, C2 N = 8
-  // end rank +4.9 -> +2.0 % over one launch (profiles/r04/e_reserve/; HDD_DEBUG_FLAGS 4194304: no reserve).
+  // end rank +4.9 -> +2.0 % over one launch (profiles/r04/e_reserve/; ablation bit 4194304: no reserve).
   int64_t slots = int64_t(cus) * wgcu;
-  const bool reserve = a.skip_ghost && a.reserve_wg > 0 && !(a.debug_flags & 4194304);
+  const bool reserve = a.skip_ghost && a.reserve_wg > 0 && !HDD_ABL(a, 4194304);
   if (reserve) slots = std::max<int64_t>(8, (slots - a.reserve_wg) & ~int64_t(7));
   const int64_t G = std::min<int64_t>(tiles, slots);
   const int n_launch = fused_of<P>::value ? 1 : a.n_comp;   // a FUSED policy emits every component per tile
@@ -2274,6 +2415,10 @@ static hipError_t launch_persistent(const AssembleArgs& a, hipStream_t s)
     }
     return hipSuccess;
   }
+  // the dispatch's choice, readable through hdd_last_tile_kernel(): "swipdg_persistent_kernel<P, TL, SKIP>"
+  static const std::string names[3] = {kernel_name<P>("true, false"), kernel_name<P>("false, true"),
+                                       kernel_name<P>("false, false")};
+  hdd::last_tile_kernel_slot() = names[a.tile_list ? 0 : (a.skip_ghost ? 1 : 2)].c_str();
   for (int c = 0; c < n_launch; ++c) {
     AssembleArgs ac = a;
     if (!fused_of<P>::value) {

@@ -30,7 +30,9 @@ struct AssembleArgs {
   double tc0, tc1, tc2;
   const double* tper;
   double sigma_inner, sigma_boundary, beta;
-  int32_t debug_flags, wgcu;   // ablation switches (HDD_DEBUG_FLAGS, 0 in production); wgcu: tiles per CU override (0: policy default)
+  int32_t debug_flags, wgcu;   // ablation switches (HDD_ABLATION builds only); wgcu: tiles per CU override (0: policy default)
+  uint32_t variant;            // HDD_VARIANT_* verification variants (hdd_ctx_set_variant; 0: the default kernels)
+  int32_t pad_v;
   const int32_t* tile_list;    // optional: 64-element tiles to assemble (relative to own_begin)
   int64_t n_tile_list;         // entries of tile_list (tile_list == nullptr: all tiles)
   int32_t list_elements;       // 1: tile_list holds single owned elements (relative to own_begin), not tiles;
@@ -70,7 +72,8 @@ struct HexArgs {
   double* vals;
   double sigma_inner, sigma_boundary, beta;
   double* ws;                   // p=3 register kernel: per-element coefficient records [n_own][HEX_REC]
-  int32_t debug_flags, pad;     // ablations (HDD_ABLATION builds only); bit 512: the register-MFMA q3 kernel
+  int32_t debug_flags;          // ablations (HDD_ABLATION builds only)
+  uint32_t variant;             // HDD_VARIANT_HEX_Q3_REGISTER: the register-fragment MFMA q3 kernel
   HexTables tab;
   // p=3 reference-matrix GEMM path (hex_q3g_kernel): per 16-element group the coefficient vectors
   // [n_groups][Q3G_K][16], per element {value offset, packed row-block layout} [n_own][2], and the
@@ -119,8 +122,8 @@ struct RhsArgs {
   int32_t skip_face;   // 1: error injection (HDD_DEBUG_FLAGS bit 524288): the split path's face launch "fails"
   double sigma_boundary, beta;
   int32_t nqv, nqd, nqn, n_cu;
-  int32_t generic;   // 1: the run-time-rule kernel only (HDD_DEBUG_FLAGS bit 32768: A/B of the unrolled path)
-  int32_t no_tiny;   // 1: no TINY_PHASE tier for the force's cos products (HDD_DEBUG_FLAGS bit 131072: A/B)
+  int32_t generic;   // 1: the run-time-rule kernel only (HDD_VARIANT_RHS_GENERIC)
+  int32_t no_tiny;   // 1: no TINY_PHASE tier for the force's cos products (HDD_VARIANT_RHS_NO_TINY)
   double qv[64][4];    // volume rule: reference point (3) + weight
   double qd[16][3];    // Dirichlet face rule: face parameters (2) + weight
   double qn[16][3];    // Neumann face rule

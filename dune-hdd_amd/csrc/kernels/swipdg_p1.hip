@@ -8,7 +8,7 @@ namespace dev {
 
 static hipError_t dispatch_smooth_p1(const AssembleArgs& a, hipStream_t s)
 {
-  if (a.debug_flags & 256) return dispatch_kinds<P1Smooth3>(a, s, true);   // A/B: the quadrature policy
+  if (a.variant & HDD_VARIANT_P1_SMOOTH_QUADRATURE) return dispatch_kinds<P1Smooth3>(a, s, true);
   const int tk = a.tkind;
   if (a.kappa[0].kind == HDD_FN_FLATTOP) {   // (the SPE10 FlatTop channel: not a BASELINE kernel, VX only)
     if (!a.ev) return dispatch_kinds<P1Smooth3>(a, s, true);

@@ -23,6 +23,10 @@ PRODUCT_L2, PRODUCT_H1_SEMI, PRODUCT_ELLIPTIC, PRODUCT_BOUNDARY_L2, PRODUCT_PENA
 TENSOR_CONST, TENSOR_ISO_PER_ELEM, TENSOR_SYM_PER_ELEM = 0, 1, 2
 BOUNDARY_ALL_DIRICHLET, BOUNDARY_ALL_NEUMANN = 0, 1
 MAX_COMP = 8
+# verification variants (hdd.h HDD_VARIANT_*; Context.set_variant or the HDD_VARIANT environment value)
+VARIANT_Q1_WHOLE_TILE, VARIANT_ELEMENT_MAJOR, VARIANT_C3_PER_COMPONENT, VARIANT_WAVE_PER_ROW = 1, 2, 4, 8
+VARIANT_P1_SMOOTH_QUADRATURE, VARIANT_HEX_Q3_REGISTER, VARIANT_PATTERN_SCAN_COPY = 16, 32, 64
+VARIANT_RHS_FUSED, VARIANT_RHS_GENERIC, VARIANT_RHS_NO_TINY = 128, 256, 512
 
 # dune-gdt LocalEvaluation::SWIPDG::internal defaults at p = 1 (pinned by the ESV2007 expectation tables)
 SIGMA_INNER_P1 = 8.0
@@ -183,6 +187,8 @@ def lib():
         "hdd_comm_wrap_rccl": (_I32, [_VP, _I32, _VP]),
         "hdd_comm_create_host": (_I32, [HOST_EXCHANGE_FN, _VP, _I32, _VP]),
         "hdd_ctx_set_debug_flags": (_I32, [_VP, _I32]),
+        "hdd_ctx_set_variant": (_I32, [_VP, C.c_uint32]),
+        "hdd_last_tile_kernel": (C.c_char_p, []),
         "hdd_device_hub_create": (_I32, [_I32, _VP]),
         "hdd_device_hub_destroy": (None, [_VP]),
         "hdd_comm_create_device": (_I32, [_VP, _I32, _I32, _VP]),
@@ -200,6 +206,12 @@ def lib():
         "hdd_shard_pattern_fill": (_I32, [_VP, _VP, _VP, _VP, _VP, _VP]),
         "hdd_block_assemble_sharded": (_I32, [_VP, _VP, _VP, C.POINTER(ScalarFn), _I32, C.POINTER(TensorFn),
                                               C.POINTER(Params), C.POINTER(CsrT), _VP, C.c_uint32, _VP]),
+        "hdd_block_step_mark": (_I32, [_VP, _VP]),
+        "hdd_block_step_query": (_I32, [_VP, C.POINTER(_I32)]),
+        "hdd_block_stage_name": (C.c_char_p, [_I32]),
+        "hdd_block_step_sync": (_I32, [_VP, _VP, C.c_double]),
+        "hdd_device_hub_stall": (_I32, [_VP, _I32, C.c_double]),
+        "hdd_device_hub_release": (_I32, [_VP]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -207,6 +219,11 @@ def lib():
         fn.argtypes = args
     _LIB = L
     return L
+
+
+def last_tile_kernel():
+    """hdd_last_tile_kernel: the persistent tile kernel this thread's last assembly launched (the dispatch's choice)"""
+    return lib().hdd_last_tile_kernel().decode()
 
 
 def _check(rc, what=""):
@@ -449,8 +466,13 @@ class Context:
         self.h = h
 
     def set_debug_flags(self, flags):
-        """profiling ablations / error injection (hdd_ctx_set_debug_flags; 0 in production)"""
+        """error injection of the tests (hdd_ctx_set_debug_flags; 0 in production; ablation bits only in the
+        HDD_ABLATION library)"""
         _check(lib().hdd_ctx_set_debug_flags(self.h, int(flags)), "hdd_ctx_set_debug_flags")
+
+    def set_variant(self, variant):
+        """verification variants (hdd_ctx_set_variant, VARIANT_*): alternative kernels of the same values"""
+        _check(lib().hdd_ctx_set_variant(self.h, int(variant)), "hdd_ctx_set_variant")
 
     def __del__(self):
         if getattr(self, "h", None):
@@ -887,6 +909,14 @@ class DeviceHub:
         _check(lib().hdd_device_hub_create(nranks, C.byref(h)), "hdd_device_hub_create")
         self.h, self.nranks = h, nranks
 
+    def stall(self, rank, max_seconds):
+        """error injection (hdd_device_hub_stall): rank's next post publishes sends that complete only after
+        release() (or max_seconds) -- a peer whose sends do not arrive"""
+        _check(lib().hdd_device_hub_stall(self.h, rank, float(max_seconds)), "hdd_device_hub_stall")
+
+    def release(self):
+        _check(lib().hdd_device_hub_release(self.h), "hdd_device_hub_release")
+
     def __del__(self):
         if getattr(self, "h", None):
             try:
@@ -941,6 +971,24 @@ class Shard:
         tbd = np.empty(self.info.n_tiles_boundary, np.int32)
         _check(lib().hdd_shard_tile_lists(self.h, _p(tin), _p(tbd)), "hdd_shard_tile_lists")
         return tin, tbd
+
+    def step_mark(self, stream=None):
+        """hdd_block_step_mark: the watchdog's marker event after the steps enqueued on `stream` so far"""
+        s = stream if stream is not None else _torch().cuda.current_stream().cuda_stream
+        _check(lib().hdd_block_step_mark(self.h, C.c_void_p(s)), "hdd_block_step_mark")
+
+    def step_query(self):
+        """hdd_block_step_query (non-blocking) -> (stage, name): the first stage of the last sharded step (and the
+        marker) that has not completed; stage 0 = complete"""
+        st = _I32()
+        _check(lib().hdd_block_step_query(self.h, C.byref(st)), "hdd_block_step_query")
+        return st.value, lib().hdd_block_stage_name(st.value).decode()
+
+    def step_sync(self, timeout_s, stream=None):
+        """hdd_block_step_sync: mark, then poll the step's stage events until done; HddError naming the rank, stage
+        and halo peers after timeout_s"""
+        s = stream if stream is not None else _torch().cuda.current_stream().cuda_stream
+        _check(lib().hdd_block_step_sync(self.h, C.c_void_p(s), float(timeout_s)), "hdd_block_step_sync")
 
     def global_ids(self):
         g = np.empty(self.n_local, np.int64)

@@ -36,11 +36,13 @@
 extern "C" {
 #endif
 
-#define HDD_ABI_VERSION 7   /* 3: hdd_mesh vertex-indexed geometry, hdd_local_vertices;
+#define HDD_ABI_VERSION 8   /* 3: hdd_mesh vertex-indexed geometry, hdd_local_vertices;
                                4: HDD_FN_FLATTOP (hdd_scalar_fn.table / n_table), hdd_indicator_sum;
                                5: hdd_shard_info.halo_elements, hdd_swipdg_assemble_elements;
                                6: hdd_grid_create_hex_from_connectivity;
-                               7: in-process device transport (hdd_device_hub, hdd_comm_create_device) */
+                               7: in-process device transport (hdd_device_hub, hdd_comm_create_device);
+                               8: sharded-step watchdog (hdd_block_step_mark / _query / _sync, HDD_ERR_TIMEOUT), the
+                                  device transport's stall injection, verification variants (hdd_ctx_set_variant) */
 #define HDD_MAX_COMP 8
 
 typedef enum {
@@ -49,7 +51,8 @@ typedef enum {
   HDD_ERR_HIP = 2,          /* HIP runtime failure */
   HDD_ERR_UNSUPPORTED = 3,  /* NotImplemented in the reference's sense */
   HDD_ERR_NOMEM = 4,
-  HDD_ERR_RANGE = 5         /* index_out_of_range */
+  HDD_ERR_RANGE = 5,        /* index_out_of_range */
+  HDD_ERR_TIMEOUT = 6       /* a deadline passed (hdd_block_step_sync: a sharded step that did not complete) */
 } hdd_status;
 
 enum { HDD_SIMPLEX = 0, HDD_CUBE = 1,                       /* P1 triangles / Q1 parallelograms (2d) */
@@ -71,12 +74,33 @@ int hdd_abi_version(void);
 /* binds `hip_device`; replaces nothing in the reference (DUNE is host-only) */
 int hdd_ctx_create(int hip_device, hdd_ctx** out);
 void hdd_ctx_destroy(hdd_ctx* ctx);
-/* profiling ablations / error injection of the tests (the HDD_DEBUG_FLAGS value a context reads at creation;
- * 0 in production).  Bit 524288: hdd_swipdg_rhs's face launch is treated as failed (the call returns
- * HDD_ERR_HIP after its volume kernel; the next call must still be correct). */
+/* error injection of the tests (the HDD_DEBUG_FLAGS value a context reads at creation; 0 in production).
+ * Bit 524288: hdd_swipdg_rhs's face launch is treated as failed (the call returns HDD_ERR_HIP after its volume
+ * kernel; the next call must still be correct).  Profiling ablations exist only in the separate -DHDD_ABLATION
+ * build (make ablation: lib_ab/libhdd_abl.so); the product library ignores every other bit. */
 int hdd_ctx_set_debug_flags(hdd_ctx* ctx, int32_t flags);
+/* Verification variants (ABI 8): alternative implementations of the same values, selected per context (or by the
+ * HDD_VARIANT value a context reads at creation) so that the tests can compare them bit for bit / to rounding
+ * with the default kernels.  Default 0: the kernels the dispatch picks for performance. */
+enum {
+  HDD_VARIANT_Q1_WHOLE_TILE = 1,      /* Q1: the whole-tile image kernel on every mesh (the default on element-major
+                                         meshes and on the sharded step's SKIP launches) instead of the half-image one */
+  HDD_VARIANT_ELEMENT_MAJOR = 2,      /* ignore the mesh's vertex-indexed geometry (element-major coordinates) */
+  HDD_VARIANT_C3_PER_COMPONENT = 4,   /* OS2014 sinusoid components: one launch per component, not the fused one */
+  HDD_VARIANT_WAVE_PER_ROW = 8,       /* the generic wave-per-row kernels instead of the persistent tile policies */
+  HDD_VARIANT_P1_SMOOTH_QUADRATURE = 16,   /* P1 smooth kappa: the quadrature policy instead of the moments */
+  HDD_VARIANT_HEX_Q3_REGISTER = 32,   /* hexahedra p = 3: the register-fragment MFMA kernel, not the GEMM one */
+  HDD_VARIANT_PATTERN_SCAN_COPY = 64, /* device pattern nnz by a scan launch + device-to-host copy */
+  HDD_VARIANT_RHS_FUSED = 128,        /* 2d RHS: one fused kernel instead of volume kernel + boundary-element list */
+  HDD_VARIANT_RHS_GENERIC = 256,      /* RHS: the run-time-rule kernel only */
+  HDD_VARIANT_RHS_NO_TINY = 512       /* RHS: no small-phase polynomial tier for the force's cos products */
+};
+int hdd_ctx_set_variant(hdd_ctx* ctx, uint32_t variant);
 /* message of the last failure on this thread (ctx may be NULL); never NULL */
 const char* hdd_last_error(const hdd_ctx* ctx);
+/* the instantiation name of the last persistent tile kernel this thread launched ("" if none; ABI 8): what the
+ * dispatch actually picked, e.g. for a benchmark's kernel label.  Element-list passes are not recorded. */
+const char* hdd_last_tile_kernel(void);
 
 /* ---------------------------------------------------------------------------------------------- */
 /* grids (host) -- replace the grid providers the reference builds its spaces on:                  */
@@ -513,8 +537,9 @@ enum {
                                    after the join (the assembly's tiles store every row block) */
   HDD_SHARD_FIX_INPLACE = 128,  /* the off-stream fixup in place, the assembly's tiles skip those row blocks:
                                    default except on P1 shards with two peers (HDD_SHARD_SPLIT_TILES) */
-  HDD_SHARD_LAUNCH_LAST = 256   /* study (round 3's order): with the in-place fixup, enqueue the full-range launch
-                                   after the halo work (pack, exchange, element pass) instead of before it */
+  HDD_SHARD_LAUNCH_LAST = 256   /* ablation builds only (round 3's order, measured and rejected): with the in-place
+                                   fixup, enqueue the full-range launch after the halo work instead of before it;
+                                   the product library ignores it */
 };
 /* One sharded assembly step -- the LHS of BlockSWIPDG::init() for the owned subdomains: pack the halo
  * records (per-element tensor / kappa rows, [+ coordinates]) of the elements the peers need -> post the
@@ -528,6 +553,30 @@ enum {
 int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm* comm, const hdd_scalar_fn* kappa,
                                int32_t n_comp, const hdd_tensor_fn* tensor, const hdd_swipdg_params* params,
                                const hdd_csr* pattern, double* const* d_vals, uint32_t flags, void* stream);
+
+/* Watchdog of the sharded step (ABI 8).  A lost or stalled peer shows as a step that never completes on the device
+ * (RCCL waits inside its kernels), so instead of blocking in a device synchronize a rank can poll the events of its
+ * last step with a deadline and report where it stopped.  Stages in pipeline order: */
+enum {
+  HDD_STAGE_COMPLETE = 0,
+  HDD_STAGE_PACK = 1,       /* the halo pack kernel (the event the transfer starts from) */
+  HDD_STAGE_EXCHANGE = 2,   /* the group send / recv with the halo peers */
+  HDD_STAGE_ELEMENTS = 3,   /* the ghost-adjacent element pass behind the receives */
+  HDD_STAGE_ASSEMBLY = 4    /* the tile launch(es) and the join on `stream` (up to the last hdd_block_step_mark) */
+};
+/* record the marker event on `stream` (after the steps to watch) */
+int hdd_block_step_mark(hdd_shard* sh, void* stream);
+/* non-blocking: *stage = the first stage of the last step (and the marker) whose event has not completed */
+int hdd_block_step_query(hdd_shard* sh, int32_t* stage);
+const char* hdd_block_stage_name(int32_t stage);
+/* mark, then poll until every stage has completed or timeout_s has passed: HDD_ERR_TIMEOUT with a message naming
+ * the rank, the stage and the halo peers (hdd_last_error) */
+int hdd_block_step_sync(hdd_shard* sh, void* stream, double timeout_s);
+/* Error injection (tests of the watchdog): the next hdd_comm_post of `rank` on this hub publishes sends that complete
+ * only when hdd_device_hub_release() opens a device-side gate, or after max_seconds (a one-wave kernel polling a
+ * host word; it always ends) -- a peer whose sends do not arrive. */
+int hdd_device_hub_stall(hdd_device_hub* hub, int32_t rank, double max_seconds);
+int hdd_device_hub_release(hdd_device_hub* hub);
 
 #ifdef __cplusplus
 }

@@ -253,7 +253,7 @@ def c5(args):
     nq, nqf = nq1v ** 3, nq1f ** 2
     # F = ne 2 nb^2 nq d + nif 24 nb^2 nqf + nbf 6 nb^2 nqf (reference quadrature)
     alg_flops = loc.n_own * 2 * nb * nb * nq * 3 + nif * 24 * nb * nb * nqf + nbf * 6 * nb * nb * nqf
-    # executed MFMA work (v_mfma_f64_16x16x4: 2048 flop).  hex_q3_kernel (HDD_DEBUG_FLAGS=512), whole element = 4 waves:
+    # executed MFMA work (v_mfma_f64_16x16x4: 2048 flop).  hex_q3_kernel (HDD_VARIANT=32), whole element = 4 waves:
     # volume 27 k-steps x 4 row tiles per wave; every face runs its rows in the layout rotated to its normal,
     # so the [V] part takes 1 row tile (4 k-steps) per wave; the [N] part 4 tiles x 4 k-steps in every wave
     # on x / y faces and in one wave only on z faces (column skip) -> x/y: 80 (S) + 80 (E, inner) per face,
@@ -261,7 +261,7 @@ def c5(args):
     nbr_own = nbr[:, loc.own_begin:loc.own_end]
     xy_inner = int((nbr_own[:4] >= 0).sum()); xy_dir = int((nbr_own[:4] == H.NBR_DIRICHLET).sum())
     z_inner = int((nbr_own[4:] >= 0).sum()); z_dir = int((nbr_own[4:] == H.NBR_DIRICHLET).sum())
-    legacy = int(os.environ.get("HDD_DEBUG_FLAGS", "0") or 0) & 512
+    legacy = int(os.environ.get("HDD_VARIANT", "0") or 0, 0) & H.VARIANT_HEX_Q3_REGISTER
     if deg != 3:
         n_mfma = 0
     elif legacy:

@@ -1,7 +1,7 @@
-"""C4-type Q1 assemblies (SPE10 checkerboard, 8 x 8 subdomains, one launch) of growing size under several
-HDD_DEBUG_FLAGS kernel selections, interleaved rounds in one process -- where the half-image kernel on vertex-indexed
-geometry (default) and the whole-tile kernel on element-major coords (1048576) cross over.
-usage: python scripts/study/q1_size_sweep.py [--sizes NXxNY,...] [flags ...]     (default flags: 0 1048576 2097152)"""
+"""C4-type Q1 assemblies (SPE10 checkerboard, 8 x 8 subdomains, one launch) of growing size under several verification
+variants (hdd_ctx_set_variant), interleaved rounds in one process -- where the half-image kernel on vertex-indexed
+geometry (default, 0) and the whole-tile kernel (1 = HDD_VARIANT_Q1_WHOLE_TILE; 3 = on element-major coords) cross over.
+usage: python scripts/study/q1_size_sweep.py [--sizes NXxNY,...] [variants ...]     (default: 0 1 3)"""
 import os
 import sys
 
@@ -19,12 +19,11 @@ def main():
     if args and args[0] == "--sizes":
         sizes = [tuple(int(v) for v in z.split("x")) for z in args[1].split(",")]
         args = args[2:]
-    flags = [int(f) for f in args] or [0, 1048576, 2097152]
+    flags = [int(f) for f in args] or [0, 1, 3]
     ctxs = {}
     for f in flags:
-        os.environ["HDD_DEBUG_FLAGS"] = str(f)
         ctxs[f] = H.Context(0)
-    os.environ["HDD_DEBUG_FLAGS"] = "0"
+        ctxs[f].set_variant(f)
     perm = 10.0 ** np.random.default_rng(10).uniform(-3, 3, 2000)
     for nx, ny in sizes:
         grid = H.Grid.structured(H.CUBE, nx, ny, (0, 0), (5.0 * nx / 3520, 1.0 * ny / 1200), px=8, py=8)
@@ -45,7 +44,7 @@ def main():
                 e1.record()
                 torch.cuda.synchronize()
                 res[f].append(e0.elapsed_time(e1) / 10)
-        line = "  ".join("flags %d %.4f ms" % (f, np.median(res[f])) for f in flags)
+        line = "  ".join("variant %d %.4f ms" % (f, np.median(res[f])) for f in flags)
         print("%d x %d (%d elements, %d tiles): %s" % (nx, ny, loc.n_own, (loc.n_own + 63) // 64, line), flush=True)
         del dm, dp, vals, loc
 

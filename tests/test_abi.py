@@ -14,7 +14,7 @@ def test_exports_every_declared_symbol():
     assert len(names) >= 24
     missing = [n for n in names if not hasattr(L, n)]
     assert not missing, missing
-    assert L.hdd_abi_version() == 7
+    assert L.hdd_abi_version() == 8
 
 
 def test_errors_are_status_codes_with_messages():

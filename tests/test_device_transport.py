@@ -38,8 +38,6 @@ SCHEDULES = {
     "inline": H.SHARD_FIX_INLINE,
     "split": H.SHARD_SPLIT_TILES,
     "serial": H.SHARD_NO_OVERLAP,
-    "last": H.SHARD_LAUNCH_LAST,
-    "inplace_last": H.SHARD_FIX_INPLACE | H.SHARD_LAUNCH_LAST,
 }
 
 

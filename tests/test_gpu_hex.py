@@ -100,7 +100,7 @@ def test_hex_neumann_boundary(ctx, deg):
 
 def test_hex_q3_gemm_equals_register_kernel():
     """p = 3 with per-element data: the reference-matrix GEMM kernel (hex_q3g_kernel, default) against the
-    register-fragment MFMA kernel (HDD_DEBUG_FLAGS bit 512) on 10 x 9 x 7 elements in 2 slabs (ragged last
+    register-fragment MFMA kernel (HDD_VARIANT_HEX_Q3_REGISTER) on 10 x 9 x 7 elements in 2 slabs (ragged last
     16-element group, every workgroup walking several groups, Dirichlet faces), both through the C ABI; and the
     oracle on the same input at the parity tolerance."""
     import os
@@ -113,19 +113,14 @@ def test_hex_q3_gemm_equals_register_kernel():
     kel = np.random.default_rng(12).uniform(0.2, 4.0, g.ne)
     ten = H.tensor_fn(H.TENSOR_SYM_PER_ELEM, per_elem=torch.from_numpy(np.ascontiguousarray(T.T)).cuda(), dim=3)
     kap = H.scalar_fn(H.FN_PER_ELEM, per_elem=torch.from_numpy(kel).cuda())
-    old = os.environ.get("HDD_DEBUG_FLAGS")
     vals = []
-    for flags in ("0", "512"):
-        os.environ["HDD_DEBUG_FLAGS"] = flags
+    for variant in (0, H.VARIANT_HEX_Q3_REGISTER):
         c = H.Context(0)
+        c.set_variant(variant)
         (v,) = H.assemble(c, dm, dp, [kap], ten, H.params_for(deg, 3))
         torch.cuda.synchronize()
         vals.append(v.cpu().numpy())
         del c
-    if old is None:
-        del os.environ["HDD_DEBUG_FLAGS"]
-    else:
-        os.environ["HDD_DEBUG_FLAGS"] = old
     rp = dp.host[0]
     worst, ok = compare_rows(rp, vals[0], vals[1], RTOL)
     assert ok, worst
@@ -211,18 +206,13 @@ def test_device_pattern_uniform_tiles_equal_host(ctx, et, px):
 @pytest.mark.parametrize("et", [H.SIMPLEX, H.CUBE])
 def test_device_elem_ptr_block_sums_equal_scan(et):
     """elem_ptr with per-block offset sums (no scan launch, > 768 blocks: the unrolled loads) and nnz through the
-    mapped host word equal the scan-launch + copy scheme (HDD_DEBUG_FLAGS bit 262144), pattern included."""
+    mapped host word equal the scan-launch + copy scheme (HDD_VARIANT_PATTERN_SCAN_COPY), pattern included."""
     import os
     torch = _torch()
     ctxs = []
-    old = os.environ.get("HDD_DEBUG_FLAGS")
-    for flags in ("0", "262144"):
-        os.environ["HDD_DEBUG_FLAGS"] = flags
+    for variant in (0, H.VARIANT_PATTERN_SCAN_COPY):
         ctxs.append(H.Context(0))
-    if old is None:
-        del os.environ["HDD_DEBUG_FLAGS"]
-    else:
-        os.environ["HDD_DEBUG_FLAGS"] = old
+        ctxs[-1].set_variant(variant)
     g = H.Grid.structured(et, 1600 if et == H.SIMPLEX else 3200, 500, px=2, py=1)
     loc = g.local()
     assert loc.n_own > 768 * 2048

@@ -18,23 +18,23 @@ from mesh_tools import affine_quad_mesh, scrambled_quad_mesh
 H = pytest.importorskip("hdd_amd")
 pytestmark = pytest.mark.gpu
 
-# HDD_DEBUG_FLAGS (swipdg_q1.hip): the default on vertex-indexed meshes is the half-image kernel
-WHOLE = 1048576     # the whole-tile image kernel (round 3's default)
-HALF_EM = 2097152   # the half-image kernel on element-major coordinates
+# verification variants (swipdg_q1.hip): the default on vertex-indexed meshes is the half-image kernel
+WHOLE = H.VARIANT_Q1_WHOLE_TILE                            # the whole-tile image kernel (round 3's default)
+WHOLE_EM = H.VARIANT_Q1_WHOLE_TILE | H.VARIANT_ELEMENT_MAJOR   # ... on element-major coordinates
 
 
 def _all(ctx, fn):
-    """fn() under the whole-tile kernel, the half-image kernel and the half-image kernel on vertex-indexed
-    geometry -> [whole, half, half_vx]"""
+    """fn() under the whole-tile kernel on element-major and on vertex-indexed geometry, and the (default)
+    half-image kernel -> [whole_em, whole_vx, half]"""
     import torch
     out = []
-    for flags in (WHOLE, HALF_EM, 0):
-        ctx.set_debug_flags(flags)
+    for variant in (WHOLE_EM, WHOLE, 0):
+        ctx.set_variant(variant)
         try:
             r = fn()
             torch.cuda.synchronize()
         finally:
-            ctx.set_debug_flags(0)
+            ctx.set_variant(0)
         out.append(r)
     return out
 
@@ -63,9 +63,9 @@ def test_half_image_equals_whole_tile(ctx, tk, bnd, kpe):
     kf = [H.scalar_fn(H.FN_PER_ELEM, per_elem=torch.from_numpy(np.ascontiguousarray(kap[idx])).cuda())
           if kpe else H.scalar_fn(H.FN_CONST, 1.7)]
     dm, dp = H.DeviceMesh(loc), H.DevicePattern(loc)
-    whole, half, half_vx = _all(ctx, lambda: H.assemble(ctx, dm, dp, kf, ten)[0].cpu().numpy())
+    whole, whole_vx, half = _all(ctx, lambda: H.assemble(ctx, dm, dp, kf, ten)[0].cpu().numpy())
+    assert np.array_equal(_bits(whole), _bits(whole_vx))
     assert np.array_equal(_bits(whole), _bits(half))
-    assert np.array_equal(_bits(whole), _bits(half_vx))
     pc, pev, _ = grid.connectivity()
     og = O.Grid(O.cube_grid(1, 1, (0, 0), (1, 1))[0], pc, pev)
     okind = O.TENSOR_SYM_PER_ELEM if tk == "sym" else O.TENSOR_ISO_PER_ELEM
@@ -87,10 +87,10 @@ def test_half_image_edge_meshes(ctx, nx, ny):
     k = torch.from_numpy(loc.checkerboard(SPE10_LOWER, SPE10_UPPER, 100, 20, perm)).cuda()
     dm, dp = H.DeviceMesh(loc), H.DevicePattern(loc)
     kf, ten = [H.scalar_fn(H.FN_CONST, 1.0)], H.tensor_fn(H.TENSOR_ISO_PER_ELEM, per_elem=k)
-    whole, half, half_vx = _all(ctx, lambda: H.assemble(ctx, dm, dp, kf, ten)[0].cpu().numpy())
+    whole, whole_vx, half = _all(ctx, lambda: H.assemble(ctx, dm, dp, kf, ten)[0].cpu().numpy())
     assert np.isfinite(half).all()
+    assert np.array_equal(_bits(whole), _bits(whole_vx))
     assert np.array_equal(_bits(whole), _bits(half))
-    assert np.array_equal(_bits(whole), _bits(half_vx))
 
 
 @pytest.mark.parametrize("kind", ["parallelogram", "scrambled"])
@@ -107,9 +107,9 @@ def test_half_image_general_quads(ctx, kind):
     k = torch.from_numpy(np.ascontiguousarray(10.0 ** np.sin(7 * x + 3 * y))).cuda()
     dm, dp = H.DeviceMesh(loc), H.DevicePattern(loc)
     kf, ten = [H.scalar_fn(H.FN_CONST, 1.0)], H.tensor_fn(H.TENSOR_ISO_PER_ELEM, per_elem=k)
-    whole, half, half_vx = _all(ctx, lambda: H.assemble(ctx, dm, dp, kf, ten)[0].cpu().numpy())
+    whole, whole_vx, half = _all(ctx, lambda: H.assemble(ctx, dm, dp, kf, ten)[0].cpu().numpy())
+    assert np.array_equal(_bits(whole), _bits(whole_vx))
     assert np.array_equal(_bits(whole), _bits(half))
-    assert np.array_equal(_bits(whole), _bits(half_vx))
 
 
 def test_half_image_tile_lists_and_element_fixup(ctx):
@@ -121,11 +121,11 @@ def test_half_image_tile_lists_and_element_fixup(ctx):
     dm, dp = H.DeviceMesh(local), H.DevicePattern(local)
     k = torch.from_numpy(local.checkerboard((0, 0), (4, 1), 100, 20, O.spe10_synthetic_permeability())).cuda()
     kf, ten = [H.scalar_fn(H.FN_CONST, 1.0)], H.tensor_fn(H.TENSOR_ISO_PER_ELEM, per_elem=k)
-    ctx.set_debug_flags(WHOLE)
+    ctx.set_variant(WHOLE)
     ref = H.assemble(ctx, dm, dp, kf, ten)[0]
     t_in, t_bd = H.halo_tiles(local)
     fix = np.random.default_rng(4).permutation(H.halo_elements(local)).astype(np.int32)
-    ctx.set_debug_flags(0)
+    ctx.set_variant(0)
     try:
         v = torch.full_like(ref, float("nan"))
         for tl in (t_in, t_bd):
@@ -145,6 +145,6 @@ def test_half_image_tile_lists_and_element_fixup(ctx):
         H.assemble_tiles(ctx, dm, dp, kf, ten, torch.from_numpy(fix).cuda(), [w], elements=True)
         torch.cuda.synchronize()
     finally:
-        ctx.set_debug_flags(0)
+        ctx.set_variant(0)
     assert torch.equal(v, ref)
     assert torch.equal(w, ref)

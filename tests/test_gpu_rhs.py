@@ -140,19 +140,14 @@ def test_rhs_vertex_indexed_equals_element_major(case):
 @pytest.mark.parametrize("et", [H.SIMPLEX, H.CUBE])
 def test_rhs_split_equals_fused(et):
     """The split 2d path (volume kernel + boundary-element list + face kernel) equals the fused one-kernel path
-    (HDD_DEBUG_FLAGS bit 65536) bit for bit, on meshes from all-boundary (3 x 2) to ragged multi-chunk ones, with
+    (HDD_VARIANT_RHS_FUSED) bit for bit, on meshes from all-boundary (3 x 2) to ragged multi-chunk ones, with
     Dirichlet + Neumann faces, repeated calls (the list's counters reset by the face kernel) and a growing list."""
     import os
     import torch
     ctxs = []
-    old = os.environ.get("HDD_DEBUG_FLAGS")
-    for flags in ("0", "65536"):
-        os.environ["HDD_DEBUG_FLAGS"] = flags
+    for variant in (0, H.VARIANT_RHS_FUSED):
         ctxs.append(H.Context(0))
-    if old is None:
-        del os.environ["HDD_DEBUG_FLAGS"]
-    else:
-        os.environ["HDD_DEBUG_FLAGS"] = old
+        ctxs[-1].set_variant(variant)
     rng = np.random.default_rng(11)
     for n in [(3, 2), (61, 23), (200, 37)]:
         grid = H.Grid.structured(et, *n, (0, 0), (2, 1))
