@@ -23,6 +23,17 @@ int hdd_assemble_elements_buf(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_
                               double* const* d_bufs, const int32_t* d_elems, int64_t n_elems, void* stream);
 int hdd_scatter_fix(hdd_ctx* ctx, const hdd_csr* pattern, int32_t rb, double* const* d_bufs, int32_t n_comp,
                     const int32_t* d_elems, int64_t n_elems, double* const* d_vals, void* stream);
+// Q1 side buffers in value-major (SoA) order: value k (canonical: row i, block b, column c, k = 20 i + 4 b + c) of
+// listed element j at d_bufs[c][k ld + j] (coalesced element-pass stores), put into place by a wave per element;
+// and a full-range launch that leaves reserve_wg workgroup slots to that element pass
+int hdd_assemble_elements_soa(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_fn* kappa, int32_t n_comp,
+                              const hdd_tensor_fn* tensor, const hdd_swipdg_params* p, const hdd_csr* pattern,
+                              double* const* d_bufs, int64_t ld, const int32_t* d_elems, int64_t n_elems, void* stream);
+int hdd_scatter_fix_q1_soa(hdd_ctx* ctx, const hdd_mesh* m, const hdd_csr* pattern, double* const* d_bufs, int64_t ld,
+                           int32_t n_comp, const int32_t* d_elems, int64_t n_elems, double* const* d_vals, void* stream);
+int hdd_assemble_reserve(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_fn* kappa, int32_t n_comp,
+                         const hdd_tensor_fn* tensor, const hdd_swipdg_params* p, const hdd_csr* pattern,
+                         double* const* d_vals, void* stream, int32_t reserve_wg);
 // the same pass in place (no side buffer), beside a full-range assembly that skips those elements' row blocks
 int hdd_assemble_elements_inplace(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_fn* kappa, int32_t n_comp,
                                   const hdd_tensor_fn* tensor, const hdd_swipdg_params* p, const hdd_csr* pattern,

@@ -268,7 +268,8 @@ static int assemble_hex(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_fn* ka
 static int assemble_impl(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_fn* kappa, int32_t n_comp,
                          const hdd_tensor_fn* tensor, const hdd_swipdg_params* p, const hdd_csr* pattern,
                          double* const* d_vals, const int32_t* d_tiles, int64_t n_tiles, void* stream,
-                         int list_elements = 0, bool skip_ghost = false, int32_t reserve_wg = 0)
+                         int list_elements = 0, bool skip_ghost = false, int32_t reserve_wg = 0,
+                         int64_t fix_ld = 0)
 {
   using namespace hdd::dev;
   if (!ctx || !m || !kappa || !tensor || !p || !pattern || !d_vals)
@@ -326,7 +327,8 @@ static int assemble_impl(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_fn* k
   a.n_tile_list = n_tiles;
   a.list_elements = list_elements;
   a.skip_ghost = skip_ghost ? 1 : 0;
-  a.reserve_wg = skip_ghost ? reserve_wg : 0;
+  a.reserve_wg = list_elements ? 0 : reserve_wg;
+  a.fix_ld = fix_ld;
   a.fix_rb = (m->elem_type == HDD_SIMPLEX ? 3 * 3 * 4 : 4 * 4 * 5);
   if (!m->elem_vertices != !m->vertex_coords)
     return set_error(HDD_ERR_INVALID, "hdd_swipdg_assemble: mesh elem_vertices / vertex_coords: both or neither");
@@ -431,6 +433,43 @@ int hdd_assemble_elements_inplace(hdd_ctx* ctx, const hdd_mesh* m, const hdd_sca
 {
   if (n_elems == 0) return HDD_OK;
   return assemble_impl(ctx, m, kappa, n_comp, tensor, p, pattern, d_vals, d_elems, n_elems, stream, 3);
+}
+
+int hdd_assemble_elements_soa(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_fn* kappa, int32_t n_comp,
+                              const hdd_tensor_fn* tensor, const hdd_swipdg_params* p, const hdd_csr* pattern,
+                              double* const* d_bufs, int64_t ld, const int32_t* d_elems, int64_t n_elems, void* stream)
+{
+  if (n_elems == 0) return HDD_OK;
+  if (m->elem_type != HDD_CUBE) return set_error(HDD_ERR_UNSUPPORTED, "hdd_assemble_elements_soa: Q1 only");
+  return assemble_impl(ctx, m, kappa, n_comp, tensor, p, pattern, d_bufs, d_elems, n_elems, stream, 4, false, 0, ld);
+}
+
+int hdd_assemble_reserve(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_fn* kappa, int32_t n_comp,
+                         const hdd_tensor_fn* tensor, const hdd_swipdg_params* p, const hdd_csr* pattern,
+                         double* const* d_vals, void* stream, int32_t reserve_wg)
+{
+  return assemble_impl(ctx, m, kappa, n_comp, tensor, p, pattern, d_vals, nullptr, 0, stream, 0, false, reserve_wg);
+}
+
+int hdd_scatter_fix_q1_soa(hdd_ctx* ctx, const hdd_mesh* m, const hdd_csr* pattern, double* const* d_bufs, int64_t ld,
+                           int32_t n_comp, const int32_t* d_elems, int64_t n_elems, double* const* d_vals, void* stream)
+{
+  if (n_elems == 0) return HDD_OK;
+  hdd::dev::AssembleArgs a{};
+  a.n_local = m->n_local;
+  a.own_begin = m->own_begin;
+  a.own_end = m->own_end;
+  a.nbrs = m->neighbors;
+  a.finfo = m->face_info;
+  a.elem_ptr = pattern->elem_ptr;
+  a.tile_list = d_elems;
+  a.n_tile_list = n_elems;
+  a.n_cu = ctx->n_cu;
+  for (int32_t c = 0; c < n_comp; ++c) {
+    const hipError_t e = hdd::dev::launch_q1_scatter_soa(a, d_bufs[c], ld, d_vals[c], static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return hip_fail(e, "hdd_scatter_fix_q1_soa");
+  }
+  return HDD_OK;
 }
 
 int hdd_assemble_skip_ghost(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_fn* kappa, int32_t n_comp,

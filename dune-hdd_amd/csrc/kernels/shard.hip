@@ -1001,7 +1001,17 @@ extern "C" int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm*
   const bool default_schedule = !(flags & (HDD_SHARD_FIX_INLINE | HDD_SHARD_FIX_SCATTER | HDD_SHARD_FIX_INPLACE));
   const bool split = (flags & HDD_SHARD_SPLIT_TILES) != 0 ||
                      (default_schedule && sh->gi.elem_type == HDD_SIMPLEX && sh->peers.size() >= 2 && sh->n_in > 0);
-  bool overlap = !(flags & HDD_SHARD_NO_OVERLAP) && sh->gi.elem_type != HDD_HEX && (split ? sh->n_in > 0 : true);
+  //
+  // Round 5, Q1: the serial step by default (pack, exchange, then one half-image launch over every tile).  One-card
+  // study on the final kernels (profiles/r05/d_shard/, loopback transfer, back-to-back steps): C4 N = 8 end / middle
+  // rank serial +8.5 / +12.3 % over one launch, the overlapped in-place step +16.7 / +20.8 %, the side buffer after
+  // the join +13.4 / +18.9 %; N = 2 serial +2.2 / +3.1 %, overlapped +4.3 / +5.0 %.  The kernel trace shows why: the
+  // half-image launch holds every wave slot it can (two waves per SIMD, all of the LDS), so the halo kernels beside
+  // it wait for the reserved slots (a D2D copy 39 us instead of 5), and each cross-stream join costs ~5 us on the
+  // step's critical path.  The overlapped schedules stay selectable (HDD_SHARD_FIX_INPLACE / _FIX_SCATTER / _SPLIT).
+  const bool q1_serial = sh->gi.elem_type == HDD_CUBE && default_schedule && !(flags & HDD_SHARD_SPLIT_TILES);
+  bool overlap = !(flags & HDD_SHARD_NO_OVERLAP) && sh->gi.elem_type != HDD_HEX && !q1_serial &&
+                 (split ? sh->n_in > 0 : true);
   // The pack and the transfer leave the assembly stream when the assembly overlaps them: the RCCL transfer
   // stream (or, in the loopback study, the shard's side stream) waits for the inputs, packs and sends while
   // `stream` starts the assembly at once -- the pack launch is off the critical path.  (The host transport
@@ -1039,6 +1049,22 @@ extern "C" int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm*
       e = hipEventCreateWithFlags(&sh->ev_out, local_event_flags());
       if (e != hipSuccess) return hip_fail(e, "hdd_block_assemble_sharded: event");
     }
+  }
+  const bool q1 = sh->gi.elem_type == HDD_CUBE;
+  // Q1: the pack runs on `stream` ahead of the tile launch.  Issued on the side stream beside the tile launch it
+  // waited for a free wave slot: the half-image SKIP kernel holds 256 VGPRs in each of its two waves per SIMD and
+  // all of the LDS, so a kernel beside it gets only the reserved workgroup slots -- the pack took 45 us there
+  // against 5 us alone, and the element pass behind it ended after the tiles (one-card kernel trace,
+  // profiles/r05/d_shard/).  On `stream` it costs its own few microseconds once, ahead of the launch.
+  const bool pack_first = side && q1;
+  for (int k = 0; k <= h.n_peers; ++k) h.prefix[k] = sh->send_prefix[k];
+  h.idx = sh->d_send_idx;
+  h.buf = sh->d_sbuf;
+  if (pack_first) {
+    e = launch_halo(true, h, s);
+    if (e != hipSuccess) return hip_fail(e, "hdd_block_assemble_sharded: pack");
+  }
+  if (side) {
     e = hipEventRecord(sh->ev_in, s);
     if (e == hipSuccess) e = hipStreamWaitEvent(ps, sh->ev_in, 0);
     if (e != hipSuccess) return hip_fail(e, "hdd_block_assemble_sharded: order pack after inputs");
@@ -1049,11 +1075,20 @@ extern "C" int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm*
   // 8): in place, except P1 ranks with two peers (C2 middle ranks: +10 % with the side buffer vs +14 % in place,
   // the P1 tiles' two waves per SIMD leaving the element pass no registers beside them; end ranks +4 % in place
   // vs +8 %); Q1 in place everywhere (+9 % middle / +15 % end rank at N = 8 vs +20 / +13 %)
+  //
+  // Round 5: Q1 keeps the in-place pass, now beside the half-image kernel's SKIP launch (full SKIP tiles stay on the
+  // rotated image and drop the skipped elements' chunks at the store), with the pack ahead of the launch (above).
+  // HDD_SHARD_FIX_SCATTER on Q1: the tile launch writes every row block (no SKIP), the ghost-adjacent elements go
+  // into a value-major (SoA) side buffer -- each store instruction 64 consecutive doubles -- and one wave per
+  // element writes its row block into place after the join (a kernel after the tiles: +18 % at C4 N = 8).
   const bool scatter = offfix && !(flags & HDD_SHARD_FIX_INPLACE) && (flags & HDD_SHARD_FIX_SCATTER);
+  const bool soa = scatter && q1;
   const int32_t rb = hdd_fix_rb(sh->gi.elem_type);
+  const int64_t soa_ld = (sh->n_fix + 1 + 63) & ~int64_t(63);   // SoA rows start 512-byte aligned
   std::vector<double*> fbufs;
   if (scatter) {
-    const size_t slot = size_t(sh->n_fix + 1) * size_t(rb), need = slot * size_t(n_comp);
+    const size_t slot = soa ? size_t(soa_ld) * size_t(rb) : size_t(sh->n_fix + 1) * size_t(rb);
+    const size_t need = slot * size_t(n_comp);
     if (need > sh->fixbuf_doubles) {   // first step (or more components): grow; warm up before graph capture
       if (sh->d_fixbuf) (void)hipFree(sh->d_fixbuf);
       sh->d_fixbuf = nullptr;
@@ -1068,17 +1103,17 @@ extern "C" int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm*
   // column are the element pass's), and the inputs event was recorded above, so the pack does not wait for it.
   const int32_t reserve = int32_t(std::min<int64_t>((sh->n_fix + 63) / 64, 256));
   bool first = false;
-  if (!last && offfix && !scatter) {
-    const int rc0 = hdd_assemble_skip_ghost(ctx, &m, kappa, n_comp, tensor, params, pattern, d_vals, stream, reserve);
+  if (!last && offfix && (!scatter || soa)) {
+    const int rc0 = soa ? hdd_assemble_reserve(ctx, &m, kappa, n_comp, tensor, params, pattern, d_vals, stream, reserve)
+                        : hdd_assemble_skip_ghost(ctx, &m, kappa, n_comp, tensor, params, pattern, d_vals, stream, reserve);
     if (rc0 == HDD_OK) first = true;
     else if (rc0 != HDD_ERR_UNSUPPORTED) return rc0;   // (unsupported rules: the order below)
   }
-  // 1. pack the records the peers need (one launch for every peer)
-  for (int k = 0; k <= h.n_peers; ++k) h.prefix[k] = sh->send_prefix[k];
-  h.idx = sh->d_send_idx;
-  h.buf = sh->d_sbuf;
-  e = launch_halo(true, h, ps);
-  if (e != hipSuccess) return hip_fail(e, "hdd_block_assemble_sharded: pack");
+  // 1. pack the records the peers need (one launch for every peer; Q1: done above)
+  if (!pack_first) {
+    e = launch_halo(true, h, ps);
+    if (e != hipSuccess) return hip_fail(e, "hdd_block_assemble_sharded: pack");
+  }
   // 2. post the exchange.  The receives land straight in the ghost columns: the ghosts of one owner are
   // contiguous (recv_col0), so peer k's message is R row messages [row r][count_k], each received into
   // arr(r)[row(r) ld + recv_col0[k] ...] -- no receive buffer, no unpack launch.  Sender and receiver list the
@@ -1140,7 +1175,9 @@ extern "C" int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm*
       e = launch_halo(false, h, ps);
       if (e != hipSuccess) return hip_fail(e, "hdd_block_assemble_sharded: unpack");
     }
-    rc = scatter ? hdd_assemble_elements_buf(ctx, &m, kappa, n_comp, tensor, params, pattern, fbufs.data(), sh->d_fix,
+    rc = soa       ? hdd_assemble_elements_soa(ctx, &m, kappa, n_comp, tensor, params, pattern, fbufs.data(), soa_ld,
+                                                 sh->d_fix, sh->n_fix, ps)
+         : scatter ? hdd_assemble_elements_buf(ctx, &m, kappa, n_comp, tensor, params, pattern, fbufs.data(), sh->d_fix,
                                              sh->n_fix, ps)
                  : hdd_assemble_elements_inplace(ctx, &m, kappa, n_comp, tensor, params, pattern, d_vals, sh->d_fix,
                                                  sh->n_fix, ps);
@@ -1182,7 +1219,9 @@ extern "C" int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm*
     e = hipStreamWaitEvent(s, sh->ev_out, 0);
     if (e != hipSuccess) return hip_fail(e, "hdd_block_assemble_sharded: join fixup");
     if (fix_unsupported) return hdd_swipdg_assemble(ctx, &m, kappa, n_comp, tensor, params, pattern, d_vals, stream);
-    if (scatter) return hdd_scatter_fix(ctx, pattern, rb, fbufs.data(), n_comp, sh->d_fix, sh->n_fix, d_vals, stream);
+    if (soa)
+      return hdd_scatter_fix_q1_soa(ctx, &m, pattern, fbufs.data(), soa_ld, n_comp, sh->d_fix, sh->n_fix, d_vals, stream);
+    if (scatter && !soa) return hdd_scatter_fix(ctx, pattern, rb, fbufs.data(), n_comp, sh->d_fix, sh->n_fix, d_vals, stream);
     return HDD_OK;   // in place: the join alone completes the step on `stream`
   }
   if (!transfer) {

@@ -1162,6 +1162,7 @@ struct Q1PwcPolicy : GenericPolicy<Cube, 1, 2, TK, KK, VX> {
   using E = Cube;
   static constexpr int NB = 4, NF = 4;
   static constexpr bool HALF = H2;
+  static constexpr bool EMIT = true;   // emit(): the row block one 4 x 4 block at a time (the sharded SoA fixup)
   static constexpr int WGCU = H2 ? 8 : 4, MINW = H2 ? 2 : 1;
   using Own = typename Base::Own;
   using Gat = typename Base::Gat;
@@ -1781,6 +1782,10 @@ template <class P>
 struct half_of<P, std::void_t<decltype(P::HALF)>> : std::bool_constant<P::HALF> {};
 template <class P>
 constexpr int image_blocks() { return half_of<P>::value ? 32 : 64; }
+template <class P, class = void>
+struct emit_of : std::false_type {};
+template <class P>
+struct emit_of<P, std::void_t<decltype(P::EMIT)>> : std::bool_constant<P::EMIT> {};
 
 // TL: tiles come from a.tile_list, else 0..n_tiles-1; SKIP: the sharded step's full-range launch, which leaves
 // the row blocks of elements with a ghost face neighbour to the concurrent element pass (a.skip_ghost)
@@ -1926,8 +1931,10 @@ swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
       // image (CSR order) with per-block predicates.
       constexpr int STH = IMG / 128;   // 16-byte chunks per lane per half (20)
       constexpr int NH = P::NV80 / 2;  // values per lane per half (40)
+      static_assert(STH % 4 == 0, "SKIP tiles store a half in 4 KB windows");
       const int nact = int(a.own_end - t0 < 64 ? a.own_end - t0 : 64);
-      const bool full = uni && nact == 64 && !(SKIP && gmask);   // wave-uniform
+      // (sharded SKIP tiles stay on the rotated image: their skipped elements' chunks are dropped at the store)
+      const bool full = uni && nact == 64;   // wave-uniform
       int ps, pf[P::NF];
       P::positions(e, own, ps, pf);
       // column byte offsets of the lane's own element: (x + rot) mod 20 (rotated image) or x (contiguous), x = block
@@ -2056,12 +2063,36 @@ swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
         if (hl <= 0) continue;
         const int nb = HDD_ABL(a, 2) ? 0 : hl * 8;
         const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc(out + base + hb, (short)0, nb, 0x00020000);
-        if (full) {   // 2560 values: every chunk in range, the lane part of the offset in voffset
+        const uint32_t gm = SKIP ? uint32_t(gmask >> (32 * h)) : 0u;   // this half's skipped elements
+        if (full && !gm) {   // 2560 values: every chunk in range, the lane part of the offset in voffset
 #pragma unroll
           for (int k = 0; k < STH; ++k) {
             // lane l's chunk k + 5 j (CSR chunk l + 64 (k + 5 j)) sits at hrd[k] + 5120 j in the rotated image
             const dvec2 v = *reinterpret_cast<const dvec2*>(ldsb + hrd[k % 5] + 5120 * (k / 5));
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ivec4, v), rh, 16 * lane, 1024 * k, 2);
+            // (ablation bit 8: default-policy stores instead of non-temporal ones)
+            // soffset 1024 k: an SGPR, no VALU per store.  hipcc does not pad the hazard of a VALU write to a
+            // > 8-byte store's data registers right after a store with a register soffset, and gfx950 then stores
+            // a stale first dword (round 5, the SKIP branch below in its first form); nothing but LDS reads follows
+            // these stores -- tests/test_isa_hazards.py scans the built library for the pattern.
+            if (HDD_ABL(a, 8)) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ivec4, v), rh, 16 * lane, 1024 * k, 0);
+            else __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ivec4, v), rh, 16 * lane, 1024 * k, 2);
+          }
+        } else if (full) {   // a sharded SKIP tile: chunk l + 64 k belongs to element (l + 64 k) / 40 of the half (40
+          // chunks per 640-byte row block); a skipped element's chunks get a voffset beyond the window and are
+          // dropped.  The predicate's VALU follows the stores, so no register soffset here: 4 KB windows, one buffer
+          // resource each, the offset inside in voffset + the instruction's immediate.
+#pragma unroll
+          for (int j = 0; j < STH / 4; ++j) {
+            const int nbj = nb - 4096 * j;
+            const __amdgpu_buffer_rsrc_t rj =
+                __builtin_amdgcn_make_buffer_rsrc(out + base + hb + 512 * j, (short)0, nbj > 0 ? nbj : 0, 0x00020000);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const int k = 4 * j + q;
+              const dvec2 v = *reinterpret_cast<const dvec2*>(ldsb + hrd[k % 5] + 5120 * (k / 5));
+              const uint32_t vo = (gm >> ((lane + 64 * k) / 40)) & 1u ? 0x40000000u : 16u * lane;
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ivec4, v), rj, vo + 1024 * q, 0, 2);
+            }
           }
         } else {      // the range check drops the chunks beyond the half; skipped elements' chunks go out of range
 #pragma unroll
@@ -2315,6 +2346,19 @@ __global__ void __launch_bounds__(64) swipdg_elements_buf_kernel(const AssembleA
     P::load_own(a, e, own);
     P::load_gat(a, e, own, gat);
     P::load_gat2(a, gat);
+    if constexpr (emit_of<P>::value) {
+      if (a.list_elements == 4) {   // value-major side buffer: canonical value k of list entry i at vals[0][k fix_ld + i]
+        double* const buf = a.vals[0] + i;
+        P::emit(a, own, gat, [&](int b, const double (&blk)[P::NB][P::NB]) {
+          if (!act) return;
+#pragma unroll
+          for (int r = 0; r < P::NB; ++r)
+#pragma unroll
+            for (int c = 0; c < P::NB; ++c) buf[int64_t(r * P::VR + b * P::NB + c) * a.fix_ld] = blk[r][c];
+        });
+        continue;
+      }
+    }
     [[maybe_unused]] typename fused_of<P>::Shared shv;
     if constexpr (FUSED) P::prepare(a, own, shv);
     const int ncomp = FUSED ? a.n_comp : 1;
@@ -2375,12 +2419,13 @@ static hipError_t launch_persistent(const AssembleArgs& a, hipStream_t s)
   // HDD_P1_WGCU sweep override, read once per context
   int wgcu = a.wgcu > 0 ? a.wgcu : P::WGCU;
   wgcu = std::max(1, std::min<int>(wgcu, int((160 * 1024) / lds)));   // resident by LDS (Q1 tiles: 3 per CU)
-  // The sharded step's full-range launch (skip_ghost) runs beside the in-place element pass: the grid is shortened
+  // The sharded step's full-range launch (SKIP, or every tile beside the SoA side-buffer pass) runs beside the
+  // element pass: the grid is shortened
   // by the pass's workgroups (a multiple of 8 keeps the XCD eighths even), so the pass gets SIMDs of its own
   // instead of slowing the persistent waves it would share them with.  C4 N = 8 middle rank +9.2 -> +7.8 %, C2 N = 8
   // end rank +4.9 -> +2.0 % over one launch (profiles/r04/e_reserve/; ablation bit 4194304: no reserve).
   int64_t slots = int64_t(cus) * wgcu;
-  const bool reserve = a.skip_ghost && a.reserve_wg > 0 && !HDD_ABL(a, 4194304);
+  const bool reserve = a.reserve_wg > 0 && !HDD_ABL(a, 4194304);
   if (reserve) slots = std::max<int64_t>(8, (slots - a.reserve_wg) & ~int64_t(7));
   const int64_t G = std::min<int64_t>(tiles, slots);
   const int n_launch = fused_of<P>::value ? 1 : a.n_comp;   // a FUSED policy emits every component per tile
@@ -2389,6 +2434,7 @@ static hipError_t launch_persistent(const AssembleArgs& a, hipStream_t s)
     const int64_t ge = std::min<int64_t>((a.n_tile_list + 63) / 64, int64_t(cus) * 4);
     if (a.list_elements >= 2) {   // no LDS: into the side buffers (2: slot RB doubles) or in place (3)
       if (a.list_elements == 2 && a.fix_rb != P::RB) return hipErrorInvalidValue;
+      if (a.list_elements == 4 && (!emit_of<P>::value || a.fix_ld < a.n_tile_list + 1)) return hipErrorInvalidValue;
       for (int c = 0; c < n_launch; ++c) {
         AssembleArgs ac = a;
         if (!fused_of<P>::value) {

@@ -39,6 +39,7 @@ struct AssembleArgs {
                                // 2: the same, row blocks into side buffers vals[c] of fix_rb doubles per element;
                                // 3: the same, in place without LDS (beside a skip_ghost assembly)
   int32_t fix_rb;
+  int64_t fix_ld;              // list_elements == 4: leading dimension of the value-major side buffers
   int32_t skip_ghost;          // 1: tiles do not store the row blocks of elements with a ghost face neighbour
   int32_t reserve_wg;          // skip_ghost launches: workgroup slots left free for the concurrent element pass
   const int32_t* ev;           // optional vertex-indexed geometry: element -> local vertex ids [nvpe][n_local]
@@ -166,6 +167,9 @@ hipError_t launch_assemble(const AssembleArgs& a, int nqv, int nqf, hipStream_t 
 // products of P1 / Q1 meshes with piecewise-constant kappa on the persistent tile driver (closed forms);
 // *supported = false: use launch_product
 hipError_t launch_product_fast(const AssembleArgs& a, int product, hipStream_t s, bool* supported);
+// the sharded Q1 step's value-major side buffers (list_elements == 4) into place (swipdg_q1.hip): a.tile_list /
+// n_tile_list = the listed elements, a.elem_ptr / nbrs / finfo / n_local / own_begin / n_cu
+hipError_t launch_q1_scatter_soa(const AssembleArgs& a, const double* buf, int64_t ld, double* vals, hipStream_t s);
 
 }  // namespace dev
 }  // namespace hdd

@@ -350,7 +350,10 @@ int hdd_swipdg_assemble_elements(hdd_ctx* ctx, const hdd_mesh* mesh, const hdd_s
  * ord(kappa) + ord(A) + p - 1 + ord(g_D)).  2d meshes with Dirichlet or Neumann data: two launches (volume
  * kernel, then a face kernel over the boundary elements the first one listed) on a list the context holds
  * (16 B per owned element, allocated on the first call of a size class: warm a context up before hipGraph
- * capture; one stream at a time per context). */
+ * capture).  Eager calls of one context on different streams are ordered behind each other by the library (an
+ * event on the previous call's stream).  A CAPTURED call is not: the replays of a graph that captured an
+ * hdd_swipdg_rhs call of context C must not run concurrently with eager hdd_swipdg_rhs calls of C or with replays
+ * of another such graph of C (they share C's list); use a separate context per concurrent graph / stream. */
 int hdd_swipdg_rhs(hdd_ctx* ctx, const hdd_mesh* mesh, const hdd_scalar_fn* force, const hdd_scalar_fn* kappa,
                    const hdd_tensor_fn* tensor, const hdd_scalar_fn* dirichlet, const hdd_scalar_fn* neumann,
                    const hdd_swipdg_params* params, double* d_rhs, void* stream);
@@ -519,7 +522,8 @@ int hdd_shard_pattern_fill(hdd_ctx* ctx, const hdd_shard* sh, int64_t* d_row_ptr
                            int64_t* d_elem_ptr, void* stream);
 
 enum {
-  HDD_SHARD_NO_OVERLAP = 1,     /* exchange, then assemble every tile (default: the assembly overlaps the halo) */
+  HDD_SHARD_NO_OVERLAP = 1,     /* exchange, then assemble every tile (the default on Q1 shards; P1 shards overlap
+                                   the assembly with the halo) */
   HDD_SHARD_HALO_GEOMETRY = 2,  /* also send the ghost vertex coordinates (default: geometry is rank-local) */
   HDD_SHARD_NO_HALO = 4,        /* ghost columns already valid (static coefficients): no exchange at all */
   HDD_SHARD_NO_TRANSFER = 8,    /* timing studies only: pack and split tile launches as in an exchange, a
@@ -528,15 +532,17 @@ enum {
                                    upper bound of the GPU-side cost of the sharded step */
   HDD_SHARD_SPLIT_TILES = 16,   /* overlap by tiles: interior tiles during the exchange, the tiles with a
                                    ghost-adjacent element after it -- the default for P1 shards with two peers;
-                                   otherwise the default is every tile during the exchange and the ghost-adjacent
-                                   ELEMENTS again, off-stream, in place (HDD_SHARD_FIX_INPLACE) */
+                                   other P1 shards default to every tile during the exchange and the ghost-adjacent
+                                   ELEMENTS again, off-stream, in place (HDD_SHARD_FIX_INPLACE); Q1 shards to the
+                                   serial step (HDD_SHARD_NO_OVERLAP; measured fastest) */
   HDD_SHARD_FIX_INLINE = 32,    /* study (round 3 A/B): the ghost-adjacent elements recomputed on `stream` after
                                    the wait (default: on the transfer stream right after the receives, beside the
                                    assembly) */
-  HDD_SHARD_FIX_SCATTER = 64,   /* study: the off-stream fixup into a side buffer, copied into place by one kernel
-                                   after the join (the assembly's tiles store every row block) */
-  HDD_SHARD_FIX_INPLACE = 128,  /* the off-stream fixup in place, the assembly's tiles skip those row blocks:
-                                   default except on P1 shards with two peers (HDD_SHARD_SPLIT_TILES) */
+  HDD_SHARD_FIX_SCATTER = 64,   /* the off-stream fixup into a side buffer, copied into place by one kernel after the
+                                   join (the assembly's tiles store every row block; Q1: a value-major buffer, one
+                                   full-range half-image launch beside the element pass) */
+  HDD_SHARD_FIX_INPLACE = 128,  /* the off-stream fixup in place, the assembly's tiles skip those row blocks (a SKIP
+                                   launch; Q1: the pack on `stream` ahead of it): the default on P1 end ranks */
   HDD_SHARD_LAUNCH_LAST = 256   /* ablation builds only (round 3's order, measured and rejected): with the in-place
                                    fixup, enqueue the full-range launch after the halo work instead of before it;
                                    the product library ignores it */

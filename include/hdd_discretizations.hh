@@ -1327,15 +1327,18 @@ class BlockSWIPDG : public SWIPDG {
     internal::check(hdd_block_operators_map_device(ctx_, &pat, n_ops, rng.data(), rp->get(), col->get(), nullptr,
                                                    nullptr, nullptr), "hdd_block_operators_map_device");
 #else
-    // debug builds (and the test programs, built without NDEBUG): the device returns the operators' offsets from
-    // the pattern itself, which must equal the face-pair counts the arrays above were sized with
+    // debug builds (and the test programs, built without NDEBUG): the device first returns the operators' offsets
+    // from the pattern itself (row pointers only, no column writes), which must equal the face-pair counts the
+    // column array was sized with -- checked BEFORE any column is written -- then fills the columns
     std::vector<int64_t> dev_off(size_t(n_ops) + 1);
-    internal::check(hdd_block_operators_map_device(ctx_, &pat, n_ops, rng.data(), rp->get(), col->get(), nullptr,
-                                                   dev_off.data(), nullptr), "hdd_block_operators_map_device");
+    internal::check(hdd_block_operators_map_device(ctx_, &pat, n_ops, rng.data(), rp->get(), nullptr, nullptr,
+                                                   dev_off.data(), nullptr), "hdd_block_operators_map_device (count)");
     for (int32_t k = 0; k <= n_ops; ++k)
       if (dev_off[size_t(k)] != noff[size_t(k)])
         throw std::runtime_error("BlockSWIPDG::extract_operators: the pattern's operator sizes differ from the face-pair "
                                  "counts (operator " + std::to_string(k) + ")");
+    internal::check(hdd_block_operators_map_device(ctx_, &pat, n_ops, rng.data(), rp->get(), col->get(), nullptr,
+                                                   nullptr, nullptr), "hdd_block_operators_map_device");
 #endif
     std::vector<std::shared_ptr<internal::DeviceArray<double>>> all;   // affine first, then the components
     std::vector<const double*> in;

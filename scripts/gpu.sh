@@ -26,7 +26,7 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 fail() { echo "step '$1' rc=$2 -- stopping"; exit "$2"; }
 for step in "$@"; do
-  set -- $step
+  eval "set -- $step"   # (a step may quote an argument: "tests -k 'sharded or watchdog'")
   kind=$1; shift
   case $kind in
     tests)
