@@ -1120,6 +1120,7 @@ extern "C" int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm*
   // rows in the same order (the layout depends on the kinds only), which is how RCCL / the host transports
   // match repeated (peer) messages.
   int rc = HDD_OK;
+  double* loop_buf = sh->d_rbuf;   // what the loopback's unpack reads
   if (transfer) {
     std::vector<int32_t> mp;
     std::vector<const double*> ms;
@@ -1144,6 +1145,13 @@ extern "C" int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm*
         hipEventRecord(sh->ev_out, ps) != hipSuccess)
       rc = set_error(HDD_ERR_HIP, "hdd_block_assemble_sharded: host transport event");
   } else {   // timing studies: the receive buffers get this rank's own messages (stream-ordered device copies)
+    // With equal send and receive counts per peer (every halo here: ghost layers are symmetric) the loopback is ONE
+    // kernel, the unpack reading the send buffer -- as the transfer is: RCCL's group kernel receives straight into
+    // the ghost columns.  (Round 4 and earlier: a copy per peer + the unpack, i.e. 2-3 kernels for one transfer.)
+    bool same = true;
+    for (int k = 0; k < h.n_peers; ++k)
+      same = same && sh->send_prefix[k + 1] - sh->send_prefix[k] == sh->recv_prefix[k + 1] - sh->recv_prefix[k];
+    if (same) loop_buf = sh->d_sbuf;
     std::vector<const double*> sp(size_t(h.n_peers));
     std::vector<double*> rp(size_t(h.n_peers));
     std::vector<int64_t> sn(size_t(h.n_peers)), rn(size_t(h.n_peers));
@@ -1153,7 +1161,7 @@ extern "C" int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm*
       rp[k] = sh->d_rbuf + int64_t(R) * sh->recv_prefix[k];
       rn[k] = int64_t(R) * (sh->recv_prefix[k + 1] - sh->recv_prefix[k]);
     }
-    for (int k = 0; k < h.n_peers && rc == HDD_OK; ++k) {
+    for (int k = 0; k < h.n_peers && rc == HDD_OK && !same; ++k) {
       const int64_t n = std::min(sn[k], rn[k]);
       if (n > 0 && hipMemcpyAsync(rp[k], sp[k], size_t(n) * sizeof(double), hipMemcpyDeviceToDevice, ps) != hipSuccess)
         rc = set_error(HDD_ERR_HIP, "hdd_block_assemble_sharded: loopback copy");
@@ -1171,7 +1179,7 @@ extern "C" int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm*
       for (int k = 0; k <= h.n_peers; ++k) h.prefix[k] = sh->recv_prefix[k];
       for (int k = 0; k < h.n_peers; ++k) h.col0[k] = sh->recv_col0[k];
       h.idx = nullptr;
-      h.buf = sh->d_rbuf;
+      h.buf = loop_buf;
       e = launch_halo(false, h, ps);
       if (e != hipSuccess) return hip_fail(e, "hdd_block_assemble_sharded: unpack");
     }
@@ -1230,7 +1238,7 @@ extern "C" int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm*
     for (int k = 0; k <= h.n_peers; ++k) h.prefix[k] = sh->recv_prefix[k];
     for (int k = 0; k < h.n_peers; ++k) h.col0[k] = sh->recv_col0[k];
     h.idx = nullptr;
-    h.buf = sh->d_rbuf;
+    h.buf = loop_buf;
     e = launch_halo(false, h, s);
     if (e != hipSuccess) return hip_fail(e, "hdd_block_assemble_sharded: unpack");
   }

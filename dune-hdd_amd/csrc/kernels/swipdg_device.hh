@@ -2074,7 +2074,14 @@ swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
             // > 8-byte store's data registers right after a store with a register soffset, and gfx950 then stores
             // a stale first dword (round 5, the SKIP branch below in its first form); nothing but LDS reads follows
             // these stores -- tests/test_isa_hazards.py scans the built library for the pattern.
+            // Cache policy nt (aux 2).  nt + sc1 (aux 18) measured 0.5350 -> 0.5208 ms in interleaved 10-launch
+            // loops but +1.0 % in the bench's own 20 / 5 window against the nt library (same box, 3 alternations):
+            // kept nt (profiles/r05/f_aux/).  Ablation bits 8 / 1024 / 2048 / 4096: default policy, nt + sc1, sc1,
+            // sc0 + nt.
             if (HDD_ABL(a, 8)) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ivec4, v), rh, 16 * lane, 1024 * k, 0);
+            else if (HDD_ABL(a, 1024)) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ivec4, v), rh, 16 * lane, 1024 * k, 18);
+            else if (HDD_ABL(a, 2048)) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ivec4, v), rh, 16 * lane, 1024 * k, 16);
+            else if (HDD_ABL(a, 4096)) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ivec4, v), rh, 16 * lane, 1024 * k, 3);
             else __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ivec4, v), rh, 16 * lane, 1024 * k, 2);
           }
         } else if (full) {   // a sharded SKIP tile: chunk l + 64 k belongs to element (l + 64 k) / 40 of the half (40
@@ -2194,6 +2201,14 @@ swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
         }
       }
     };
+    // uniform-tile 16-byte stores (ablation bits 1024 / 2048 / 4096: nt + sc1, sc1, sc0 + nt instead of nt; C2
+    // measured within noise of nt for each, 20 interleaved rounds, profiles/r05/f_aux/)
+    auto st128 = [&](const dvec2& v, int off) {
+      if (HDD_ABL(a, 1024)) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ivec4, v), rsrc, off, 0, 18);
+      else if (HDD_ABL(a, 2048)) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ivec4, v), rsrc, off, 0, 16);
+      else if (HDD_ABL(a, 4096)) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ivec4, v), rsrc, off, 0, 3);
+      else __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ivec4, v), rsrc, off, 0, 2);
+    };
     auto stores = [&](bool front) {
       if (gmask) {
         if (!front) stores_skip();
@@ -2218,7 +2233,7 @@ swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
             if ((k < ksplit) != front) continue;
             const int d = 2 * (lane + 64 * k);
             const dvec2 v = *reinterpret_cast<const dvec2*>(lds + at(d <= dmax ? d : 0));
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ivec4, v), rsrc, d * 8, 0, 2);
+            st128(v, d * 8);
           }
         } else {
 #pragma unroll
@@ -2229,7 +2244,7 @@ swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
             dvec2 v;
             v.x = lds[at(d)];
             v.y = lds[at(d + 1)];
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ivec4, v), rsrc, m2 * 8, 0, 2);
+            st128(v, m2 * 8);
           }
         }
       } else {

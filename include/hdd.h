@@ -526,8 +526,9 @@ enum {
                                    the assembly with the halo) */
   HDD_SHARD_HALO_GEOMETRY = 2,  /* also send the ghost vertex coordinates (default: geometry is rank-local) */
   HDD_SHARD_NO_HALO = 4,        /* ghost columns already valid (static coefficients): no exchange at all */
-  HDD_SHARD_NO_TRANSFER = 8,    /* timing studies only: pack and split tile launches as in an exchange, a
-                                   loopback copy + unpack kernel instead of the transfer (comm may be NULL; the
+  HDD_SHARD_NO_TRANSFER = 8,    /* timing studies only: pack and split tile launches as in an exchange, one
+                                   loopback kernel instead of the transfer -- the unpack, reading the send buffer
+                                   (a copy per peer first when send and receive counts differ) (comm may be NULL; the
                                    ghost columns receive the rank's own send buffers, i.e. wrong values) -- an
                                    upper bound of the GPU-side cost of the sharded step */
   HDD_SHARD_SPLIT_TILES = 16,   /* overlap by tiles: interior tiles during the exchange, the tiles with a

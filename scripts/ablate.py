@@ -61,7 +61,7 @@ def main():
             runs.append((cfg, f, workload(cfg, ctxs[f])))
     os.environ["HDD_DEBUG_FLAGS"] = "0"
     res = {(c, f): [] for c, f, _ in runs}
-    for rnd in range(6):
+    for rnd in range(int(os.environ.get("ABLATE_ROUNDS", "6"))):
         for cfg, f, fn in runs:
             for _ in range(3):
                 fn()
