@@ -285,6 +285,15 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kernel_label = H.last_tile_kernel()
+    # at N > 1 the ranks may dispatch different kernels (P1 middle ranks split their tiles: tile-list kernels; end
+    # ranks the SKIP launch): every rank's label, grouped
+    kernels_by_rank = None
+    if world > 1:
+        labels = [None] * world
+        dist.all_gather_object(labels, kernel_label)
+        kernels_by_rank = {}
+        for r_, lab in enumerate(labels):
+            kernels_by_rank.setdefault(lab, []).append(r_)
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in events])) / (1 if per_step else args.steps)
     t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64)
     if world > 1:
@@ -323,8 +332,10 @@ def main():
         if world > 1 and args.halo == "once":
             halo_desc = ", face halo exchanged once at setup (static mesh and coefficients)"
         elif world > 1:
+            # the library's default schedule: Q1 (c4) exchange first, then every tile; P1 (c2) overlapped
+            overlapped = not args.no_overlap and not c4
             halo_desc = ", %s face halo%s" % ("RCCL" if args.backend == "nccl" else "gloo host-staged (rehearsal)",
-                                              " overlapped with interior tiles" if not args.no_overlap else "")
+                                              " overlapped with the tiles" if overlapped else ", then every tile")
         if att is None:
             att = attainable_hbm(torch)
         cpu = None
@@ -363,6 +374,7 @@ def main():
                          # the dominant kernel as the library's dispatch picked it in the last timed step
                          # (hdd_last_tile_kernel, rank 0)
                          "kernel": kernel_label,
+                         "kernels_by_rank": kernels_by_rank,
                          # event-timed average step on the assembly stream (one event pair around the K steps, so
                          # dispatch gaps -- and at N > 1 the step's pack / exchange / element pass -- are included)
                          "step_ms_event": kernel_ms, "step_ms_event_max_rank": kernel_ms_max,
