@@ -2015,7 +2015,9 @@ swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
           }
         }
       };
-      if (!HDD_ABL(a, 1)) P::emit(a, own, gat, put0);
+      // (ablation bit 8192: tiles off the rotated-image path skip their compute and stores -- what they cost)
+      const bool abl_nf = HDD_ABL(a, 8192) && !full;
+      if (!HDD_ABL(a, 1) && !abl_nf) P::emit(a, own, gat, put0);
       // sharded step: image ranges of the skipped elements, tile coordinates (as in stores_skip below)
       constexpr int NR = 4;
       int rb[NR], re[NR];
@@ -2060,7 +2062,7 @@ swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         if (h == 1 && !HDD_ABL(a, 4)) P::load_gat(a, en, own_n, gat_n);   // first gather stage of tile t+1
-        if (hl <= 0) continue;
+        if (hl <= 0 || abl_nf) continue;
         const int nb = HDD_ABL(a, 2) ? 0 : hl * 8;
         const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc(out + base + hb, (short)0, nb, 0x00020000);
         const uint32_t gm = SKIP ? uint32_t(gmask >> (32 * h)) : 0u;   // this half's skipped elements
