@@ -746,6 +746,21 @@ __device__ __forceinline__ void p1_load_gat2(const AssembleArgs& a, P1Gat& g)
 // P1 closed-form per-element math on preloaded data (role form, see above); writes the row block into `img`.
 // PEN: only the interior-penalty terms (the SWIPDG penalty product, swipdg.hh:462-508), no volume and no
 // consistency / symmetry terms.
+// the element's own block from one face: S_ij += -c (Ae_j [i != fc] + Ae_i [j != fc]) + (pen / 3 or pen / 6 on the
+// face's vertex pairs), c = |F| / 2 times the consistency weight (fc: the vertex opposite the face)
+__device__ __forceinline__ void p1_face_self(double (&S)[3][3], const double (&Ae)[3], int fc, double c, double penT,
+                                             double penS)
+{
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = i; j < 3; ++j) {   // the block is symmetric: the upper triangle (p1_compute mirrors it)
+      if (i == fc && j == fc) continue;
+      const double v = i == fc ? Ae[i] : (j == fc ? Ae[j] : Ae[i] + Ae[j]);
+      S[i][j] = fma(-c, v, S[i][j] + (i == fc || j == fc ? 0.0 : (i == j ? penT : penS)));
+    }
+}
+
 template <bool PEN = false>
 __device__ __forceinline__ void p1_compute(const AssembleArgs& a, int64_t e, const P1Own& o, const P1Gat& gt,
                                            double* img)
@@ -788,7 +803,7 @@ __device__ __forceinline__ void p1_compute(const AssembleArgs& a, int64_t e, con
 #pragma unroll
     for (int i = 0; i < 3; ++i)
 #pragma unroll
-      for (int j = 0; j < 3; ++j) S[i][j] = fac * (Ag[j][0] * g[i][0] + Ag[j][1] * g[i][1]);
+      for (int j = i; j < 3; ++j) S[i][j] = fac * (Ag[j][0] * g[i][0] + Ag[j][1] * g[i][1]);   // symmetric A
   }
   constexpr double CS = PEN ? 0.0 : 1.0;   // consistency / symmetry terms on (stiffness) or off (penalty)
 #pragma unroll
@@ -827,40 +842,34 @@ __device__ __forceinline__ void p1_compute(const AssembleArgs& a, int64_t e, con
       const double AnB = ((Oy - Ay) * mx + (Ax - Ox) * my) * iD;
       const double AnO = ((Ay - By) * mx + (Bx - Ax) * my) * iD;
       const int jA = rev ? tb : ta, jB = rev ? ta : tb;
-      const double cpl = -w_plus * kn * CS;
-      const double sym = w_minus * ke * CS;
+      // the face's constants folded once (half = |F| / 2, third, sixth = the P1 trace mass entries), so every entry
+      // is a two-FMA chain (fc, fa, fb are compile-time per unrolled face)
+      const double cplh = -w_plus * kn * CS * half;
+      const double symh = w_minus * ke * CS * half;
+      const double penT = pen * third, penS = pen * sixth;
 #pragma unroll
       for (int i = 0; i < 3; ++i) {
         double* row = img + i * rowlen + pos[f] * 3;
-        const double m1i = i == fc ? 0.0 : half;
-        row[jA] = cpl * AnA * m1i + sym * Ae[i] * half - pen * (i == fc ? 0.0 : (i == fa ? third : sixth));
-        row[jB] = cpl * AnB * m1i + sym * Ae[i] * half - pen * (i == fc ? 0.0 : (i == fb ? third : sixth));
-        row[to] = cpl * AnO * m1i;
-      }
-#pragma unroll
-      for (int i = 0; i < 3; ++i)
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          const double m1i = i == fc ? 0.0 : half, m1j = j == fc ? 0.0 : half;
-          const double mm = (i == fc || j == fc) ? 0.0 : (i == j ? third : sixth);
-          S[i][j] += -w_minus * ke * CS * (Ae[j] * m1i + Ae[i] * m1j) + pen * mm;
+        if (i == fc) {
+          row[jA] = symh * Ae[i];
+          row[jB] = symh * Ae[i];
+          row[to] = 0.0;
+        } else {
+          row[jA] = fma(cplh, AnA, fma(symh, Ae[i], -(i == fa ? penT : penS)));
+          row[jB] = fma(cplh, AnB, fma(symh, Ae[i], -(i == fb ? penT : penS)));
+          row[to] = cplh * AnO;
         }
+      }
+      p1_face_self(S, Ae, fc, symh, penT, penS);
     } else {
       const double pen = (a.sigma_boundary * ke * dm) * ihp;
-#pragma unroll
-      for (int i = 0; i < 3; ++i)
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          const double m1i = i == fc ? 0.0 : half, m1j = j == fc ? 0.0 : half;
-          const double mm = (i == fc || j == fc) ? 0.0 : (i == j ? third : sixth);
-          S[i][j] += -ke * CS * (Ae[j] * m1i + Ae[i] * m1j) + pen * mm;
-        }
+      p1_face_self(S, Ae, fc, ke * CS * half, pen * third, pen * sixth);
     }
   }
 #pragma unroll
   for (int i = 0; i < 3; ++i)
 #pragma unroll
-    for (int j = 0; j < 3; ++j) img[i * rowlen + pos_self * 3 + j] = S[i][j];
+    for (int j = 0; j < 3; ++j) img[i * rowlen + pos_self * 3 + j] = j >= i ? S[i][j] : S[j][i];
 }
 
 typedef int ivec4 __attribute__((ext_vector_type(4)));
