@@ -1457,11 +1457,14 @@ struct P1SmoothPolicy {
       pos[f] = p;
     }
     const int rowlen = nblk * 3;
+    // the own block is symmetric (volume g_i.A g_j, face terms symmetric in i, j): its upper triangle, mirrored at
+    // the end
     double S[3][3];
+    const double vol = adet * kv;
 #pragma unroll
     for (int i = 0; i < 3; ++i)
 #pragma unroll
-      for (int j = 0; j < 3; ++j) S[i][j] = adet * kv * (Ag[j][0] * g[i][0] + Ag[j][1] * g[i][1]);
+      for (int j = i; j < 3; ++j) S[i][j] = vol * (Ag[j][0] * g[i][0] + Ag[j][1] * g[i][1]);
 #pragma unroll
     for (int f = 0; f < 3; ++f) {
       const int32_t n = o.nbr[f];
@@ -1514,30 +1517,33 @@ struct P1SmoothPolicy {
         const double AnB = ((Oy - Ay) * mx + (Ax - Ox) * my) * iD;
         const double AnO = ((Ay - By) * mx + (Bx - Ax) * my) * iD;
         const int jA = rev ? tb : ta, jB = rev ? ta : tb;
+        // per-face products once: each entry a two-FMA chain
+        const double wA = -w_plus * AnA, wB = -w_plus * AnB, wO = -w_plus * AnO;
+        const double wka = w_minus * k1a, wkb = w_minus * k1b;
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
           double* row = img + i * rowlen + pos[f] * 3;
           const double m1i = M1(i);
-          row[jA] = -w_plus * AnA * m1i + w_minus * Ae[i] * k1a - pc * MM(i, fa);
-          row[jB] = -w_plus * AnB * m1i + w_minus * Ae[i] * k1b - pc * MM(i, fb);
-          row[to] = -w_plus * AnO * m1i;
+          row[jA] = fma(wA, m1i, fma(Ae[i], wka, -pc * MM(i, fa)));
+          row[jB] = fma(wB, m1i, fma(Ae[i], wkb, -pc * MM(i, fb)));
+          row[to] = wO * m1i;
         }
 #pragma unroll
         for (int i = 0; i < 3; ++i)
 #pragma unroll
-          for (int j = 0; j < 3; ++j) S[i][j] += -w_minus * (Ae[j] * M1(i) + Ae[i] * M1(j)) + pc * MM(i, j);
+          for (int j = i; j < 3; ++j) S[i][j] += -w_minus * (Ae[j] * M1(i) + Ae[i] * M1(j)) + pc * MM(i, j);
       } else {   // Dirichlet: SWIPDG::BoundaryLHS, penalty sigma_b kappa (n.An) / |F|^beta
         const double pc = (a.sigma_boundary * dm) * ihp;
 #pragma unroll
         for (int i = 0; i < 3; ++i)
 #pragma unroll
-          for (int j = 0; j < 3; ++j) S[i][j] += -(Ae[j] * M1(i) + Ae[i] * M1(j)) + pc * MM(i, j);
+          for (int j = i; j < 3; ++j) S[i][j] += -(Ae[j] * M1(i) + Ae[i] * M1(j)) + pc * MM(i, j);
       }
     }
 #pragma unroll
     for (int i = 0; i < 3; ++i)
 #pragma unroll
-      for (int j = 0; j < 3; ++j) img[i * rowlen + pos_self * 3 + j] = S[i][j];
+      for (int j = 0; j < 3; ++j) img[i * rowlen + pos_self * 3 + j] = j >= i ? S[i][j] : S[j][i];
   }
 };
 
