@@ -655,6 +655,13 @@ extern "C" int hdd_comm_post(hdd_comm* c, int32_t n_peers, const int32_t* peers,
   return comm_post(c, n_peers, peers, d_send, send_count, d_recv, recv_count, stream, false);
 }
 
+extern "C" int hdd_comm_post_direct(hdd_comm* c, int32_t n_peers, const int32_t* peers, const double* const* d_send,
+                                    const int64_t* send_count, double* const* d_recv, const int64_t* recv_count,
+                                    void* stream)
+{
+  return comm_post(c, n_peers, peers, d_send, send_count, d_recv, recv_count, stream, true);
+}
+
 extern "C" int hdd_comm_wait(hdd_comm* c, void* stream)
 {
   if (!c) return set_error(HDD_ERR_INVALID, "hdd_comm_wait: null comm");

@@ -194,6 +194,7 @@ def lib():
         "hdd_comm_create_device": (_I32, [_VP, _I32, _I32, _VP]),
         "hdd_comm_destroy": (None, [_VP]),
         "hdd_comm_post": (_I32, [_VP, _I32, _VP, _VP, _VP, _VP, _VP, _VP]),
+        "hdd_comm_post_direct": (_I32, [_VP, _I32, _VP, _VP, _VP, _VP, _VP, _VP]),
         "hdd_comm_wait": (_I32, [_VP, _VP]),
         "hdd_shard_create": (_I32, [_VP, _VP, _I32, _I32, _VP, _VP]),
         "hdd_shard_halo_lists": (_I32, [_VP, _VP, _VP, _VP, _VP, _VP]),
@@ -875,8 +876,9 @@ class Comm:
         _check(lib().hdd_comm_create_device(hub.h, rank, device, C.byref(h)), "hdd_comm_create_device")
         return cls(h, keep=hub)
 
-    def post(self, peers, sends, recvs, stream=None):
-        """hdd_comm_post of device tensors (float64), then the caller calls wait()."""
+    def post(self, peers, sends, recvs, stream=None, direct=False):
+        """hdd_comm_post (direct: hdd_comm_post_direct, RCCL on `stream` itself) of device tensors (float64), then
+        the caller calls wait()."""
         torch = _torch()
         n = len(peers)
         pe = (C.c_int32 * n)(*peers)
@@ -885,7 +887,8 @@ class Comm:
         sc = (C.c_int64 * n)(*[t.numel() for t in sends])
         rc = (C.c_int64 * n)(*[t.numel() for t in recvs])
         s = stream if stream is not None else torch.cuda.current_stream().cuda_stream
-        _check(lib().hdd_comm_post(self.h, n, pe, sp, sc, rp, rc, C.c_void_p(s)), "hdd_comm_post")
+        fn = lib().hdd_comm_post_direct if direct else lib().hdd_comm_post
+        _check(fn(self.h, n, pe, sp, sc, rp, rc, C.c_void_p(s)), "hdd_comm_post")
 
     def wait(self, stream=None):
         torch = _torch()

@@ -478,6 +478,11 @@ void hdd_comm_destroy(hdd_comm* comm);
  * work enqueued on `stream` afterwards overlaps it until hdd_comm_wait(comm, stream). */
 int hdd_comm_post(hdd_comm* comm, int32_t n_peers, const int32_t* peers, const double* const* d_send,
                   const int64_t* send_count, double* const* d_recv, const int64_t* recv_count, void* stream);
+/* The same exchange ordered on `stream` itself: RCCL runs the group send/recv on `stream` (no transfer stream, no
+ * cross-stream events -- for callers that overlap nothing with it, as the serial sharded step); other transports
+ * behave as hdd_comm_post.  hdd_comm_wait(comm, stream) is then a no-op on that stream. */
+int hdd_comm_post_direct(hdd_comm* comm, int32_t n_peers, const int32_t* peers, const double* const* d_send,
+                         const int64_t* send_count, double* const* d_recv, const int64_t* recv_count, void* stream);
 /* make `stream` wait for the receives of the last hdd_comm_post (no host blocking with RCCL) */
 int hdd_comm_wait(hdd_comm* comm, void* stream);
 

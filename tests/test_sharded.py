@@ -194,6 +194,18 @@ def test_rccl_self_exchange():
         comm.wait()
     torch.cuda.synchronize()
     assert torch.equal(a, b)
+    # hdd_comm_post_direct (the serial sharded step's form): the group on the caller's stream, wait a no-op there;
+    # a kernel enqueued right after it on that stream sees the received values
+    s = torch.cuda.Stream()
+    c = torch.full((1000,), -1.0, dtype=torch.float64, device="cuda")
+    with torch.cuda.stream(s):
+        for k in range(3):
+            a.add_(1.0)
+            comm.post([0], [a], [c], stream=s.cuda_stream, direct=True)
+            comm.wait(stream=s.cuda_stream)
+            d = c * 2.0
+    torch.cuda.synchronize()
+    assert torch.equal(c, a) and torch.equal(d, a * 2.0)
     del comm
 
 
