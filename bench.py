@@ -47,10 +47,10 @@ def parse():
     ap.add_argument("--ny", type=int, default=0, help="c2: 640; c4: 1200")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU work of the baseline sample")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r05", "traffic.json"),
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r06", "traffic.json"),
                     help="PMC traffic summary (scripts/traffic_summary.py); used only when its build_id matches the "
                          "timed libhdd_amd.so")
-    ap.add_argument("--kernel-times-json", default=os.path.join(ROOT, "profiles", "r05", "kernel_times.json"),
+    ap.add_argument("--kernel-times-json", default=os.path.join(ROOT, "profiles", "r06", "kernel_times.json"),
                     help="rocprofv3 kernel durations per workload (scripts/kernel_times.py); used only when its build_id "
                          "matches the timed libhdd_amd.so and its kernel the dispatched one")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
@@ -295,9 +295,14 @@ def main():
         for r_, lab in enumerate(labels):
             kernels_by_rank.setdefault(lab, []).append(r_)
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in events])) / (1 if per_step else args.steps)
+    # max over ranks: wall time, event-timed step; sum over ranks: algorithmic bytes (every rank assembles its own rows)
     t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64)
+    per_rank = torch.tensor([[float(alg_bytes), kernel_ms]], dtype=torch.float64)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        gathered = [torch.zeros_like(per_rank) for _ in range(world)]
+        dist.all_gather(gathered, per_rank)
+        per_rank = torch.cat(gathered)
     elapsed, kernel_ms_max = float(t[0]), float(t[1])
     if not np.isfinite(vals[0][:1024].cpu().numpy()).all():
         raise SystemExit("non-finite values: a ghost column was not filled by the halo")
@@ -305,29 +310,47 @@ def main():
     value = total_dofs * args.steps / elapsed
 
     if rank == 0:
-        achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
+        # roofline of the whole job: every rank's algorithmic bytes / the slowest rank's event-timed step, against N x
+        # the per-GPU peak (at N = 1: this rank's bytes / its step); slowest_rank: that rank's own bytes / its step
+        all_bytes = float(per_rank[:, 0].sum())
+        achieved = all_bytes / (kernel_ms_max * 1e-3) / 1e9
+        peak = HBM_PEAK_GBS * world
+        slow = int(torch.argmax(per_rank[:, 1]))
+        slowest = {"rank": slow, "step_ms_event": float(per_rank[slow, 1]),
+                   "algorithmic_bytes": float(per_rank[slow, 0]),
+                   "frac": float(per_rank[slow, 0]) / (float(per_rank[slow, 1]) * 1e-3) / 1e9 / HBM_PEAK_GBS}
         traffic, traffic_src = None, None
         bid = lib_build_id()
-        if os.path.exists(args.traffic_json) and world == 1:
+        # the stamped profile figures are per-GPU launches of one workload: the C2 strip is the same at every N (weak
+        # scaling); the C4 rank piece shrinks with N, so at N > 1 its N = 1 figures do not describe the timed launches
+        same_launch = world == 1 or not c4
+        wl_key = ("spe10_block_swipdg_q1_%dx%d_8x8_subdomains" % (nx, ny) if c4
+                  else "spe10_swipdg_p1_kuhn_%dx%d" % (nx // world, ny))
+        if os.path.exists(args.traffic_json) and same_launch:
             try:
                 tj = json.load(open(args.traffic_json))
-                wl = ("spe10_block_swipdg_q1_%dx%d_8x8_subdomains" % (nx, ny) if c4
-                      else "spe10_swipdg_p1_kuhn_%dx%d" % (nx, ny))
-                if tj.get("build_id") == bid and wl in tj.get("workloads", {}):
-                    traffic = tj["workloads"][wl]["hbm_bytes_per_launch"]
+                if tj.get("build_id") == bid and wl_key in tj.get("workloads", {}):
+                    traffic = tj["workloads"][wl_key]["hbm_bytes_per_launch"]
                     traffic_src = os.path.relpath(args.traffic_json, ROOT)
             except (OSError, ValueError, KeyError):
                 traffic = None
         rocprof_ms, rocprof_src = None, None
-        if os.path.exists(args.kernel_times_json) and world == 1:
+        if os.path.exists(args.kernel_times_json) and same_launch:
             try:
                 kj = json.load(open(args.kernel_times_json))
                 ent = kj.get("workloads", {}).get("c4" if c4 else "c2", {})
                 if kj.get("build_id") == bid and ent.get("kernel") == kernel_label:
-                    rocprof_ms = ent["avg_ns"] * 1e-6
-                    rocprof_src = os.path.relpath(args.kernel_times_json, ROOT)
+                    # the launches of the bench command's timed window (scripts/kernel_times.py), else the all-launch
+                    # average of an older file
+                    rocprof_ms = ent.get("window_avg_ns", ent["avg_ns"]) * 1e-6
+                    rocprof_src = os.path.relpath(args.kernel_times_json, ROOT) + (
+                        " (timed-window launches %d-%d of the profiled bench command)"
+                        % (ent["window_first_launch"], ent["window_last_launch"]) if "window_avg_ns" in ent else
+                        " (all launches)")
             except (OSError, ValueError, KeyError):
                 rocprof_ms = None
+        if not same_launch:
+            traffic_src = rocprof_src = "n/a: the C4 rank piece at N > 1 is not the profiled N = 1 launch"
         halo_desc = ""
         if world > 1 and args.halo == "once":
             halo_desc = ", face halo exchanged once at setup (static mesh and coefficients)"
@@ -364,12 +387,15 @@ def main():
                         "total_dofs": total_dofs, "components": qp1,
                         "parallelism": "block-swipdg strips x%d, owner-computes%s" % (world, halo_desc)
                         if world > 1 else "single GPU"}),
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
+                         "frac": achieved / peak, "traffic": traffic,
                          # the physical figure: HBM bytes the kernel really moves (PMC, same build) per second,
                          # over the same peak -- below `frac` because the layout reads less than SURVEY 8(d) prices
                          "traffic_frac": (traffic / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if traffic else None,
                          "traffic_gbs": (traffic / (kernel_ms * 1e-3) / 1e9) if traffic else None,
+                         # N > 1: frac = all ranks' bytes / the slowest rank's step / (N x peak); the slowest rank alone
+                         "slowest_rank": slowest if world > 1 else None,
+                         "peak_per_gpu": HBM_PEAK_GBS,
                          "traffic_source": traffic_src, "build_id": bid,
                          # the dominant kernel as the library's dispatch picked it in the last timed step
                          # (hdd_last_tile_kernel, rank 0)
@@ -381,7 +407,10 @@ def main():
                          # the same kernel's average duration from a rocprofv3 --kernel-trace run of this build
                          # (profiles/*/kernel_times.json, build-stamped like the traffic), else null
                          "kernel_ms_rocprof": rocprof_ms, "kernel_ms_rocprof_source": rocprof_src,
+                         # the same roofline over the profiled kernel duration (per GPU: rank 0's bytes)
+                         "frac_rocprof": (alg_bytes / (rocprof_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if rocprof_ms else None,
                          "algorithmic_bytes_per_launch": alg_bytes,
+                         "algorithmic_bytes_all_ranks": all_bytes,
                          # measured on this box in this run: device copy (read + write) and fill (write)
                          "attainable": dict(att, source="torch copy_ / fill_ of 1 GiB, HIP events"),
                          "frac_of_torch_copy": achieved / att["copy_gbs"],
@@ -391,6 +420,9 @@ def main():
             "cpu_baseline": cpu,
         }
         out["config"]["entry"] = "hdd_block_assemble_sharded (C ABI)"
+        # any HDD_* variable of this process (the release library reads none but the tests' HDD_DEBUG_FLAGS error
+        # injection; recorded so that an inherited environment is visible in the line)
+        out["config"]["hdd_env"] = {k: v for k, v in sorted(os.environ.items()) if k.startswith("HDD_")}
         if world > 1:
             out["config"]["comm_init_s_rank0"] = rccl_init_s
             out["config"]["halo"] = args.halo

@@ -25,9 +25,9 @@ struct hdd_ctx {
   // read once at hdd_ctx_create, never per launch
   int n_cu = 256;           // hipDeviceAttributeMultiprocessorCount
   int debug_flags = 0;      // HDD_DEBUG_FLAGS: error injection of the tests; ablation bits (HDD_ABLATION builds only)
-  uint32_t variant = 0;     // HDD_VARIANT / hdd_ctx_set_variant: verification variants (0: the default kernels)
-  int wgcu = 0;             // HDD_P1_WGCU: tiles-per-CU sweep override (0: the policy's measured value)
-  int q3g_reps = 0;         // HDD_Q3G_REPS: workgroups per (XCD, row quad) of the p=3 GEMM kernel (0: by CU count)
+  uint32_t variant = 0;     // hdd_ctx_set_variant (ablation build: also HDD_VARIANT): verification variants (0: default)
+  int wgcu = 0;             // ablation build, HDD_P1_WGCU: tiles-per-CU sweep override (0: the policy's measured value)
+  int q3g_reps = 0;         // ablation build, HDD_Q3G_REPS: workgroups per (XCD, row quad) of the p=3 GEMM kernel
   double* q3g_tab = nullptr;   // p=3 reference matrices [Q3G_K][4096], uploaded on first use
   void* scan_ws = nullptr;     // device-pattern row-length scan scratch (kept: no allocation per build)
   size_t scan_ws_bytes = 0;
@@ -65,6 +65,10 @@ static hipError_t ctx_workspace(hdd_ctx* ctx, size_t bytes, void** out)
 
 using hdd::set_error;
 
+// vertex-indexed geometry is read with 32-bit byte offsets (swipdg_device.hh rsrc32): every [rows][n_local] int32 /
+// f64 row offset and every vertex row (at most 3 n_local vertices of 16 B) must stay below 2^32
+static bool vx_offsets_fit(int64_t n_local) { return n_local >= 0 && n_local * 48 < (int64_t(1) << 32); }
+
 static int hip_fail(hipError_t e, const char* where)
 {
   return set_error(HDD_ERR_HIP, std::string(where) + ": " + hipGetErrorString(e));
@@ -85,9 +89,13 @@ extern "C" int hdd_ctx_create(int hip_device, hdd_ctx** out)
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, hip_device) == hipSuccess && cus > 0)
     c->n_cu = cus;
   if (const char* df = getenv("HDD_DEBUG_FLAGS")) c->debug_flags = atoi(df);
+#ifdef HDD_ABLATION
+  // study knobs: only the ablation build reads them from the environment, so an inherited variable cannot change
+  // which kernel a release build times; the tests select variants with hdd_ctx_set_variant
   if (const char* v = getenv("HDD_VARIANT")) c->variant = uint32_t(strtoul(v, nullptr, 0));
   if (const char* w = getenv("HDD_P1_WGCU")) c->wgcu = std::max(0, atoi(w));
   if (const char* r = getenv("HDD_Q3G_REPS")) c->q3g_reps = std::max(0, atoi(r));
+#endif
   *out = c;
   return HDD_OK;
 }
@@ -333,7 +341,9 @@ static int assemble_impl(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_fn* k
   if (!m->elem_vertices != !m->vertex_coords)
     return set_error(HDD_ERR_INVALID, "hdd_swipdg_assemble: mesh elem_vertices / vertex_coords: both or neither");
   // vertex-indexed geometry (HDD_VARIANT_ELEMENT_MAJOR: the element-major coords, cross-check)
-  if (m->elem_vertices && !(ctx->variant & HDD_VARIANT_ELEMENT_MAJOR)) {
+  // (the P1 vertex-indexed loads use 32-bit byte offsets: meshes beyond n_local * 48 >= 2^32 take the element-major
+  // coords, vx_offsets_fit)
+  if (m->elem_vertices && !(ctx->variant & HDD_VARIANT_ELEMENT_MAJOR) && vx_offsets_fit(m->n_local)) {
     a.ev = m->elem_vertices;
     a.vxy = m->vertex_coords;
   }
@@ -1067,7 +1077,8 @@ extern "C" int hdd_product_assemble(hdd_ctx* ctx, const hdd_mesh* m, int32_t pro
     f.wgcu = ctx->wgcu;
     if (!m->elem_vertices != !m->vertex_coords)
       return set_error(HDD_ERR_INVALID, "hdd_product_assemble: mesh elem_vertices / vertex_coords: both or neither");
-    if (m->elem_vertices && m->elem_type == HDD_SIMPLEX && !(ctx->variant & HDD_VARIANT_ELEMENT_MAJOR)) {
+    if (m->elem_vertices && m->elem_type == HDD_SIMPLEX && !(ctx->variant & HDD_VARIANT_ELEMENT_MAJOR) &&
+        vx_offsets_fit(m->n_local)) {
       f.ev = m->elem_vertices;   // vertex-indexed geometry, as hdd_swipdg_assemble
       f.vxy = m->vertex_coords;
     }

@@ -986,8 +986,12 @@ static hipError_t launch_hex_q3(const HexArgs& a, hipStream_t s)
 
 static bool hex_generic_forced()
 {
+#ifdef HDD_ABLATION
   static const bool generic = getenv("HDD_HEX_GENERIC") != nullptr;   // A/B against the LDS-table kernel
   return generic;
+#else
+  return false;   // (release builds read no kernel choice from the environment)
+#endif
 }
 
 bool hex_uses_records(const HexArgs& a, int degree, int nq1v, int nq1f)

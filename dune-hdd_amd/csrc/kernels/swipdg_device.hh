@@ -687,21 +687,87 @@ __device__ __forceinline__ double kappa_k(const AssembleArgs& a, int64_t e)
   else return a.kappa[0].c;
 }
 
+// ------------------------------------------------------------------------------------------------
+// 32-bit offset loads (vertex-indexed P1 meshes).  Each SoA array is read through a buffer resource made from its
+// base pointer (wave-uniform SGPRs, hoisted out of the tile loop), the row of a [rows][n_local] array in the
+// instruction's SGPR soffset and the element part in a 32-bit VGPR offset: no 64-bit VALU address arithmetic (the
+// global loads cost a v_lshl_add_u64 each, the neighbours' vertex-id gathers a 64-bit multiply-add; round 5 counted
+// 461 integer / select instructions beside 359 f64 ones in the C2 kernel).  The host enables vertex-indexed
+// geometry only while every byte offset fits in 32 bits (n_local * 48 < 2^32, hdd_swipdg_assemble); the resources
+// carry no range (num_records = 2^32 - 1).
+// ------------------------------------------------------------------------------------------------
+typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc32(const void* p)
+{
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, -1, 0x00020000);
+}
+__device__ __forceinline__ uint32_t ld32(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff = 0)
+{
+  return __builtin_amdgcn_raw_buffer_load_b32(r, int(voff), int(soff), 0);
+}
+__device__ __forceinline__ double ld64f(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff = 0)
+{
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, int(voff), int(soff), 0));
+}
+__device__ __forceinline__ dvec2 ld128f(__amdgpu_buffer_rsrc_t r, uint32_t voff)
+{
+  return __builtin_bit_cast(dvec2, __builtin_amdgcn_raw_buffer_load_b128(r, int(voff), 0, 0));
+}
+// the tensor / kappa of local element e (byte offset e8 = 8 e)
+template <int TK>
+__device__ __forceinline__ Tensor tensor_o32(const AssembleArgs& a, uint32_t e8)
+{
+  Tensor t;
+  if constexpr (TK == HDD_TENSOR_ISO_PER_ELEM) {
+    const double v = ld64f(rsrc32(a.tper), e8);
+    t.a00 = v; t.a01 = 0.0; t.a11 = v;
+  } else if constexpr (TK == HDD_TENSOR_SYM_PER_ELEM) {
+    const __amdgpu_buffer_rsrc_t r = rsrc32(a.tper);
+    const uint32_t row = uint32_t(a.n_local) * 8u;
+    t.a00 = ld64f(r, e8); t.a01 = ld64f(r, e8, row); t.a11 = ld64f(r, e8, 2u * row);
+  } else {
+    t.a00 = a.tc0; t.a01 = a.tc1; t.a11 = a.tc2;
+  }
+  return t;
+}
+template <int KK>
+__device__ __forceinline__ double kappa_o32(const AssembleArgs& a, uint32_t e8)
+{
+  if constexpr (KK == HDD_FN_PER_ELEM) return ld64f(rsrc32(a.kappa[0].per_elem), e8);
+  else return a.kappa[0].c;
+}
+__device__ __forceinline__ void vertex_xy_o32(const AssembleArgs& a, int32_t v, double& x, double& y)
+{
+  const dvec2 p = ld128f(rsrc32(a.vxy), uint32_t(v) * 16u);
+  x = p.x;
+  y = p.y;
+}
+
 // Own-data loads of a tile (coalesced SoA).  VX: vertex ids instead of coordinates -- the vertex
 // coordinates are then gathered with the neighbour data (p1_load_gat), the neighbour's off-face vertex in a
-// second stage (p1_load_gat2) that the persistent driver issues after the tile's stores.
+// second stage (p1_load_gat2) that the persistent driver issues after the tile's stores.  VX reads go through the
+// 32-bit offset loads above.
 template <int TK, int KK, bool VX = false>
 __device__ __forceinline__ void p1_load_own(const AssembleArgs& a, int64_t e, P1Own& o)
 {
   const int64_t ne = a.n_local;
+  if constexpr (VX) {
+    const uint32_t e4 = uint32_t(e) * 4u, row = uint32_t(ne) * 4u;
+    const __amdgpu_buffer_rsrc_t rv = rsrc32(a.ev), rn = rsrc32(a.nbrs);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) o.vid[k] = int32_t(ld32(rv, e4, uint32_t(k) * row));
+#pragma unroll
+    for (int f = 0; f < 3; ++f) o.nbr[f] = int32_t(ld32(rn, e4, uint32_t(f) * row));
+    o.finfo = ld32(rsrc32(a.finfo), e4);
+    o.A = tensor_o32<TK>(a, 2u * e4);
+    o.ke = kappa_o32<KK>(a, 2u * e4);
+    return;
+  }
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
-    if constexpr (VX) {
-      o.vid[k] = a.ev[k * ne + e];
-    } else {
-      o.X[k] = a.coords[(2 * k) * ne + e];
-      o.Y[k] = a.coords[(2 * k + 1) * ne + e];
-    }
+    o.X[k] = a.coords[(2 * k) * ne + e];
+    o.Y[k] = a.coords[(2 * k + 1) * ne + e];
   }
 #pragma unroll
   for (int f = 0; f < 3; ++f) o.nbr[f] = a.nbrs[f * ne + e];
@@ -716,7 +782,20 @@ __device__ __forceinline__ void p1_load_gat(const AssembleArgs& a, int64_t e, P1
   const int64_t ne = a.n_local;
   if constexpr (VX) {
 #pragma unroll
-    for (int k = 0; k < 3; ++k) vertex_xy(a, o.vid[k], o.X[k], o.Y[k]);
+    for (int k = 0; k < 3; ++k) vertex_xy_o32(a, o.vid[k], o.X[k], o.Y[k]);
+    const uint32_t row = uint32_t(ne) * 4u;
+    const __amdgpu_buffer_rsrc_t rv = rsrc32(a.ev);
+#pragma unroll
+    for (int f = 0; f < 3; ++f) {
+      const uint32_t n = o.nbr[f] >= 0 ? uint32_t(o.nbr[f]) : uint32_t(e);   // boundary faces: harmless own reload
+      // the neighbour's vertex opposite its twin face tw (Simplex faces (0,1), (0,2), (1,2)): 2 - tw (clamped, so
+      // whatever a boundary face's info bits hold the offset stays inside the array)
+      const uint32_t to = min(2u - ((o.finfo >> (4 * f)) & 7u), 2u);
+      g.ov[f] = int32_t(ld32(rv, to * row + 4u * n));
+      g.Ap[f] = tensor_o32<TK>(a, 8u * n);
+      g.kn[f] = kappa_o32<KK>(a, 8u * n);
+    }
+    return;
   }
 #pragma unroll
   for (int f = 0; f < 3; ++f) {
@@ -724,12 +803,8 @@ __device__ __forceinline__ void p1_load_gat(const AssembleArgs& a, int64_t e, P1
     const uint32_t inf = (o.finfo >> (4 * f)) & 15u;
     const int tw = int(inf & 7u);
     const int to = 3 - Simplex::fv(tw, 0) - Simplex::fv(tw, 1);
-    if constexpr (VX) {
-      g.ov[f] = a.ev[to * ne + n];
-    } else {
-      g.Ox[f] = a.coords[(2 * to) * ne + n];
-      g.Oy[f] = a.coords[(2 * to + 1) * ne + n];
-    }
+    g.Ox[f] = a.coords[(2 * to) * ne + n];
+    g.Oy[f] = a.coords[(2 * to + 1) * ne + n];
     g.Ap[f] = tensor_k<TK>(a, n);
     g.kn[f] = kappa_k<KK>(a, n);
   }
@@ -739,7 +814,7 @@ __device__ __forceinline__ void p1_load_gat2(const AssembleArgs& a, P1Gat& g)
 {
   if constexpr (VX) {
 #pragma unroll
-    for (int f = 0; f < 3; ++f) vertex_xy(a, g.ov[f], g.Ox[f], g.Oy[f]);
+    for (int f = 0; f < 3; ++f) vertex_xy_o32(a, g.ov[f], g.Ox[f], g.Oy[f]);
   }
 }
 
@@ -761,7 +836,9 @@ __device__ __forceinline__ void p1_face_self(double (&S)[3][3], const double (&A
     }
 }
 
-template <bool PEN = false>
+// ALLIN: the caller guarantees three interior faces (every element of a full interior tile, see the persistent
+// driver): no per-face branches, the row length and block count compile-time constants
+template <bool PEN = false, bool ALLIN = false>
 __device__ __forceinline__ void p1_compute(const AssembleArgs& a, int64_t e, const P1Own& o, const P1Gat& gt,
                                            double* img)
 {
@@ -782,20 +859,21 @@ __device__ __forceinline__ void p1_compute(const AssembleArgs& a, int64_t e, con
   }
   const double adet = fabs(det);
   const double osgn = det > 0.0 ? 1.0 : -1.0;
+  const int32_t ei = int32_t(e);   // local ids are int32 (hdd_mesh neighbors): 32-bit compares
   int nblk = 1, pos_self = 0, pos[3];
 #pragma unroll
   for (int f = 0; f < 3; ++f) {
-    nblk += o.nbr[f] >= 0;
-    pos_self += (o.nbr[f] >= 0 && o.nbr[f] < e);
+    nblk += ALLIN || o.nbr[f] >= 0;
+    pos_self += ((ALLIN || o.nbr[f] >= 0) && o.nbr[f] < ei);
   }
 #pragma unroll
   for (int f = 0; f < 3; ++f) {
-    int p = (e < o.nbr[f]) ? 1 : 0;
+    int p = (ei < o.nbr[f]) ? 1 : 0;
 #pragma unroll
-    for (int q = 0; q < 3; ++q) p += (o.nbr[q] >= 0 && o.nbr[q] < o.nbr[f]);
+    for (int q = 0; q < 3; ++q) p += ((ALLIN || o.nbr[q] >= 0) && o.nbr[q] < o.nbr[f]);
     pos[f] = p;
   }
-  const int rowlen = nblk * 3;
+  const int rowlen = ALLIN ? 12 : nblk * 3;
   const double ke = o.ke;
   double S[3][3];
   {
@@ -809,7 +887,7 @@ __device__ __forceinline__ void p1_compute(const AssembleArgs& a, int64_t e, con
 #pragma unroll
   for (int f = 0; f < 3; ++f) {
     const int32_t n = o.nbr[f];
-    if (n <= HDD_NBR_NEUMANN) continue;
+    if (!ALLIN && n <= HDD_NBR_NEUMANN) continue;
     const int fa = E::fv(f, 0), fb = E::fv(f, 1), fc = 3 - fa - fb;
     const double tx = o.X[fb] - o.X[fa], ty = o.Y[fb] - o.Y[fa];
     const double il = rsq_nr(tx * tx + ty * ty);
@@ -822,7 +900,7 @@ __device__ __forceinline__ void p1_compute(const AssembleArgs& a, int64_t e, con
     const double dm = agn(o.A, nx, ny, nx, ny);
     const double ihp = a.beta == 1.0 ? il : inv_pow(len, a.beta);
     const double half = 0.5 * len, third = len * (1.0 / 3.0), sixth = len * (1.0 / 6.0);
-    if (n >= 0) {
+    if (ALLIN || n >= 0) {
       const uint32_t inf = (o.finfo >> (4 * f)) & 15u;
       const int tw = int(inf & 7u);
       const bool rev = (inf & 8u) != 0u;
@@ -1354,6 +1432,13 @@ struct P1PwcPolicy {
   {
     p1_compute<PEN>(a, e, o, g, img);
   }
+  // full interior tiles (64 elements, three interior faces each: tile length 64 RB): branch-free faces, the image
+  // layout static (lane l's row block at l RB)
+  static constexpr bool FULLTILE = true;
+  __device__ static void compute_full(const AssembleArgs& a, int64_t e, const Own& o, const Gat& g, double* img)
+  {
+    p1_compute<PEN, true>(a, e, o, g, img);
+  }
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -1421,10 +1506,24 @@ struct P1SmoothPolicy {
   }
 
   // the entries from the volume moment kv = sum_q w_q kappa(x_q) and kappa at the face Gauss points,
-  // KF(f, x, y, q) (point q of face f at (x, y), from vertex a to b)
-  template <class KFace>
+  // KF(f, x, y, q) (point q of face f at (x, y), from vertex a to b); ALLIN: three interior faces (full tiles of the
+  // persistent driver, as p1_compute)
+  template <bool ALLIN = false, class KFace>
   __device__ static void emit(const AssembleArgs& a, int64_t e, const Own& o, const Gat& gt, double* img, double kv,
                               KFace KF)
+  {
+    double* imgs[1] = {img};
+    const double kvs[1] = {kv};
+    emitN<1, ALLIN>(a, e, o, gt, imgs, kvs, [&](int, int f, double x, double y, int q) { return KF(f, x, y, q); });
+  }
+
+  // NC components at once (the fused C3 policy): the geometry -- Jacobian, gradients, face normals and lengths, the
+  // neighbour's gradients, the harmonic weights -- is evaluated once and each component's entries (its own kappa
+  // moments) written into its image img[c]; per component the arithmetic is exactly that of emit (NC = 1).
+  // KF(c, f, x, y, q): component c's kappa at point q of face f.
+  template <int NC, bool ALLIN = false, class KFace>
+  __device__ static void emitN(const AssembleArgs& a, int64_t e, const Own& o, const Gat& gt, double* const (&img)[NC],
+                               const double (&kv)[NC], KFace KF)
   {
     using E = Simplex;
     const double j00 = o.X[1] - o.X[0], j01 = o.X[2] - o.X[0], j10 = o.Y[1] - o.Y[0], j11 = o.Y[2] - o.Y[0];
@@ -1443,32 +1542,36 @@ struct P1SmoothPolicy {
     }
     const double adet = fabs(det);
     const double osgn = det > 0.0 ? 1.0 : -1.0;
+    const int32_t ei = int32_t(e);   // 32-bit compares (local ids are int32)
     int nblk = 1, pos_self = 0, pos[3];
 #pragma unroll
     for (int f = 0; f < 3; ++f) {
-      nblk += o.nbr[f] >= 0;
-      pos_self += (o.nbr[f] >= 0 && o.nbr[f] < e);
+      nblk += ALLIN || o.nbr[f] >= 0;
+      pos_self += ((ALLIN || o.nbr[f] >= 0) && o.nbr[f] < ei);
     }
 #pragma unroll
     for (int f = 0; f < 3; ++f) {
-      int p = (e < o.nbr[f]) ? 1 : 0;
+      int p = (ei < o.nbr[f]) ? 1 : 0;
 #pragma unroll
-      for (int q = 0; q < 3; ++q) p += (o.nbr[q] >= 0 && o.nbr[q] < o.nbr[f]);
+      for (int q = 0; q < 3; ++q) p += ((ALLIN || o.nbr[q] >= 0) && o.nbr[q] < o.nbr[f]);
       pos[f] = p;
     }
-    const int rowlen = nblk * 3;
+    const int rowlen = ALLIN ? 12 : nblk * 3;
     // the own block is symmetric (volume g_i.A g_j, face terms symmetric in i, j): its upper triangle, mirrored at
     // the end
-    double S[3][3];
-    const double vol = adet * kv;
+    double S[NC][3][3];
 #pragma unroll
-    for (int i = 0; i < 3; ++i)
+    for (int c = 0; c < NC; ++c) {
+      const double vol = adet * kv[c];
 #pragma unroll
-      for (int j = i; j < 3; ++j) S[i][j] = vol * (Ag[j][0] * g[i][0] + Ag[j][1] * g[i][1]);
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = i; j < 3; ++j) S[c][i][j] = vol * (Ag[j][0] * g[i][0] + Ag[j][1] * g[i][1]);
+    }
 #pragma unroll
     for (int f = 0; f < 3; ++f) {
       const int32_t n = o.nbr[f];
-      if (n <= HDD_NBR_NEUMANN) continue;
+      if (!ALLIN && n <= HDD_NBR_NEUMANN) continue;
       const int fa = E::fv(f, 0), fb = E::fv(f, 1), fc = 3 - fa - fb;
       const double Ax = o.X[fa], Ay = o.Y[fa], Bx = o.X[fb], By = o.Y[fb];
       const double tx = Bx - Ax, ty = By - Ay;
@@ -1481,23 +1584,27 @@ struct P1SmoothPolicy {
       for (int k = 0; k < 3; ++k) Ae[k] = Ag[k][0] * nx + Ag[k][1] * ny;
       const double dm = agn(o.A, nx, ny, nx, ny);
       const double ihp = a.beta == 1.0 ? il : inv_pow(len, a.beta);
-      const bool inner = n >= 0;
-      // moments over the face's Gauss 3 points (s from vertex a to vertex b)
-      double k1a = 0.0, k1b = 0.0, qaa = 0.0, qab = 0.0, qbb = 0.0;
+      const bool inner = ALLIN || n >= 0;
+      // moments over the face's Gauss 3 points (s from vertex a to vertex b), per component
+      double k1a[NC], k1b[NC], qaa[NC], qab[NC], qbb[NC];
 #pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        const double sq = Gauss01<3>::s(q), wq = Gauss01<3>::w(q) * len;
-        const double k = KF(f, Ax + sq * tx, Ay + sq * ty, q);
-        const double kk = inner ? k * k : k;
-        k1a += wq * k * (1.0 - sq);
-        k1b += wq * k * sq;
-        qaa += wq * kk * (1.0 - sq) * (1.0 - sq);
-        qab += wq * kk * sq * (1.0 - sq);
-        qbb += wq * kk * sq * sq;
+      for (int c = 0; c < NC; ++c) {
+        k1a[c] = k1b[c] = qaa[c] = qab[c] = qbb[c] = 0.0;
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          const double sq = Gauss01<3>::s(q), wq = Gauss01<3>::w(q) * len;
+          const double k = KF(c, f, Ax + sq * tx, Ay + sq * ty, q);
+          const double kk = inner ? k * k : k;
+          k1a[c] += wq * k * (1.0 - sq);
+          k1b[c] += wq * k * sq;
+          qaa[c] += wq * kk * (1.0 - sq) * (1.0 - sq);
+          qab[c] += wq * kk * sq * (1.0 - sq);
+          qbb[c] += wq * kk * sq * sq;
+        }
       }
-      auto M1 = [&](int i) { return i == fa ? k1a : (i == fb ? k1b : 0.0); };
-      auto MM = [&](int i, int j) {
-        return (i == fc || j == fc) ? 0.0 : (i != j ? qab : (i == fa ? qaa : qbb));
+      auto M1 = [&](int c, int i) { return i == fa ? k1a[c] : (i == fb ? k1b[c] : 0.0); };
+      auto MM = [&](int c, int i, int j) {
+        return (i == fc || j == fc) ? 0.0 : (i != j ? qab[c] : (i == fa ? qaa[c] : qbb[c]));
       };
       if (inner) {
         const uint32_t inf = (o.finfo >> (4 * f)) & 15u;
@@ -1519,31 +1626,39 @@ struct P1SmoothPolicy {
         const int jA = rev ? tb : ta, jB = rev ? ta : tb;
         // per-face products once: each entry a two-FMA chain
         const double wA = -w_plus * AnA, wB = -w_plus * AnB, wO = -w_plus * AnO;
-        const double wka = w_minus * k1a, wkb = w_minus * k1b;
 #pragma unroll
-        for (int i = 0; i < 3; ++i) {
-          double* row = img + i * rowlen + pos[f] * 3;
-          const double m1i = M1(i);
-          row[jA] = fma(wA, m1i, fma(Ae[i], wka, -pc * MM(i, fa)));
-          row[jB] = fma(wB, m1i, fma(Ae[i], wkb, -pc * MM(i, fb)));
-          row[to] = wO * m1i;
+        for (int c = 0; c < NC; ++c) {
+          const double wka = w_minus * k1a[c], wkb = w_minus * k1b[c];
+#pragma unroll
+          for (int i = 0; i < 3; ++i) {
+            double* row = img[c] + i * rowlen + pos[f] * 3;
+            const double m1i = M1(c, i);
+            row[jA] = fma(wA, m1i, fma(Ae[i], wka, -pc * MM(c, i, fa)));
+            row[jB] = fma(wB, m1i, fma(Ae[i], wkb, -pc * MM(c, i, fb)));
+            row[to] = wO * m1i;
+          }
+#pragma unroll
+          for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int j = i; j < 3; ++j)
+              S[c][i][j] += -w_minus * (Ae[j] * M1(c, i) + Ae[i] * M1(c, j)) + pc * MM(c, i, j);
         }
-#pragma unroll
-        for (int i = 0; i < 3; ++i)
-#pragma unroll
-          for (int j = i; j < 3; ++j) S[i][j] += -w_minus * (Ae[j] * M1(i) + Ae[i] * M1(j)) + pc * MM(i, j);
       } else {   // Dirichlet: SWIPDG::BoundaryLHS, penalty sigma_b kappa (n.An) / |F|^beta
         const double pc = (a.sigma_boundary * dm) * ihp;
 #pragma unroll
-        for (int i = 0; i < 3; ++i)
+        for (int c = 0; c < NC; ++c)
 #pragma unroll
-          for (int j = i; j < 3; ++j) S[i][j] += -(Ae[j] * M1(i) + Ae[i] * M1(j)) + pc * MM(i, j);
+          for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int j = i; j < 3; ++j) S[c][i][j] += -(Ae[j] * M1(c, i) + Ae[i] * M1(c, j)) + pc * MM(c, i, j);
       }
     }
 #pragma unroll
-    for (int i = 0; i < 3; ++i)
+    for (int c = 0; c < NC; ++c)
 #pragma unroll
-      for (int j = 0; j < 3; ++j) img[i * rowlen + pos_self * 3 + j] = j >= i ? S[i][j] : S[j][i];
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) img[c][i * rowlen + pos_self * 3 + j] = j >= i ? S[c][i][j] : S[c][j][i];
   }
 };
 
@@ -1554,12 +1669,14 @@ struct P1SmoothPolicy {
 // driver builds each component's LDS image and streams it to that component's value array.  The mesh and
 // the gathers are read once instead of once per component.  Entries equal the per-component kernel's up to
 // rounding (kappa's volume sum is a_c sum w + b_c sum w sin instead of sum w (a_c + b_c sin)).
-template <int TK, bool VX = false>
+// TWO: exactly two components (C3), emitted in one pass over the geometry into two LDS images (emit_two)
+template <int TK, bool VX = false, bool TWO_ = false>
 struct P1SmoothFusedPolicy : P1SmoothPolicy<TK, VX> {
   using Base = P1SmoothPolicy<TK, VX>;
   using Own = typename Base::Own;
   using Gat = typename Base::Gat;
   static constexpr bool FUSED = true;
+  static constexpr bool TWO = TWO_;
   // one wave per SIMD with the whole register file: at two (<= 256 registers) the shared sines, the tile's
   // records and the next tile's in-flight data spill (160-400 B of scratch per lane)
   static constexpr int WGCU = 4, MINW = 1;
@@ -1615,13 +1732,30 @@ struct P1SmoothFusedPolicy : P1SmoothPolicy<TK, VX> {
       }
     }
   }
+  template <bool ALLIN = false>
   __device__ static void emit_component(const AssembleArgs& a, int c, int64_t e, const Own& o, const Gat& gt,
                                         const Shared& sh, double* img)
   {
     const KappaArg& K = a.kappa[c];
-    Base::emit(a, e, o, gt, img, K.c * wv() + K.b * sh.sv,
-               [&](int f, double, double, int q) { return K.c + K.b * sh.sf[f][q]; });
+    Base::template emit<ALLIN>(a, e, o, gt, img, K.c * wv() + K.b * sh.sv,
+                               [&](int f, double, double, int q) { return K.c + K.b * sh.sf[f][q]; });
   }
+  // both components of a two-component call in one pass over the geometry (the C3 case: OS2014's affine part and
+  // its mu-component), into the images img0 / img1
+  template <bool ALLIN = false>
+  __device__ static void emit_two(const AssembleArgs& a, int64_t e, const Own& o, const Gat& gt, const Shared& sh,
+                                  double* img0, double* img1)
+  {
+    const KappaArg& K0 = a.kappa[0];
+    const KappaArg& K1 = a.kappa[1];
+    double* const imgs[2] = {img0, img1};
+    const double kvs[2] = {K0.c * wv() + K0.b * sh.sv, K1.c * wv() + K1.b * sh.sv};
+    Base::template emitN<2, ALLIN>(a, e, o, gt, imgs, kvs, [&](int c, int f, double, double, int q) {
+      return c == 0 ? K0.c + K0.b * sh.sf[f][q] : K1.c + K1.b * sh.sf[f][q];
+    });
+  }
+  // full interior tiles: branch-free faces (see P1PwcPolicy::compute_full)
+  static constexpr bool FULLTILE = true;
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -1797,6 +1931,16 @@ template <class P>
 struct half_of<P, std::void_t<decltype(P::HALF)>> : std::bool_constant<P::HALF> {};
 template <class P>
 constexpr int image_blocks() { return half_of<P>::value ? 32 : 64; }
+// TWO policies (P1SmoothFusedPolicy<.., true>) emit two components per tile into two images (the LDS holds both)
+template <class P, class = void>
+struct two_of : std::false_type {};
+template <class P>
+struct two_of<P, std::void_t<decltype(P::TWO)>> : std::bool_constant<P::TWO> {};
+// FULLTILE policies (P1PwcPolicy) have a compute_full for tiles of 64 elements with every face interior
+template <class P, class = void>
+struct fulltile_of : std::false_type {};
+template <class P>
+struct fulltile_of<P, std::void_t<decltype(P::FULLTILE)>> : std::bool_constant<P::FULLTILE> {};
 template <class P, class = void>
 struct emit_of : std::false_type {};
 template <class P>
@@ -1813,6 +1957,8 @@ swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
   constexpr int RB = P::RB;
   constexpr int IMG = image_blocks<P>() * RB;
   constexpr int STORES = (IMG / 2 + 63) / 64;
+  constexpr bool TWO = two_of<P>::value;
+  constexpr int IMGS = IMG + 2 + RB;   // TWO: doubles per image (+ the alignment slot and the tail lanes' scratch row)
   static_assert(!HALF || (P::PAD && !FUSED && RB == 80), "half images: the Q1 closed-form policy");
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const int lane = threadIdx.x;
@@ -1909,8 +2055,13 @@ swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
     const int64_t t0 = a.own_begin + tile * 64;
     const bool active = t0 + lane < a.own_end;
     const int64_t base_al = base & ~int64_t(1);
-    const int off = tile_offset<P::NB>(P::n_interior(own), active) + int(base - base_al);
     const int tlen = int(tile_end - base);
+    // FULLTILE policies: a tile of 64 elements whose row blocks all have the maximum length (every face interior) --
+    // the bulk of a mesh -- has a static image layout (lane l at l RB) and takes the branch-free compute_full
+    const bool fullt = fulltile_of<P>::value && tlen == 64 * RB;   // wave-uniform
+    int off;
+    if (fullt) off = lane * RB + int(base - base_al);
+    else off = tile_offset<P::NB>(P::n_interior(own), active) + int(base - base_al);
     // sharded step (a.skip_ghost): the row blocks of elements with a ghost face neighbour are written by the
     // element pass on the transfer stream, concurrently -- this tile must not store them (wave-uniform mask)
     uint64_t gmask = 0;
@@ -2134,9 +2285,29 @@ swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
       if (!HDD_ABL(a, 1)) P::compute(a, e, own, gat, img);
     } else {
       double* img = active ? lds + off : scratch;
-      if constexpr (FUSED) {   // the shared part once, then component 0 (the others after its stores)
+      if constexpr (TWO) {   // the shared part once, then both components into their images
         P::prepare(a, own, shv);
-        if (!HDD_ABL(a, 1)) P::emit_component(a, 0, e, own, gat, shv, img);
+        if (HDD_ABL(a, 1)) {
+        } else if (fullt) {
+          P::template emit_two<true>(a, e, own, gat, shv, lds + off, lds + IMGS + off);
+        } else {
+          P::emit_two(a, e, own, gat, shv, img, img + IMGS);
+        }
+      } else if constexpr (FUSED) {   // the shared part once, then component 0 (the others after its stores)
+        P::prepare(a, own, shv);
+        if (HDD_ABL(a, 1)) {
+        } else if (fullt) {
+          P::template emit_component<true>(a, 0, e, own, gat, shv, lds + off);
+        } else {
+          P::emit_component(a, 0, e, own, gat, shv, img);
+        }
+      } else if constexpr (fulltile_of<P>::value) {
+        if (HDD_ABL(a, 1)) {
+        } else if (fullt) {
+          P::compute_full(a, e, own, gat, lds + off);
+        } else {
+          P::compute(a, e, own, gat, img);
+        }
       } else {
         if (!HDD_ABL(a, 1)) P::compute(a, e, own, gat, img);
       }
@@ -2145,6 +2316,7 @@ swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
+    double* img_base = lds;   // the image the non-PAD store paths read (TWO: lds + IMGS for component 1)
     const int64_t start = (base + 1) & ~int64_t(1);
     const int64_t stop = tile_end & ~int64_t(1);
     const int nbytes = stop > start && !HDD_ABL(a, 2) ? int(stop - start) * 8 : 0;
@@ -2201,13 +2373,13 @@ swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
           return r;
         };
         const int a0 = int(start - base_al);   // image position of the first chunk
-        if (!skipped(int(base - base_al))) out[base] = lds[base - base_al];
-        if (!skipped(int(tile_end - 1 - base_al))) out[tile_end - 1] = lds[tile_end - 1 - base_al];
+        if (!skipped(int(base - base_al))) out[base] = img_base[base - base_al];
+        if (!skipped(int(tile_end - 1 - base_al))) out[tile_end - 1] = img_base[tile_end - 1 - base_al];
 #pragma unroll
         for (int k = 0; k < STORES; ++k) {
           const int idx = 2 * (lane + 64 * k);
           const int li = idx < IMG ? idx : 0;
-          const dvec2 v = *reinterpret_cast<const dvec2*>(lds + a0 + li);
+          const dvec2 v = *reinterpret_cast<const dvec2*>(img_base + a0 + li);
           // (even blocks, Q1: a chunk's two doubles always share an element)
           const bool s0 = skipped(a0 + li), s1 = (P::NB * P::NB) % 2 == 1 ? skipped(a0 + li + 1) : s0;
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ivec4, v), rsrc, s0 || s1 ? nbytes : idx * 8, 0, 2);
@@ -2266,12 +2438,12 @@ swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
         }
       } else {
         if (!front) {
-          const double head = lds[base - base_al];
-          const double tail = lds[tile_end - 1 - base_al];
+          const double head = img_base[base - base_al];
+          const double tail = img_base[tile_end - 1 - base_al];
           out[base] = head;
           out[tile_end - 1] = tail;
         }
-        const double* src = lds + (start - base_al);
+        const double* src = img_base + (start - base_al);
 #pragma unroll
         for (int k = 0; k < STORES; ++k) {
           if ((k < ksplit) != front) continue;
@@ -2285,10 +2457,22 @@ swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
     if (ksplit > 0) stores(true);
     if (!HDD_ABL(a, 4)) P::load_gat(a, en, own_n, gat_n);
     stores(false);
-    if constexpr (FUSED) {   // the other components: same image slots, their own value arrays
+    if constexpr (TWO) {   // component 1 from the second image
+      img_base = lds + IMGS;
+      out = a.vals[1];
+      rsrc = __builtin_amdgcn_make_buffer_rsrc(out + start, (short)0, nbytes, 0x00020000);
+      stores(false);
+      img_base = lds;
+      out = a.vals[0];
+    } else if constexpr (FUSED) {   // the other components: same image slots, their own value arrays
       for (int c = 1; c < a.n_comp; ++c) {
         double* img = active ? lds + off : scratch;
-        if (!HDD_ABL(a, 1)) P::emit_component(a, c, e, own, gat, shv, img);
+        if (HDD_ABL(a, 1)) {
+        } else if (fullt) {
+          P::template emit_component<true>(a, c, e, own, gat, shv, lds + off);
+        } else {
+          P::emit_component(a, c, e, own, gat, shv, img);
+        }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -2445,7 +2629,9 @@ static hipError_t launch_persistent(const AssembleArgs& a, hipStream_t s)
   if (n_own <= 0) return hipSuccess;
   const int64_t tiles = a.tile_list ? a.n_tile_list : (n_own + 63) / 64;
   if (tiles <= 0) return hipSuccess;
-  const size_t lds = (P::PAD ? size_t(image_blocks<P>()) * P::RB : size_t(64) * P::RB + 2 + P::RB) * sizeof(double);
+  const size_t lds = (P::PAD ? size_t(image_blocks<P>()) * P::RB : size_t(64) * P::RB + 2 + P::RB) * sizeof(double) *
+                     (two_of<P>::value ? 2 : 1);
+  if (two_of<P>::value && a.n_comp != 2) return hipErrorInvalidValue;
   const int cus = a.n_cu;
   // tiles per CU measured per policy (profiles/r01/sweep_wg_per_cu.log, profiles/r01/s2/); a.wgcu > 0 is the
   // HDD_P1_WGCU sweep override, read once per context

@@ -29,9 +29,17 @@ static hipError_t dispatch_smooth_p1(const AssembleArgs& a, hipStream_t s)
 
 hipError_t launch_p1_pwc(const AssembleArgs& a, hipStream_t s) { return dispatch_kinds<P1Pwc>(a, s, false); }
 hipError_t launch_p1_smooth(const AssembleArgs& a, hipStream_t s) { return dispatch_smooth_p1(a, s); }
+// two components (OS2014, C3): both emitted in one pass over the geometry (P1SmoothFusedPolicy<.., TWO>); tile lists
+// and the sharded SKIP launch included.  More components: one image, emitted one after the other.
 hipError_t launch_p1_smooth_fused(const AssembleArgs& a, hipStream_t s)
 {
   const int tk = a.tkind;
+  if (a.n_comp == 2) {
+    if (tk == HDD_TENSOR_CONST) return launch_persistent<P1SmoothFusedPolicy<HDD_TENSOR_CONST, true, true>>(a, s);
+    if (tk == HDD_TENSOR_ISO_PER_ELEM)
+      return launch_persistent<P1SmoothFusedPolicy<HDD_TENSOR_ISO_PER_ELEM, true, true>>(a, s);
+    return launch_persistent<P1SmoothFusedPolicy<HDD_TENSOR_SYM_PER_ELEM, true, true>>(a, s);
+  }
   if (tk == HDD_TENSOR_CONST) return launch_persistent<P1SmoothFusedPolicy<HDD_TENSOR_CONST, true>>(a, s);
   if (tk == HDD_TENSOR_ISO_PER_ELEM) return launch_persistent<P1SmoothFusedPolicy<HDD_TENSOR_ISO_PER_ELEM, true>>(a, s);
   return launch_persistent<P1SmoothFusedPolicy<HDD_TENSOR_SYM_PER_ELEM, true>>(a, s);

@@ -23,7 +23,8 @@ PRODUCT_L2, PRODUCT_H1_SEMI, PRODUCT_ELLIPTIC, PRODUCT_BOUNDARY_L2, PRODUCT_PENA
 TENSOR_CONST, TENSOR_ISO_PER_ELEM, TENSOR_SYM_PER_ELEM = 0, 1, 2
 BOUNDARY_ALL_DIRICHLET, BOUNDARY_ALL_NEUMANN = 0, 1
 MAX_COMP = 8
-# verification variants (hdd.h HDD_VARIANT_*; Context.set_variant or the HDD_VARIANT environment value)
+# verification variants (hdd.h HDD_VARIANT_*; Context.set_variant; the HDD_VARIANT environment value only in the
+# ablation build)
 VARIANT_Q1_WHOLE_TILE, VARIANT_ELEMENT_MAJOR, VARIANT_C3_PER_COMPONENT, VARIANT_WAVE_PER_ROW = 1, 2, 4, 8
 VARIANT_P1_SMOOTH_QUADRATURE, VARIANT_HEX_Q3_REGISTER, VARIANT_PATTERN_SCAN_COPY = 16, 32, 64
 VARIANT_RHS_FUSED, VARIANT_RHS_GENERIC, VARIANT_RHS_NO_TINY = 128, 256, 512

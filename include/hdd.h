@@ -80,8 +80,8 @@ void hdd_ctx_destroy(hdd_ctx* ctx);
  * build (make ablation: lib_ab/libhdd_abl.so); the product library ignores every other bit. */
 int hdd_ctx_set_debug_flags(hdd_ctx* ctx, int32_t flags);
 /* Verification variants (ABI 8): alternative implementations of the same values, selected per context (or by the
- * HDD_VARIANT value a context reads at creation) so that the tests can compare them bit for bit / to rounding
- * with the default kernels.  Default 0: the kernels the dispatch picks for performance. */
+ * HDD_VARIANT value a context of the -DHDD_ABLATION build reads at creation; the product library takes no kernel
+ * choice from the environment) so that the tests can compare them bit for bit / to rounding with the default kernels.  Default 0: the kernels the dispatch picks for performance. */
 enum {
   HDD_VARIANT_Q1_WHOLE_TILE = 1,      /* Q1: the whole-tile image kernel on every mesh (the default on element-major
                                          meshes and on the sharded step's SKIP launches) instead of the half-image one */

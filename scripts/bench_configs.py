@@ -261,7 +261,9 @@ def c5(args):
     nbr_own = nbr[:, loc.own_begin:loc.own_end]
     xy_inner = int((nbr_own[:4] >= 0).sum()); xy_dir = int((nbr_own[:4] == H.NBR_DIRICHLET).sum())
     z_inner = int((nbr_own[4:] >= 0).sum()); z_dir = int((nbr_own[4:] == H.NBR_DIRICHLET).sum())
-    legacy = int(os.environ.get("HDD_VARIANT", "0") or 0, 0) & H.VARIANT_HEX_Q3_REGISTER
+    # (HDD_VARIANT selects the register kernel only in the ablation build, HDD_AMD_LIB=.../libhdd_abl.so)
+    legacy = ("abl" in os.path.basename(H.LIB_PATH)
+              and int(os.environ.get("HDD_VARIANT", "0") or 0, 0) & H.VARIANT_HEX_Q3_REGISTER)
     if deg != 3:
         n_mfma = 0
     elif legacy:

@@ -1,6 +1,8 @@
 """Tiles (single-wave workgroups) per CU of the persistent tile kernels, swept in ONE process, interleaved rounds: one
 context per value (HDD_P1_WGCU is read at context creation; it overrides every persistent policy's measured WGCU,
-still capped by the LDS).  usage: python scripts/sweep_wgcu.py c4|c2 [wgcu ...]   (default: 4 5 6 7 8)"""
+still capped by the LDS).  Only the ablation build reads it (make -C dune-hdd_amd ablation; run with
+HDD_AMD_LIB=dune-hdd_amd/lib_ab/libhdd_abl.so): release libraries take no kernel choice from the environment.
+usage: python scripts/sweep_wgcu.py c4|c2 [wgcu ...]   (default: 4 5 6 7 8)"""
 import os
 import sys
 

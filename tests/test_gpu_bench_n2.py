@@ -14,6 +14,18 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def _check_roofline(r, n):
+    """N > 1: frac = every rank's algorithmic bytes / the SLOWEST rank's event-timed step / (N x the per-GPU peak)"""
+    assert r["peak"] == n * r["peak_per_gpu"]
+    assert r["algorithmic_bytes_all_ranks"] >= r["algorithmic_bytes_per_launch"]
+    expect = r["algorithmic_bytes_all_ranks"] / (r["step_ms_event_max_rank"] * 1e-3) / 1e9
+    assert abs(r["achieved"] - expect) <= 1e-9 * expect
+    assert abs(r["frac"] - expect / r["peak"]) <= 1e-9
+    s = r["slowest_rank"]
+    assert 0 <= s["rank"] < n and abs(s["step_ms_event"] - r["step_ms_event_max_rank"]) <= 1e-12
+    assert abs(s["frac"] - s["algorithmic_bytes"] / (s["step_ms_event"] * 1e-3) / 1e9 / r["peak_per_gpu"]) <= 1e-9
+
+
 def _run(port, extra):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
            "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "gloo",
@@ -34,6 +46,7 @@ def test_bench_two_ranks_c2_strips():
     assert sorted(sum(r["kernels_by_rank"].values(), [])) == [0, 1]
     assert all("P1PwcPolicy" in k for k in r["kernels_by_rank"])
     assert r["step_ms_event_max_rank"] >= r["step_ms_event"] > 0
+    _check_roofline(r, 2)
     assert "halo peers [1]" in err and "halo peers [0]" in err
 
 
@@ -45,3 +58,6 @@ def test_bench_two_ranks_c4_columns():
     assert sorted(sum(r["kernels_by_rank"].values(), [])) == [0, 1]
     assert all("Q1PwcPolicy" in k for k in r["kernels_by_rank"])
     assert "then every tile" in d["config"]["parallelism"]
+    _check_roofline(r, 2)
+    # the C4 rank piece at N = 2 is not the profiled N = 1 launch: no stamped figures
+    assert r["traffic"] is None and r["kernel_ms_rocprof"] is None
