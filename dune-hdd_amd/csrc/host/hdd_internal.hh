@@ -8,7 +8,8 @@
 
 namespace hdd {
 std::string& last_error_slot();
-// name of the last persistent tile kernel launched on this thread (hdd_last_tile_kernel): static strings only
+// name of the assembly kernel the last hdd_swipdg_assemble call on this thread launched (hdd_last_tile_kernel; every
+// launch path sets it, element-list side passes keep the tile launch's): static strings only
 const char*& last_tile_kernel_slot();
 int set_error(int code, const std::string& msg);
 int ctx_device(const hdd_ctx* ctx);   // HIP device ordinal a context is bound to

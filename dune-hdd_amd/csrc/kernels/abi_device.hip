@@ -292,6 +292,9 @@ static int assemble_impl(hdd_ctx* ctx, const hdd_mesh* m, const hdd_scalar_fn* k
     return set_error(HDD_ERR_RANGE, "hdd_swipdg_assemble: 0 <= own_begin <= own_end <= n_local violated");
   if (m->n_local >= int64_t(INT32_MAX))
     return set_error(HDD_ERR_RANGE, "hdd_swipdg_assemble: n_local must fit int32 neighbour ids");
+  // hdd_last_tile_kernel names the kernel THIS call launches (every launch path sets it); an element-list pass (the
+  // sharded step's side pass beside its tile launch) leaves the tile launch's name in place
+  if (!list_elements) hdd::last_tile_kernel_slot() = "";
   // The sharded step (shard.hip) runs this function on two streams at once with one context: the element-list
   // pass on the transfer stream beside the SKIP launch on the caller's stream.  That is safe only because the
   // 2d paths below (tiles, element lists, skip_ghost) use no context workspace (ws / scan_ws / rhs_ws); the

@@ -27,8 +27,10 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstdlib>
+#include <string>
 #include <type_traits>
 
+#include "hdd_internal.hh"
 #include "swipdg_kernels.hh"
 #include "trig_phase.hh"
 
@@ -974,9 +976,11 @@ static hipError_t launch_hex_q3(const HexArgs& a, hipStream_t s)
   hipLaunchKernelGGL(hex_q3_setup_kernel, dim3(unsigned((n_own + 255) / 256)), dim3(256), 0, s, a);
   if (a.variant & HDD_VARIANT_HEX_Q3_REGISTER) {   // the register-fragment MFMA kernel (operands generated per element)
     const int64_t grid = std::min<int64_t>(n_own, 1 << 20);
+    hdd::last_tile_kernel_slot() = "hex_q3_kernel";
     hipLaunchKernelGGL(hex_q3_kernel, dim3(unsigned(grid)), dim3(256), 0, s, a);
     return hipGetLastError();
   }
+  hdd::last_tile_kernel_slot() = "hex_q3g_kernel";
   const int64_t n_groups = (n_own + 15) / 16;
   hipLaunchKernelGGL(hex_q3g_coef_kernel, dim3(unsigned((n_groups * 16 + 255) / 256)), dim3(256), 0, s, a, n_groups);
   // 16 row quads x 8 XCDs x reps workgroups of 4 row waves
@@ -1006,6 +1010,8 @@ static hipError_t launch_hex_t(const HexArgs& a, hipStream_t s)
   const int64_t n_own = a.own_end - a.own_begin;
   if (n_own <= 0) return hipSuccess;
   const int64_t grid = std::min<int64_t>(n_own, 1 << 20);
+  static const std::string name = "hex_qp_kernel<" + std::to_string(P) + ", " + std::to_string(SM) + ">";
+  hdd::last_tile_kernel_slot() = name.c_str();   // (hdd_last_tile_kernel)
   hipLaunchKernelGGL((hex_qp_kernel<P, SM>), dim3(unsigned(grid)), dim3(C::THREADS), 0, s, a);
   return hipGetLastError();
 }

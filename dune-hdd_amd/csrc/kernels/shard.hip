@@ -532,9 +532,12 @@ static int device_post(hdd_comm* c, int32_t n_peers, const int32_t* peers, const
 // direct (RCCL only; the serial step): the group send/recv on `stream` itself instead of the transfer stream --
 // nothing overlaps it there, and it saves the two cross-stream hops (ready -> transfer stream, done -> `stream`),
 // ~5 us each on the one-card traces; the ready / done events are still recorded for the watchdog.
+// also_ready / also_done (optional): events of the caller recorded right after the communicator's own ready / done
+// events on the same streams -- the sharded step's watchdog stages, owned by the shard, so that a later post on the
+// same communicator or its destruction cannot change what the step query reports
 static int comm_post(hdd_comm* c, int32_t n_peers, const int32_t* peers, const double* const* d_send,
                      const int64_t* send_count, double* const* d_recv, const int64_t* recv_count, void* stream,
-                     bool direct)
+                     bool direct, hipEvent_t also_ready = nullptr, hipEvent_t also_done = nullptr)
 {
   if (!c || n_peers < 0 || (n_peers && (!peers || !d_send || !send_count || !d_recv || !recv_count)))
     return set_error(HDD_ERR_INVALID, "hdd_comm_post: invalid argument");
@@ -548,6 +551,7 @@ static int comm_post(hdd_comm* c, int32_t n_peers, const int32_t* peers, const d
   c->direct = nullptr;
   if (direct && (c->kind == hdd_comm::RCCL_OWNED || c->kind == hdd_comm::RCCL_WRAPPED)) {
     e = hipEventRecord(c->ready, s);
+    if (e == hipSuccess && also_ready) e = hipEventRecord(also_ready, s);
     if (e != hipSuccess) return hip_fail(e, "hdd_comm_post: record ready");
     const RcclApi& R = rccl();
     ncclResult_t r = R.GroupStart();
@@ -566,6 +570,7 @@ static int comm_post(hdd_comm* c, int32_t n_peers, const int32_t* peers, const d
     if (r != ncclSuccess) return nccl_fail(r, "ncclSend/ncclRecv");
     if (r2 != ncclSuccess) return nccl_fail(r2, "ncclGroupEnd");
     e = hipEventRecord(c->done, s);
+    if (e == hipSuccess && also_done) e = hipEventRecord(also_done, s);
     if (e != hipSuccess) return hip_fail(e, "hdd_comm_post: record completion");
     c->posted = true;
     c->direct = s;
@@ -574,12 +579,14 @@ static int comm_post(hdd_comm* c, int32_t n_peers, const int32_t* peers, const d
   if (c->kind != hdd_comm::HOST) {
     // the transfer stream starts after the packs already enqueued on `stream`
     e = hipEventRecord(c->ready, s);
+    if (e == hipSuccess && also_ready) e = hipEventRecord(also_ready, s);
     if (e == hipSuccess) e = hipStreamWaitEvent(c->xfer, c->ready, 0);
     if (e != hipSuccess) return hip_fail(e, "hdd_comm_post: order transfer after pack");
     if (c->kind == hdd_comm::DEVICE) {
       const int rc = device_post(c, n_peers, peers, d_send, send_count, d_recv, recv_count);
       if (rc) return rc;
       e = hipEventRecord(c->done, c->xfer);
+      if (e == hipSuccess && also_done) e = hipEventRecord(also_done, c->xfer);
       if (e != hipSuccess) return hip_fail(e, "hdd_comm_post: record completion");
       c->posted = true;
       return HDD_OK;
@@ -601,6 +608,7 @@ static int comm_post(hdd_comm* c, int32_t n_peers, const int32_t* peers, const d
     if (r != ncclSuccess) return nccl_fail(r, "ncclSend/ncclRecv");
     if (r2 != ncclSuccess) return nccl_fail(r2, "ncclGroupEnd");
     e = hipEventRecord(c->done, c->xfer);
+    if (e == hipSuccess && also_done) e = hipEventRecord(also_done, c->xfer);
     if (e != hipSuccess) return hip_fail(e, "hdd_comm_post: record completion");
     c->posted = true;
     return HDD_OK;
@@ -718,8 +726,9 @@ struct hdd_shard {
   double* d_fixbuf = nullptr;          // side buffers of the off-stream fixup (n_comp x (n_fix + 1) x fix_rb)
   size_t fixbuf_doubles = 0;
   // watchdog (hdd_block_step_query / _sync): the stages the last step recorded events for, and a marker event
-  uint32_t stages = 0;                 // bit 0: pack (comm->ready), 1: exchange (comm->done), 2: element pass (ev_out)
-  const hdd_comm* stage_comm = nullptr;
+  uint32_t stages = 0;                 // bit 0: pack (ev_pack), 1: exchange (ev_xdone), 2: element pass (ev_out)
+  hipEvent_t ev_pack = nullptr, ev_xdone = nullptr;   // recorded beside the communicator's ready / done (comm_post)
+  std::vector<int32_t> stage_peers;    // the halo peers of the last step (watchdog messages)
   hipEvent_t ev_mark = nullptr;
   bool marked = false;
 };
@@ -732,6 +741,8 @@ extern "C" void hdd_shard_destroy(hdd_shard* sh)
   if (sh->ev_in) (void)hipEventDestroy(sh->ev_in);
   if (sh->ev_out) (void)hipEventDestroy(sh->ev_out);
   if (sh->ev_mark) (void)hipEventDestroy(sh->ev_mark);
+  if (sh->ev_pack) (void)hipEventDestroy(sh->ev_pack);
+  if (sh->ev_xdone) (void)hipEventDestroy(sh->ev_xdone);
   for (void* p : {static_cast<void*>(sh->d_coords), static_cast<void*>(sh->d_nbrs), static_cast<void*>(sh->d_finfo),
                   static_cast<void*>(sh->d_gid), static_cast<void*>(sh->d_send_idx), static_cast<void*>(sh->d_sbuf),
                   static_cast<void*>(sh->d_rbuf), static_cast<void*>(sh->d_tiles_in),
@@ -1039,7 +1050,6 @@ extern "C" int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm*
   hipError_t e = hipSetDevice(sh->device);
   if (e != hipSuccess) return hip_fail(e, "hdd_block_assemble_sharded: hipSetDevice");
   sh->stages = 0;
-  sh->stage_comm = comm;
   sh->marked = false;
   // Default schedule by element type and peer count (one-card step study, profiles/r04/e_reserve/): P1 ranks with
   // two peers split the tiles -- interior tiles during the exchange, the 2 % of tiles with a ghost-adjacent element
@@ -1130,7 +1140,12 @@ extern "C" int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm*
   // into a value-major (SoA) side buffer -- each store instruction 64 consecutive doubles -- and one wave per
   // element writes its row block into place after the join (a kernel after the tiles: +18 % at C4 N = 8).
   const bool scatter = offfix && !(flags & HDD_SHARD_FIX_INPLACE) && (flags & HDD_SHARD_FIX_SCATTER);
-  const bool soa = scatter && q1;
+  // the value-major pass exists for the closed-form Q1 policy only (piecewise-constant kappa: Q1PwcPolicy::emit); a
+  // smooth kappa (GenericPolicy) takes the row-block side buffer + hdd_scatter_fix like P1
+  bool pwc_kappa = true;
+  for (int32_t c = 0; c < n_comp; ++c)
+    pwc_kappa = pwc_kappa && (kappa[c].kind == HDD_FN_CONST || kappa[c].kind == HDD_FN_PER_ELEM);
+  const bool soa = scatter && q1 && pwc_kappa;
   const int32_t rb = hdd_fix_rb(sh->gi.elem_type);
   const int64_t soa_ld = (sh->n_fix + 1 + 63) & ~int64_t(63);   // SoA rows start 512-byte aligned
   std::vector<double*> fbufs;
@@ -1187,8 +1202,15 @@ extern "C" int hdd_block_assemble_sharded(hdd_ctx* ctx, hdd_shard* sh, hdd_comm*
       }
     }
     // serial step (no overlap, ps == s): RCCL runs straight on `stream`
-    rc = comm_post(comm, int32_t(mp.size()), mp.data(), ms.data(), mn.data(), mr.data(), mrn.data(), ps, !overlap);
-    if (rc == HDD_OK && comm->kind != hdd_comm::HOST) sh->stages |= 3u;
+    const bool staged = comm->kind != hdd_comm::HOST;
+    if (staged && !sh->ev_pack && hipEventCreateWithFlags(&sh->ev_pack, hipEventDisableTiming) != hipSuccess)
+      return set_error(HDD_ERR_HIP, "hdd_block_assemble_sharded: stage event");
+    if (staged && !sh->ev_xdone && hipEventCreateWithFlags(&sh->ev_xdone, hipEventDisableTiming) != hipSuccess)
+      return set_error(HDD_ERR_HIP, "hdd_block_assemble_sharded: stage event");
+    rc = comm_post(comm, int32_t(mp.size()), mp.data(), ms.data(), mn.data(), mr.data(), mrn.data(), ps, !overlap,
+                   staged ? sh->ev_pack : nullptr, staged ? sh->ev_xdone : nullptr);
+    if (rc == HDD_OK && staged) sh->stages |= 3u;
+    if (rc == HDD_OK) sh->stage_peers = comm->last_peers;
     // host transport on the side stream, fixup on `stream`: the ghost columns were written on ps
     if (rc == HDD_OK && side && !offfix && ps != s && comm->kind == hdd_comm::HOST &&
         hipEventRecord(sh->ev_out, ps) != hipSuccess)
@@ -1325,8 +1347,7 @@ extern "C" int hdd_block_step_mark(hdd_shard* sh, void* stream)
 extern "C" int hdd_block_step_query(hdd_shard* sh, int32_t* stage)
 {
   if (!sh || !stage || sh->host_only) return set_error(HDD_ERR_INVALID, "hdd_block_step_query: invalid argument");
-  const hdd_comm* c = sh->stage_comm;
-  const hipEvent_t evs[4] = {(sh->stages & 1u) && c ? c->ready : nullptr, (sh->stages & 2u) && c ? c->done : nullptr,
+  const hipEvent_t evs[4] = {(sh->stages & 1u) ? sh->ev_pack : nullptr, (sh->stages & 2u) ? sh->ev_xdone : nullptr,
                              (sh->stages & 4u) ? sh->ev_out : nullptr, sh->marked ? sh->ev_mark : nullptr};
   *stage = HDD_STAGE_COMPLETE;
   for (int i = 0; i < 4; ++i) {
@@ -1359,8 +1380,7 @@ extern "C" int hdd_block_step_sync(hdd_shard* sh, void* stream, double timeout_s
     const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     if (dt > timeout_s) {
       std::string peers;
-      if (sh->stage_comm)
-        for (int32_t p : sh->stage_comm->last_peers) peers += (peers.empty() ? "" : ", ") + std::to_string(p);
+      for (int32_t p : sh->stage_peers) peers += (peers.empty() ? "" : ", ") + std::to_string(p);
       return set_error(HDD_ERR_TIMEOUT, "rank " + std::to_string(sh->rank) + " of " + std::to_string(sh->nranks) +
                                             ": the sharded step's " + stage_names[st] + " did not complete within " +
                                             std::to_string(timeout_s) + " s (halo peers: " +

@@ -2596,6 +2596,12 @@ static hipError_t launch_t(const AssembleArgs& a, hipStream_t s)
 {
   const int64_t n_own = a.own_end - a.own_begin;
   if (n_own <= 0) return hipSuccess;
+  static const std::string name = [] {   // "swipdg_assemble_kernel<E, NQV, NQF, PWC>" (hdd_last_tile_kernel)
+    const std::string f = __PRETTY_FUNCTION__;
+    const size_t i = f.find('['), j = f.rfind(']');
+    return "swipdg_assemble_kernel<" + (i == std::string::npos ? std::string("?") : f.substr(i + 1, j - i - 1)) + ">";
+  }();
+  hdd::last_tile_kernel_slot() = name.c_str();
   const int64_t tiles = (n_own + 63) / 64;
   // tile image (64 elements x full row blocks) + 1 alignment slot + a scratch row for tail lanes
   const size_t lds = (size_t(64) * E::NB * (E::NF + 1) * E::NB + 2 + (E::NF + 1) * E::NB) * sizeof(double);

@@ -7,6 +7,12 @@ with a watchdog thread beside it: if the deadline passes first, the watchdog ask
 rank's last sharded step has not completed (hdd_block_step_query: halo pack, halo exchange, ghost-adjacent element
 pass, tile assembly and join), prints the rank, the stage and the halo peers to stderr and ends the process with a
 non-zero status (os._exit: no re-exec, no retry, no Python teardown that could block on the device again).
+
+Coverage: the stage report needs device-side stage events, which the RCCL and in-process device transports record
+(the exchange runs on the device).  The host transport (hdd_comm_create_host: gloo, MPI, a mailbox -- bench.py's
+`--backend gloo` rehearsal) exchanges synchronously inside the step call, before this guard is armed: a stalled peer
+blocks there and is bounded only by the transport's own timeout (the gloo process group's, >= 120 s in bench.py),
+and no stage is named.
 """
 import os
 import sys

@@ -43,7 +43,12 @@ def code_objects(lib):
 
 
 def scan_text(lines):
-    """-> [(symbol, store line, next line)] for every hazard in one disassembly"""
+    """-> [(symbol, store line, next line)] for every hazard in one disassembly.
+
+    Window: the ONE instruction right after the store.  That is the hazard's extent on gfx950 (the VALU write
+    conflicts with the store's read of its data registers only in the slot immediately following the issue; one
+    wait state -- an s_nop or any other instruction -- resolves it, which is how hipcc pads the soffset-free form),
+    so a register overwritten two or more instructions later is not a hazard."""
     out, sym, pend = [], "?", None
     for line in lines:
         m = SYM.match(line.strip())

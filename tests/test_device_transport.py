@@ -12,6 +12,8 @@ Reference semantics: block-swipdg.hh:355-382 (the owner of ss writes A_ss and A_
 Checks, for C2-like strips (P1 Kuhn, one subdomain column per rank) and C4-like subdomain columns (Q1, 2 x 4
 subdomains per rank), at N = 2 and N = 3 (a middle rank with two peers):
   * every rank's rows are bit-identical to the single-GPU assembly of the same block grid;
+  * Q1 with a smooth diffusion factor (quadrature policy) through every schedule, the side-buffer one included
+    (its value-major pass exists for the closed-form policy only: ADVICE r5);
   * the default, in-place, side-buffer (scatter), inline, split-tile and serial schedules agree bit for bit;
   * three consecutive steps per schedule (the second and third re-pack while the previous step's receivers may
     still read the send buffers: the "copied" ordering), with the ghost columns reset to NaN before each
@@ -49,7 +51,15 @@ def _layout(kind, n):
         return H.Grid.structured(H.CUBE, 56 * n, 36, LOWER, UPPER, px=2 * n, py=4), H.TENSOR_ISO_PER_ELEM, True
     if kind == "p1_sym":    # symmetric tensor, per-element diffusion factor
         return H.Grid.structured(H.SIMPLEX, 40 * n, 18, LOWER, UPPER, px=2 * n, py=2), H.TENSOR_SYM_PER_ELEM, True
+    if kind == "q1_smooth":   # Q1 with a smooth (sinusoid) diffusion factor: the quadrature policy, no closed form
+        return H.Grid.structured(H.CUBE, 48 * n, 30, LOWER, UPPER, px=2 * n, py=3), H.TENSOR_ISO_PER_ELEM, "smooth"
     raise ValueError(kind)
+
+
+def _kappas(two, kap_dev):
+    if two == "smooth":
+        return [H.scalar_fn(H.FN_SINUSOID, 1.0, 0.5, 3.0, 2.0, order=3)]
+    return [H.scalar_fn(H.FN_CONST, 1.0)] + ([H.scalar_fn(H.FN_PER_ELEM, per_elem=kap_dev)] if two else [])
 
 
 def _coefficients(centers):
@@ -67,8 +77,7 @@ def _single_gpu(grid, tk, two):
     ctx = H.Context(0)
     dm, dp = H.DeviceMesh(loc, 0), H.DevicePattern(loc, 0)
     tensor = H.tensor_fn(tk, per_elem=torch.from_numpy(iso if tk == H.TENSOR_ISO_PER_ELEM else sym).cuda())
-    kappas = [H.scalar_fn(H.FN_CONST, 1.0)] + (
-        [H.scalar_fn(H.FN_PER_ELEM, per_elem=torch.from_numpy(kap).cuda())] if two else [])
+    kappas = _kappas(two, torch.from_numpy(kap).cuda())
     out = np.stack([v.cpu().numpy() for v in H.assemble(ctx, dm, dp, kappas, tensor)])
     torch.cuda.synchronize()
     return out
@@ -91,7 +100,7 @@ class _Rank:
             self.host.append(a)
         self.dev = [torch.from_numpy(a).cuda() for a in self.host]
         self.tensor = H.tensor_fn(tk, per_elem=self.dev[0])
-        self.kappas = [H.scalar_fn(H.FN_CONST, 1.0)] + ([H.scalar_fn(H.FN_PER_ELEM, per_elem=self.dev[1])] if two else [])
+        self.kappas = _kappas(two, self.dev[1])
         _, _, _, self.pat = self.sh.pattern(self.ctx)
         self.comm = H.Comm.device(hub, r, 0)
         self.stream = torch.cuda.Stream()
@@ -140,7 +149,8 @@ def run_device_ranks(grid, n, tk, two, schedules, steps=3, flags_extra=0):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kind,n", [("c2_p1", 2), ("c2_p1", 3), ("c4_q1", 2), ("c4_q1", 3), ("p1_sym", 3)])
+@pytest.mark.parametrize("kind,n", [("c2_p1", 2), ("c2_p1", 3), ("c4_q1", 2), ("c4_q1", 3), ("p1_sym", 3),
+                                    ("q1_smooth", 3)])
 def test_device_transport_equals_single_gpu(kind, n):
     grid, tk, two = _layout(kind, n)
     got, infos = run_device_ranks(grid, n, tk, two, SCHEDULES)

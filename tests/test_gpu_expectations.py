@@ -41,7 +41,10 @@ def test_sgrid_q1_table_from_gpu_matrix(ctx):
     assert l2s == SGRID_L2 and h1s == SGRID_H1
 
 
-@pytest.mark.parametrize("p", [1, 4])
+# the reference runs the block table at the partitions [1 1 1], [2 2 1], [4 4 1], [8 8 1]
+# (test/linearelliptic-block-swipdg.cc:68-77), each pinned to the same values
+# (..._esv2007_2daluconform.cxx:35-37, 60-62, 85-87, 110-112): p x p subdomains, p = 1 the monolithic case
+@pytest.mark.parametrize("p", [1, 2, 4, 8])
 def test_alu_p1_table_from_gpu_matrix(ctx, p):
     l2s, h1s = [], []
     for lvl in range(4):

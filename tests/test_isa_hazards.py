@@ -12,14 +12,27 @@ sys.path.insert(0, os.path.join(ROOT, "scripts"))
 LIB = os.path.join(ROOT, "dune-hdd_amd", "lib", "libhdd_amd.so")
 
 
-@pytest.mark.timeout(300)
-def test_no_store_data_hazard_in_library():
+def _scan():
     import check_store_hazard as C
-    if not os.path.exists(LIB) or not os.path.exists(C.OBJDUMP):
-        pytest.skip("library not built or llvm-objdump absent")
+    if not os.path.exists(LIB):
+        pytest.skip("library not built")
+    # a built library with no disassembler must not pass silently: the guard would check nothing
+    assert os.path.exists(C.OBJDUMP), "library present but %s absent: the hazard scan cannot run" % C.OBJDUMP
     n, found = C.scan_lib(LIB)
     assert n > 0, "no gfx950 code object found in %s" % LIB
     assert not found, "store-data hazards: %s" % found[:5]
+
+
+@pytest.mark.timeout(300)
+def test_no_store_data_hazard_in_library():
+    _scan()
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_no_store_data_hazard_in_library_gpu_suite():
+    """the same scan in the GPU suite, on the box that loads the library (same image: llvm-objdump present)"""
+    _scan()
 
 
 def test_scanner_flags_the_round5_pattern():
