@@ -1754,8 +1754,9 @@ struct P1SmoothFusedPolicy : P1SmoothPolicy<TK, VX> {
       return c == 0 ? K0.c + K0.b * sh.sf[f][q] : K1.c + K1.b * sh.sf[f][q];
     });
   }
-  // full interior tiles: branch-free faces (see P1PwcPolicy::compute_full)
-  static constexpr bool FULLTILE = true;
+  // (no FULLTILE path: a branch-free second copy of the two-component emission measured slower -- C3 0.249 vs 0.234
+  // ms per assembly, rocprof averages on one box, profiles/r06/c_c3/; the kernel is one wave per SIMD and larger code
+  // / register allocation across both copies cost more than the branches save)
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -2287,20 +2288,10 @@ swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
       double* img = active ? lds + off : scratch;
       if constexpr (TWO) {   // the shared part once, then both components into their images
         P::prepare(a, own, shv);
-        if (HDD_ABL(a, 1)) {
-        } else if (fullt) {
-          P::template emit_two<true>(a, e, own, gat, shv, lds + off, lds + IMGS + off);
-        } else {
-          P::emit_two(a, e, own, gat, shv, img, img + IMGS);
-        }
+        if (!HDD_ABL(a, 1)) P::emit_two(a, e, own, gat, shv, img, img + IMGS);
       } else if constexpr (FUSED) {   // the shared part once, then component 0 (the others after its stores)
         P::prepare(a, own, shv);
-        if (HDD_ABL(a, 1)) {
-        } else if (fullt) {
-          P::template emit_component<true>(a, 0, e, own, gat, shv, lds + off);
-        } else {
-          P::emit_component(a, 0, e, own, gat, shv, img);
-        }
+        if (!HDD_ABL(a, 1)) P::emit_component(a, 0, e, own, gat, shv, img);
       } else if constexpr (fulltile_of<P>::value) {
         if (HDD_ABL(a, 1)) {
         } else if (fullt) {
@@ -2467,12 +2458,7 @@ swipdg_persistent_kernel(const AssembleArgs a, int64_t n_tiles)
     } else if constexpr (FUSED) {   // the other components: same image slots, their own value arrays
       for (int c = 1; c < a.n_comp; ++c) {
         double* img = active ? lds + off : scratch;
-        if (HDD_ABL(a, 1)) {
-        } else if (fullt) {
-          P::template emit_component<true>(a, c, e, own, gat, shv, lds + off);
-        } else {
-          P::emit_component(a, c, e, own, gat, shv, img);
-        }
+        if (!HDD_ABL(a, 1)) P::emit_component(a, c, e, own, gat, shv, img);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");

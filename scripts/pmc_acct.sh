@@ -4,17 +4,19 @@
 # SCA / VMEM / MISC / FLAT parts) + WAIT_ANY (parked at s_waitcnt / barrier) + WAIT_INST_ANY (issue stall) --
 # then FETCH_SIZE / WRITE_SIZE.  Environment (HDD_DEBUG_FLAGS ...) passes through to bench.py.
 # usage: scripts/pmc_acct.sh TAG [bench.py args...]      (summary: scripts/pmc_summary.py)
+#        PMC_SCRIPT=scripts/bench_configs.py scripts/pmc_acct.sh TAG c3 --steps 5   (any script, args as given)
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 ROOT=$(pwd)
 OUT=$ROOT/gpurun_out
 TAG=$1; shift
-ARGS="--steps 5 --warmup 2 --no-cpu-baseline $*"
+SCRIPT=${PMC_SCRIPT:-bench.py}
+if [ -n "${PMC_SCRIPT:-}" ]; then ARGS="$*"; else ARGS="--steps 5 --warmup 2 --no-cpu-baseline $*"; fi
 export TMPDIR=/tmp
 cd /tmp
 mkdir -p "$OUT/pmc_$TAG"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/pmc_$TAG/stats" -o run --output-format csv -- \
-  python3 "$ROOT/bench.py" $ARGS > "$OUT/pmc_$TAG/stats.log" 2>&1
+  python3 "$ROOT/$SCRIPT" $ARGS > "$OUT/pmc_$TAG/stats.log" 2>&1
 rc=$?
 echo "stats rc=$rc"
 [ $rc -eq 0 ] || exit $rc
@@ -25,7 +27,7 @@ for pmc in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY 
            "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i+1))
   timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $pmc -d "$OUT/pmc_$TAG/p$i" -o run --output-format csv -- \
-    python3 "$ROOT/bench.py" $ARGS > "$OUT/pmc_$TAG/p$i.log" 2>&1
+    python3 "$ROOT/$SCRIPT" $ARGS > "$OUT/pmc_$TAG/p$i.log" 2>&1
   rc=$?
   echo "pass $i ($pmc) rc=$rc"
   [ $rc -eq 0 ] || exit $rc
