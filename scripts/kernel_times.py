@@ -77,6 +77,16 @@ def main():
                            window_launches_us=[round(x / 1e3, 1) for x in win],
                            avg_ns_without_first=statistics.fmean(dur[1:]),
                            trace_source=os.path.relpath(traces[0], ROOT))
+        # the profiled bench command's own JSON line (gpu.sh "prof" writes it to PROF_DIR.log): its step time brackets
+        # the same launches the window averages
+        blog = d.rstrip("/") + ".log"
+        if os.path.exists(blog):
+            for line in open(blog):
+                if line.startswith("{"):
+                    b = json.loads(line)
+                    ent.update(profiled_run_ms_per_step=b["ms_per_step"],
+                               profiled_run_step_ms_event=b["roofline"]["step_ms_event"],
+                               profiled_run_log=os.path.relpath(blog, ROOT))
         res["workloads"][wl] = ent
     os.makedirs(os.path.dirname(os.path.abspath(out)), exist_ok=True)
     json.dump(res, open(out, "w"), indent=1)
