@@ -329,8 +329,18 @@ def main():
         if os.path.exists(args.traffic_json) and same_launch:
             try:
                 tj = json.load(open(args.traffic_json))
-                if tj.get("build_id") == bid and wl_key in tj.get("workloads", {}):
-                    traffic = tj["workloads"][wl_key]["hbm_bytes_per_launch"]
+                tw = tj.get("workloads", {}).get(wl_key)
+                # the counters' kernel in hdd_last_tile_kernel()'s form (rocprof's demangled name, namespaces dropped)
+                tk = (tw or {}).get("kernel", "").split("(")[0].replace("void ", "").replace("hdd::dev::", "")
+                if tj.get("build_id") != bid:
+                    traffic_src = "n/a: %s measured on build %s, timed build %s" % (
+                        os.path.relpath(args.traffic_json, ROOT), tj.get("build_id"), bid)
+                elif tw is None:
+                    traffic_src = "n/a: workload %s not in %s" % (wl_key, os.path.relpath(args.traffic_json, ROOT))
+                elif tk != kernel_label:
+                    traffic_src = "n/a: the timed launch (%s) is not the counted kernel (%s)" % (kernel_label, tk)
+                else:
+                    traffic = tw["hbm_bytes_per_launch"]
                     traffic_src = os.path.relpath(args.traffic_json, ROOT)
             except (OSError, ValueError, KeyError):
                 traffic = None
@@ -339,7 +349,13 @@ def main():
             try:
                 kj = json.load(open(args.kernel_times_json))
                 ent = kj.get("workloads", {}).get("c4" if c4 else "c2", {})
-                if kj.get("build_id") == bid and ent.get("kernel") == kernel_label:
+                if kj.get("build_id") != bid:
+                    rocprof_src = "n/a: %s profiled build %s, timed build %s" % (
+                        os.path.relpath(args.kernel_times_json, ROOT), kj.get("build_id"), bid)
+                elif ent.get("kernel") != kernel_label:
+                    rocprof_src = "n/a: the timed launch (%s) is not the profiled kernel (%s)" % (kernel_label,
+                                                                                             ent.get("kernel"))
+                else:
                     # the launches of the bench command's timed window (scripts/kernel_times.py), else the all-launch
                     # average of an older file
                     rocprof_ms = ent.get("window_avg_ns", ent["avg_ns"]) * 1e-6
