@@ -1,8 +1,7 @@
 #!/usr/bin/env python3
 """C3 (OS2014 1024^2 Kuhn, affine part + mu-component, sinusoid kappa) under its verification variants, interleaved
 rounds in ONE process on one box: the default two-component pass (P1SmoothFusedPolicy TWO), one launch per component
-(HDD_VARIANT_C3_PER_COMPONENT: P1SmoothPolicy, one value stream per wave, two waves per SIMD), and the quadrature
-policy (HDD_VARIANT_P1_SMOOTH_QUADRATURE).  Prints the median / min per variant and checks that the variants agree
+(HDD_VARIANT_C3_PER_COMPONENT: P1SmoothPolicy, one value stream per wave, two waves per SIMD).  Prints the median / min per variant and checks that the variants agree
 (to rounding: the fused volume moment is a_c sum w + b_c sum w sin).
 usage: python scripts/study/c3_variants.py [rounds]"""
 import math
@@ -45,8 +44,7 @@ def main():
             torch.cuda.synchronize()
             res[name].append(e0.elapsed_time(e1) / 20)
     for name in variants:
-        print("c3 %-14s median %.4f ms  min %.4f ms  kernel %s" % (name, np.median(res[name]), np.min(res[name]),
-                                                                  H.last_tile_kernel() if False else ""), flush=True)
+        print("c3 %-14s median %.4f ms  min %.4f ms" % (name, np.median(res[name]), np.min(res[name])), flush=True)
     a, b = vals["two_pass"], vals["per_component"]
     for c in range(2):
         d = (a[c] - b[c]).abs().max().item()
