@@ -2,7 +2,8 @@
 context per value (HDD_P1_WGCU is read at context creation; it overrides every persistent policy's measured WGCU,
 still capped by the LDS).  Only the ablation build reads it (make -C dune-hdd_amd ablation; run with
 HDD_AMD_LIB=dune-hdd_amd/lib_ab/libhdd_abl.so): release libraries take no kernel choice from the environment.
-usage: python scripts/sweep_wgcu.py c4|c2 [wgcu ...]   (default: 4 5 6 7 8)"""
+usage: python scripts/sweep_wgcu.py c4|c2|c3 [wgcu ...]   (default: 4 5 6 7 8)"""
+import math
 import os
 import sys
 
@@ -16,16 +17,22 @@ import hdd_amd as H  # noqa: E402
 
 def main():
     args = sys.argv[1:]
-    wl = args.pop(0) if args and args[0] in ("c2", "c4") else "c4"
+    wl = args.pop(0) if args and args[0] in ("c2", "c3", "c4") else "c4"
     values = [int(v) for v in args] or [4, 5, 6, 7, 8]
-    et, nx, ny, p = (H.SIMPLEX, 3200, 640, 1) if wl == "c2" else (H.CUBE, 3520, 1200, 8)
-    grid = H.Grid.structured(et, nx, ny, (0, 0), (5, 1), px=p, py=p)
-    local = grid.local()
-    rng = np.random.default_rng(10)
-    k = torch.from_numpy(local.checkerboard((0, 0), (5, 1), 100, 20, 10.0 ** rng.uniform(-3, 3, 2000))).cuda()
+    if wl == "c3":   # OS2014 1024^2 Kuhn, affine part + mu-component (scripts/bench_configs.py c3)
+        local = H.Grid.structured(H.SIMPLEX, 1024, 1024, (-1, -1), (1, 1)).local()
+        kap = [H.scalar_fn(H.FN_SINUSOID, 1.0, 0.75, 4 * math.pi, 2 * math.pi, order=3),
+               H.scalar_fn(H.FN_SINUSOID, 0.0, -0.75, 4 * math.pi, 2 * math.pi, order=3)]
+        ten = H.tensor_fn()
+    else:
+        et, nx, ny, p = (H.SIMPLEX, 3200, 640, 1) if wl == "c2" else (H.CUBE, 3520, 1200, 8)
+        grid = H.Grid.structured(et, nx, ny, (0, 0), (5, 1), px=p, py=p)
+        local = grid.local()
+        rng = np.random.default_rng(10)
+        k = torch.from_numpy(local.checkerboard((0, 0), (5, 1), 100, 20, 10.0 ** rng.uniform(-3, 3, 2000))).cuda()
+        kap, ten = [H.scalar_fn(H.FN_CONST, 1.0)], H.tensor_fn(H.TENSOR_ISO_PER_ELEM, per_elem=k)
     dm, dp = H.DeviceMesh(local), H.DevicePattern(local)
-    kap, ten = [H.scalar_fn(H.FN_CONST, 1.0)], H.tensor_fn(H.TENSOR_ISO_PER_ELEM, per_elem=k)
-    vals = [torch.empty(dp.nnz, dtype=torch.float64, device="cuda")]
+    vals = [torch.empty(dp.nnz, dtype=torch.float64, device="cuda") for _ in kap]
     ctxs = {}
     for v in values:
         os.environ["HDD_P1_WGCU"] = str(v)
