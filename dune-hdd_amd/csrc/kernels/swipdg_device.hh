@@ -2628,7 +2628,16 @@ static hipError_t launch_persistent(const AssembleArgs& a, hipStream_t s)
   // tiles per CU measured per policy (profiles/r01/sweep_wg_per_cu.log, profiles/r01/s2/); a.wgcu > 0 is the
   // HDD_P1_WGCU sweep override, read once per context
   int wgcu = a.wgcu > 0 ? a.wgcu : P::WGCU;
-  wgcu = std::max(1, std::min<int>(wgcu, int((160 * 1024) / lds)));   // resident by LDS (Q1 tiles: 3 per CU)
+#ifdef HDD_ABLATION
+  // HDD_P1_WGCU = W + 16 C (C > 0): W tiles per CU with at most C resident per CU -- the dynamic LDS padded to
+  // 160 KB / C, so the dispatcher cannot stack more workgroups on one CU than C (residency study)
+  const size_t lds_launch = a.wgcu >= 16 ? std::max(lds, size_t((160 * 1024) / (a.wgcu >> 4)) & ~size_t(15)) : lds;
+  if (a.wgcu >= 16) wgcu = (a.wgcu & 15) ? (a.wgcu & 15) : P::WGCU;
+#define HDD_LDS_LAUNCH lds_launch
+#else
+#define HDD_LDS_LAUNCH lds
+#endif
+  wgcu = std::max(1, std::min<int>(wgcu, int((160 * 1024) / HDD_LDS_LAUNCH)));   // resident by LDS (Q1 tiles: 3 per CU)
   // The sharded step's full-range launch (SKIP, or every tile beside the SoA side-buffer pass) runs beside the
   // element pass: the grid is shortened
   // by the pass's workgroups (a multiple of 8 keeps the XCD eighths even), so the pass gets SIMDs of its own
@@ -2683,16 +2692,17 @@ static hipError_t launch_persistent(const AssembleArgs& a, hipStream_t s)
       ac.vals[0] = a.vals[c];
     }
     if (a.tile_list)
-      hipLaunchKernelGGL((swipdg_persistent_kernel<P, true>), dim3(unsigned(G)), dim3(64), lds, s, ac, tiles);
+      hipLaunchKernelGGL((swipdg_persistent_kernel<P, true>), dim3(unsigned(G)), dim3(64), HDD_LDS_LAUNCH, s, ac, tiles);
     else if (a.skip_ghost)
-      hipLaunchKernelGGL((swipdg_persistent_kernel<P, false, true>), dim3(unsigned(G)), dim3(64), lds, s, ac, tiles);
+      hipLaunchKernelGGL((swipdg_persistent_kernel<P, false, true>), dim3(unsigned(G)), dim3(64), HDD_LDS_LAUNCH, s, ac, tiles);
     else
-      hipLaunchKernelGGL((swipdg_persistent_kernel<P, false>), dim3(unsigned(G)), dim3(64), lds, s, ac, tiles);
+      hipLaunchKernelGGL((swipdg_persistent_kernel<P, false>), dim3(unsigned(G)), dim3(64), HDD_LDS_LAUNCH, s, ac, tiles);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
 }
+#undef HDD_LDS_LAUNCH
 
 // instantiate a policy for the runtime (tensor kind, piecewise-constant kappa kind) pair
 template <template <int, int> class PT>

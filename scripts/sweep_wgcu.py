@@ -2,6 +2,9 @@
 context per value (HDD_P1_WGCU is read at context creation; it overrides every persistent policy's measured WGCU,
 still capped by the LDS).  Only the ablation build reads it (make -C dune-hdd_amd ablation; run with
 HDD_AMD_LIB=dune-hdd_amd/lib_ab/libhdd_abl.so): release libraries take no kernel choice from the environment.
+A value W + 16 C (C > 0) runs W tiles per CU with at most C resident per CU (the dynamic LDS padded to 160 KB / C).
+NOTE: this in-process sweep can mislead (profiles/r06/e_wgcu: bimodal at 3 per CU); confirm a choice with bench.py
+in fresh processes, the way the driver measures.
 usage: python scripts/sweep_wgcu.py c4|c2|c3 [wgcu ...]   (default: 4 5 6 7 8)"""
 import math
 import os
