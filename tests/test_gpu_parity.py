@@ -410,6 +410,47 @@ def test_scrambled_quad_orientations(ctx, smooth):
     assert ok, worst
 
 
+@pytest.mark.parametrize("coef", ["const", "per_elem_sym", "sinusoid"])
+def test_scrambled_simplex_full_tiles(ctx, coef):
+    """P1 full interior tiles (64 elements with three interior faces: P1PwcPolicy's branch-free compute_full with its
+    static image layout) under a random element numbering and a random vertex order per triangle (rotations and
+    reflections): the row blocks' neighbour order, sorted by id, takes every permutation and the twin-face ids every
+    value.  Interior elements first (shuffled), then the boundary elements (shuffled), so most tiles are full."""
+    torch = _torch()
+    et, coords, ev = O.kuhn_grid(48, 40, (0, 0), (3, 2))
+    rng = np.random.default_rng(11)
+    edges = np.sort(np.stack([ev[:, [0, 1]], ev[:, [0, 2]], ev[:, [1, 2]]], 1), axis=2).reshape(-1, 2)
+    _, inv, cnt = np.unique(edges, axis=0, return_inverse=True, return_counts=True)
+    bnd = (cnt[inv.reshape(-1)].reshape(-1, 3) == 1).any(axis=1)
+    order = np.concatenate([rng.permutation(np.flatnonzero(~bnd)), rng.permutation(np.flatnonzero(bnd))])
+    perms = np.array([[0, 1, 2], [1, 2, 0], [2, 0, 1], [0, 2, 1], [2, 1, 0], [1, 0, 2]])
+    ev = np.ascontiguousarray(np.take_along_axis(ev[order], perms[rng.integers(0, 6, len(order))], 1)).astype(np.int32)
+    grid = H.Grid.from_connectivity(et, coords, ev)
+    ne = ev.shape[0]
+    ten, oten = H.tensor_fn(), O.tensor(O.TENSOR_CONST)
+    if coef == "sinusoid":
+        fns = [H.scalar_fn(H.FN_SINUSOID, 1.0, 0.75, 4 * np.pi, 2 * np.pi, order=3)]
+        ofn = O.scalar(O.FN_SINUSOID, 1.0, 0.75, 4 * np.pi, 2 * np.pi, order=3)
+    elif coef == "per_elem_sym":
+        kap = rng.uniform(0.1, 10.0, ne)
+        sym = np.stack([rng.uniform(0.5, 2.0, ne), rng.uniform(-0.3, 0.3, ne), rng.uniform(0.5, 2.0, ne)], 0)
+        fns = [H.scalar_fn(H.FN_PER_ELEM, per_elem=torch.from_numpy(kap).cuda())]
+        ofn = O.scalar(O.FN_PER_ELEM, per_elem=kap)
+        ten = H.tensor_fn(H.TENSOR_SYM_PER_ELEM, per_elem=torch.from_numpy(np.ascontiguousarray(sym)).cuda())
+        oten = O.tensor(O.TENSOR_SYM_PER_ELEM, per_elem=np.ascontiguousarray(sym.T))
+    else:
+        fns, ofn = [H.scalar_fn(H.FN_CONST, 1.0)], O.scalar(O.FN_CONST, 1.0)
+    local, (rp, col, _), (val,) = _run_product(ctx, grid, fns, ten)
+    nb = local.neighbors[:, local.own_begin:local.own_end]
+    full = (nb >= 0).all(axis=0)[: (local.n_own // 64) * 64].reshape(-1, 64).all(axis=1)
+    assert full.sum() >= 50 and not full.all(), "expected mostly full tiles and some boundary tiles"
+    og = O.Grid(et, coords, ev)
+    orp, ocol, oval = O.assemble(og, ofn, oten, O.params())
+    assert np.array_equal(rp, orp) and np.array_equal(col, ocol)
+    worst, ok = compare_rows(rp, val, oval, RTOL)
+    assert ok, worst
+
+
 @pytest.mark.parametrize("case", ["kuhn_spe10", "quad_spe10", "kuhn_sinusoid_sym", "quad_sinusoid", "nvb", "scrambled"])
 def test_vertex_indexed_geometry_equals_element_major(ctx, case):
     """hdd_mesh elem_vertices / vertex_coords (the default of DeviceMesh and of the shards): the P1 / Q1
