@@ -410,7 +410,7 @@ def test_scrambled_quad_orientations(ctx, smooth):
     assert ok, worst
 
 
-@pytest.mark.parametrize("coef", ["const", "per_elem_sym", "sinusoid"])
+@pytest.mark.parametrize("coef", ["const", "per_elem_sym", "sinusoid", "os2014_two"])
 def test_scrambled_simplex_full_tiles(ctx, coef):
     """P1 full interior tiles (64 elements with three interior faces: P1PwcPolicy's branch-free compute_full with its
     static image layout) under a random element numbering and a random vertex order per triangle (rotations and
@@ -430,25 +430,30 @@ def test_scrambled_simplex_full_tiles(ctx, coef):
     ten, oten = H.tensor_fn(), O.tensor(O.TENSOR_CONST)
     if coef == "sinusoid":
         fns = [H.scalar_fn(H.FN_SINUSOID, 1.0, 0.75, 4 * np.pi, 2 * np.pi, order=3)]
-        ofn = O.scalar(O.FN_SINUSOID, 1.0, 0.75, 4 * np.pi, 2 * np.pi, order=3)
+        ofns = [O.scalar(O.FN_SINUSOID, 1.0, 0.75, 4 * np.pi, 2 * np.pi, order=3)]
+    elif coef == "os2014_two":   # C3's two-component pass (P1SmoothFusedPolicy TWO)
+        comps = os2014_components()
+        fns = [H.scalar_fn(H.FN_SINUSOID, c, b, kx, ky, order=3) for (c, b, kx, ky) in comps]
+        ofns = [O.scalar(O.FN_SINUSOID, c, b, kx, ky, order=3) for (c, b, kx, ky) in comps]
     elif coef == "per_elem_sym":
         kap = rng.uniform(0.1, 10.0, ne)
         sym = np.stack([rng.uniform(0.5, 2.0, ne), rng.uniform(-0.3, 0.3, ne), rng.uniform(0.5, 2.0, ne)], 0)
         fns = [H.scalar_fn(H.FN_PER_ELEM, per_elem=torch.from_numpy(kap).cuda())]
-        ofn = O.scalar(O.FN_PER_ELEM, per_elem=kap)
+        ofns = [O.scalar(O.FN_PER_ELEM, per_elem=kap)]
         ten = H.tensor_fn(H.TENSOR_SYM_PER_ELEM, per_elem=torch.from_numpy(np.ascontiguousarray(sym)).cuda())
         oten = O.tensor(O.TENSOR_SYM_PER_ELEM, per_elem=np.ascontiguousarray(sym.T))
     else:
-        fns, ofn = [H.scalar_fn(H.FN_CONST, 1.0)], O.scalar(O.FN_CONST, 1.0)
-    local, (rp, col, _), (val,) = _run_product(ctx, grid, fns, ten)
+        fns, ofns = [H.scalar_fn(H.FN_CONST, 1.0)], [O.scalar(O.FN_CONST, 1.0)]
+    local, (rp, col, _), vals = _run_product(ctx, grid, fns, ten)
     nb = local.neighbors[:, local.own_begin:local.own_end]
     full = (nb >= 0).all(axis=0)[: (local.n_own // 64) * 64].reshape(-1, 64).all(axis=1)
     assert full.sum() >= 50 and not full.all(), "expected mostly full tiles and some boundary tiles"
     og = O.Grid(et, coords, ev)
-    orp, ocol, oval = O.assemble(og, ofn, oten, O.params())
-    assert np.array_equal(rp, orp) and np.array_equal(col, ocol)
-    worst, ok = compare_rows(rp, val, oval, RTOL)
-    assert ok, worst
+    for ofn, val in zip(ofns, vals):
+        orp, ocol, oval = O.assemble(og, ofn, oten, O.params())
+        assert np.array_equal(rp, orp) and np.array_equal(col, ocol)
+        worst, ok = compare_rows(rp, val, oval, RTOL)
+        assert ok, worst
 
 
 @pytest.mark.parametrize("case", ["kuhn_spe10", "quad_spe10", "kuhn_sinusoid_sym", "quad_sinusoid", "nvb", "scrambled"])
