@@ -411,20 +411,27 @@ def test_scrambled_quad_orientations(ctx, smooth):
 
 
 @pytest.mark.parametrize("coef", ["const", "per_elem_sym", "sinusoid", "os2014_two"])
-def test_scrambled_simplex_full_tiles(ctx, coef):
-    """P1 full interior tiles (64 elements with three interior faces: P1PwcPolicy's branch-free compute_full with its
-    static image layout) under a random element numbering and a random vertex order per triangle (rotations and
-    reflections): the row blocks' neighbour order, sorted by id, takes every permutation and the twin-face ids every
-    value.  Interior elements first (shuffled), then the boundary elements (shuffled), so most tiles are full."""
+@pytest.mark.parametrize("et", [H.SIMPLEX, H.CUBE])
+def test_scrambled_numbering_full_tiles(ctx, et, coef):
+    """Full interior tiles under a random element numbering and a random vertex order per element -- P1: the
+    branch-free compute_full of P1PwcPolicy with its static image layout; Q1: the rotated (padded) image of the
+    half-image kernel (rotations and reflections of the reference element, Dune vertex order kept valid): the row
+    blocks' neighbour order, sorted by id, takes every permutation and the twin-face ids every value.  Interior
+    elements first (shuffled), then the boundary elements (shuffled), so most tiles are full."""
     torch = _torch()
-    et, coords, ev = O.kuhn_grid(48, 40, (0, 0), (3, 2))
+    simplex = et == H.SIMPLEX
+    et, coords, ev = (O.kuhn_grid if simplex else O.cube_grid)(48, 40, (0, 0), (3, 2))
     rng = np.random.default_rng(11)
-    edges = np.sort(np.stack([ev[:, [0, 1]], ev[:, [0, 2]], ev[:, [1, 2]]], 1), axis=2).reshape(-1, 2)
+    sides = [[0, 1], [0, 2], [1, 2]] if simplex else [[0, 1], [2, 3], [0, 2], [1, 3]]
+    edges = np.sort(np.stack([ev[:, e] for e in sides], 1), axis=2).reshape(-1, 2)
     _, inv, cnt = np.unique(edges, axis=0, return_inverse=True, return_counts=True)
-    bnd = (cnt[inv.reshape(-1)].reshape(-1, 3) == 1).any(axis=1)
+    bnd = (cnt[inv.reshape(-1)].reshape(-1, len(sides)) == 1).any(axis=1)
     order = np.concatenate([rng.permutation(np.flatnonzero(~bnd)), rng.permutation(np.flatnonzero(bnd))])
-    perms = np.array([[0, 1, 2], [1, 2, 0], [2, 0, 1], [0, 2, 1], [2, 1, 0], [1, 0, 2]])
-    ev = np.ascontiguousarray(np.take_along_axis(ev[order], perms[rng.integers(0, 6, len(order))], 1)).astype(np.int32)
+    perms = np.array([[0, 1, 2], [1, 2, 0], [2, 0, 1], [0, 2, 1], [2, 1, 0], [1, 0, 2]] if simplex else
+                     [[0, 1, 2, 3], [1, 3, 0, 2], [3, 2, 1, 0], [2, 0, 3, 1],     # the square's rotations
+                      [1, 0, 3, 2], [2, 3, 0, 1], [0, 2, 1, 3], [3, 1, 2, 0]])    # and reflections
+    pick = perms[rng.integers(0, len(perms), len(order))]
+    ev = np.ascontiguousarray(np.take_along_axis(ev[order], pick, 1)).astype(np.int32)
     grid = H.Grid.from_connectivity(et, coords, ev)
     ne = ev.shape[0]
     ten, oten = H.tensor_fn(), O.tensor(O.TENSOR_CONST)
@@ -447,7 +454,7 @@ def test_scrambled_simplex_full_tiles(ctx, coef):
     local, (rp, col, _), vals = _run_product(ctx, grid, fns, ten)
     nb = local.neighbors[:, local.own_begin:local.own_end]
     full = (nb >= 0).all(axis=0)[: (local.n_own // 64) * 64].reshape(-1, 64).all(axis=1)
-    assert full.sum() >= 50 and not full.all(), "expected mostly full tiles and some boundary tiles"
+    assert full.sum() >= len(full) - 4 and not full.all(), "expected mostly full tiles and some boundary tiles"
     og = O.Grid(et, coords, ev)
     for ofn, val in zip(ofns, vals):
         orp, ocol, oval = O.assemble(og, ofn, oten, O.params())
