@@ -16,7 +16,8 @@ from cases import compare_rows
 
 H = pytest.importorskip("hdd_amd")
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-EXE = os.path.join(ROOT, "examples", "bin", "surface_main")
+# HDD_EXAMPLES_BIN: another build of the examples, e.g. examples/bin_asan (make -C dune-hdd_amd asan)
+EXE = os.path.join(os.environ.get("HDD_EXAMPLES_BIN") or os.path.join(ROOT, "examples", "bin"), "surface_main")
 
 
 def test_surface_example_is_built():

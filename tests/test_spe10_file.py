@@ -15,7 +15,8 @@ import pytest
 import hdd_amd as H
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-EXE = os.path.join(ROOT, "examples", "bin", "problems_main")
+# HDD_EXAMPLES_BIN: another build of the examples, e.g. examples/bin_asan (make -C dune-hdd_amd asan)
+EXE = os.path.join(os.environ.get("HDD_EXAMPLES_BIN") or os.path.join(ROOT, "examples", "bin"), "problems_main")
 
 
 def _write_model1(path, values, per_line=6):
